@@ -1,0 +1,409 @@
+/*
+ * mgdp_oracle.c -- CPU ORACLE for the Minigrid step / value-iteration hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+ * may load this library, and only as the checker (or the timed CPU baseline).  The product path
+ * (minigrid_dynamicprogramming_amd/) never links, imports or calls it.
+ *
+ * A plain-C restatement of the reference's semantics.  Parity is PINNED: tests/test_oracle_golden.py
+ * checks every function below against golden vectors captured from the reference itself
+ * (tests/golden/make_golden.py drives /root/reference through an offline gymnasium shim).
+ *
+ *   orc_xyd_next / orc_doorkey_next   MiniGridEnv.step transition       minigrid/minigrid_env.py:520-583
+ *                                       front_pos / DIR_TO_VEC           minigrid/minigrid_env.py:392-419,
+ *                                                                        minigrid/core/constants.py:49-58
+ *                                       cell predicates                  minigrid/core/world_object.py:46-64,
+ *                                                                        :114,129,142,165,178-195,244,266,278-294
+ *   orc_vi                            Jacobi value iteration (build-defined, DESIGN.md "A9"; the
+ *                                     reference has no DP code -- SURVEY.md section 0)
+ *   orc_step / orc_gen_obs            step() + gen_obs()                 minigrid/minigrid_env.py:520-645,
+ *                                       Grid.slice/rotate_left/encode/process_vis
+ *                                                                        minigrid/core/grid.py:110-143,244-328
+ *   orc_reward                        _reward()                         minigrid/minigrid_env.py:235-240
+ *
+ * Build: oracle/Makefile (gcc -O3 -ffp-contract=off).  Floating point is evaluated without
+ * contraction so fp32 and fp64 results are bit-identical to the HIP kernels (also built with
+ * -ffp-contract=off) for the same operation order.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* OBJECT_TO_IDX, minigrid/core/constants.py:25-37 */
+enum { T_UNSEEN = 0, T_EMPTY = 1, T_WALL = 2, T_FLOOR = 3, T_DOOR = 4, T_KEY = 5, T_BALL = 6,
+       T_BOX = 7, T_GOAL = 8, T_LAVA = 9, T_AGENT = 10 };
+/* COLOR_TO_IDX grey = 5, constants.py:20 ; door STATE_TO_IDX open 0 closed 1 locked 2, :42-46 */
+enum { C_GREY = 5 };
+enum { D_OPEN = 0, D_CLOSED = 1, D_LOCKED = 2 };
+
+/* DIR_TO_VEC, constants.py:49-58: 0 +x, 1 +y, 2 -x, 3 -y */
+static const int DX[4] = {1, 0, -1, 0};
+static const int DY[4] = {0, 1, 0, -1};
+
+int orc_abi_version(void) { return 1; }
+
+/* ------------------------------------------------------------------------------------------- */
+/* DP models (A9).  cells = H*W OBJECT_TO_IDX codes, row-major y*W+x (grid.py:72,78).           */
+/* ------------------------------------------------------------------------------------------- */
+
+static int xyd_free(int t) { return t == T_EMPTY || t == T_FLOOR; }
+
+/* Agent-state validity of the XYD model: the agent stands on an empty/floor cell.  Goal, lava,
+ * wall cells are absorbing V = 0 states. */
+int orc_xyd_valid(const uint8_t *cells, int W, int H, int s) {
+    int c = s >> 2;
+    if (c < 0 || c >= W * H) return 0;
+    return xyd_free(cells[c]);
+}
+
+/* One transition of the XYD model (Empty / FourRooms / LavaCrossing: cells in {empty, wall, floor,
+ * goal, lava}).  Mirrors MiniGridEnv.step, minigrid_env.py:536-553: left/right rotate, forward moves
+ * iff the front cell is None or can_overlap (goal/floor/lava), goal -> terminated with reward,
+ * lava -> terminated with 0; pickup/drop/toggle/done are no-ops on these cell types.
+ * Reward is the stationary surrogate R = 1 on entering the goal.
+ * Returns 0 for an absorbing s (no transition), 1 otherwise. */
+int orc_xyd_next(const uint8_t *cells, int W, int H, int s, int a, int *sp, double *r, int *done) {
+    if (!orc_xyd_valid(cells, W, H, s)) return 0;
+    int c = s >> 2, d = s & 3, x = c % W, y = c / W;
+    *r = 0.0;
+    *done = 0;
+    *sp = s;
+    if (a == 0) {            /* left, minigrid_env.py:536-539 */
+        *sp = c * 4 + ((d + 3) & 3);
+    } else if (a == 1) {     /* right, :542-543 */
+        *sp = c * 4 + ((d + 1) & 3);
+    } else if (a == 2) {     /* forward, :546-553 */
+        int nx = x + DX[d], ny = y + DY[d];
+        if (nx < 0 || ny < 0 || nx >= W || ny >= H) return 1; /* reference asserts; treated as blocked */
+        int t = cells[ny * W + nx];
+        if (t == T_EMPTY || t == T_FLOOR || t == T_GOAL || t == T_LAVA) *sp = (ny * W + nx) * 4 + d;
+        if (t == T_GOAL) { *done = 1; *r = 1.0; }
+        if (t == T_LAVA) { *done = 1; }
+    }
+    /* a = 3..6: pickup/drop/toggle/done change nothing on these cell types */
+    return 1;
+}
+
+/* DoorKey product model: s = (((y*W+x)*4+dir)*2+has_key)*2+door_open.  The grid holds exactly one
+ * door (locked at reset) and one key of the door's colour.  Action lanes 0..4 = env actions
+ * left, right, forward, pickup, toggle (doorkey.py:25-33; drop excluded).
+ * door_open = 0 is "locked" (reset config); with has_key = 1 closed and locked doors behave alike.
+ * Cell walkable: empty/floor; door iff open; key cell iff the key has been picked up. */
+static int dk_walk(int t, int hk, int dopen) {
+    return t == T_EMPTY || t == T_FLOOR || (t == T_DOOR && dopen) || (t == T_KEY && hk);
+}
+
+int orc_doorkey_valid(const uint8_t *cells, int W, int H, int s) {
+    int c = s >> 4;
+    if (c < 0 || c >= W * H) return 0;
+    return dk_walk(cells[c], (s >> 1) & 1, s & 1);
+}
+
+int orc_doorkey_next(const uint8_t *cells, int W, int H, int s, int a, int *sp, double *r, int *done) {
+    if (!orc_doorkey_valid(cells, W, H, s)) return 0;
+    int dopen = s & 1, hk = (s >> 1) & 1, d = (s >> 2) & 3, c = s >> 4;
+    int x = c % W, y = c / W;
+    int nx = x + DX[d], ny = y + DY[d];
+    int ft = (nx < 0 || ny < 0 || nx >= W || ny >= H) ? T_WALL : cells[ny * W + nx];
+    *r = 0.0;
+    *done = 0;
+    *sp = s;
+    if (a == 0) {
+        *sp = (((c * 4 + ((d + 3) & 3)) * 2 + hk) * 2) + dopen;
+    } else if (a == 1) {
+        *sp = (((c * 4 + ((d + 1) & 3)) * 2 + hk) * 2) + dopen;
+    } else if (a == 2) {     /* forward: can_overlap = goal, floor, lava, open door (+ empty) */
+        if (dk_walk(ft, hk, dopen) || ft == T_GOAL || ft == T_LAVA)
+            *sp = ((((ny * W + nx) * 4 + d) * 2 + hk) * 2) + dopen;
+        if (ft == T_GOAL) { *done = 1; *r = 1.0; }
+        if (ft == T_LAVA) { *done = 1; }
+    } else if (a == 3) {     /* pickup, minigrid_env.py:556-561: Key.can_pickup, world_object.py:244 */
+        if (ft == T_KEY && !hk) *sp = (((c * 4 + d) * 2 + 1) * 2) + dopen;
+    } else if (a == 4) {     /* toggle -> Door.toggle, world_object.py:185-195 */
+        if (ft == T_DOOR) {
+            if (dopen) *sp = (((c * 4 + d) * 2 + hk) * 2) + 0;
+            else if (hk) *sp = (((c * 4 + d) * 2 + hk) * 2) + 1;
+        }
+    }
+    return 1;
+}
+
+typedef int (*next_fn)(const uint8_t *, int, int, int, int, int *, double *, int *);
+
+/* Transition table of one env: nxt[s*A+a] (-1 for absorbing s), rew, done. */
+int orc_build_table(int model, int W, int H, const uint8_t *cells, int32_t *nxt, double *rew,
+                    uint8_t *done) {
+    int A = model == 0 ? 7 : 5;
+    int S = W * H * (model == 0 ? 4 : 16);
+    next_fn fn = model == 0 ? orc_xyd_next : orc_doorkey_next;
+    for (int s = 0; s < S; ++s) {
+        for (int a = 0; a < A; ++a) {
+            int sp, dn;
+            double r;
+            if (fn(cells, W, H, s, a, &sp, &r, &dn)) {
+                nxt[s * A + a] = sp;
+                rew[s * A + a] = r;
+                done[s * A + a] = (uint8_t)dn;
+            } else {
+                nxt[s * A + a] = -1;
+                rew[s * A + a] = 0.0;
+                done[s * A + a] = 0;
+            }
+        }
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------- */
+/* Jacobi value iteration over B independent envs with ONE global stopping rule (A9):           */
+/*   Qd[s,a] = done ? R : R + g*V[s']          (R = 0 whenever done = 0, so this is g*V[s'])    */
+/*   slip:   Q[s,a] = p*Qd[s,a] + c*(((((Qd0+Qd1)+Qd2)+Qd3)+Qd4)+Qd5),  c = (T)((1-p)/6)        */
+/*           (StochasticActionWrapper, minigrid/wrappers.py:775-796: keep a w.p. p, else        */
+/*            integers(0, 6) uniform over actions 0..5)                                          */
+/*   V_{k+1}[s] = max_a Q (lowest index wins exact ties), pi = argmax; absorbing s: V=0, pi=-1  */
+/*   stop after sweep k when max over all envs/states |V_k - V_{k-1}| < tol; V_0 = 0            */
+/* T = float (fp32) or double (fp64); no FP contraction.                                         */
+/* ------------------------------------------------------------------------------------------- */
+#define DEFINE_VI(T, NAME)                                                                        \
+    static int NAME(int model, int B, int W, int H, const uint8_t *cells, double gamma, double tol, \
+                    double slip_p, int max_sweeps, int nthreads, T *V, int8_t *pi, int *sweeps_out, \
+                    double *dv_trace, double *dv_last) {                                          \
+        const int A = model == 0 ? 7 : 5;                                                         \
+        const int S = W * H * (model == 0 ? 4 : 16);                                              \
+        const long long BS = (long long)B * S;                                                    \
+        const int slip = slip_p >= 0.0;                                                           \
+        if (slip && model != 0) return -3;                                                        \
+        int32_t *nxt = (int32_t *)malloc(sizeof(int32_t) * BS * A);                               \
+        double *rew = (double *)malloc(sizeof(double) * BS * A);                                  \
+        uint8_t *dn = (uint8_t *)malloc(BS * A);                                                  \
+        T *Vn = (T *)malloc(sizeof(T) * BS);                                                      \
+        if (!nxt || !rew || !dn || !Vn) { free(nxt); free(rew); free(dn); free(Vn); return -2; }  \
+        for (int b = 0; b < B; ++b)                                                               \
+            orc_build_table(model, W, H, cells + (long long)b * W * H, nxt + (long long)b * S * A, \
+                            rew + (long long)b * S * A, dn + (long long)b * S * A);               \
+        const T g = (T)gamma, p = (T)slip_p, cc = (T)((1.0 - slip_p) / 6.0);                      \
+        for (long long i = 0; i < BS; ++i) V[i] = (T)0;                                           \
+        int k = 0;                                                                                \
+        double dv = 0.0;                                                                          \
+        (void)nthreads;                                                                           \
+        while (1) {                                                                               \
+            ++k;                                                                                  \
+            double dvk = 0.0;                                                                     \
+            _Pragma("omp parallel for reduction(max : dvk) num_threads(nthreads) schedule(static)") \
+            for (long long i = 0; i < BS; ++i) {                                                  \
+                const long long b = i / S;                                                        \
+                const int32_t *nx = nxt + i * A;                                                  \
+                if (nx[0] < 0) { Vn[i] = (T)0; pi[i] = -1; continue; }                            \
+                const T *Vb = V + b * S;                                                          \
+                T qd[7];                                                                          \
+                for (int a = 0; a < A; ++a) {                                                     \
+                    const T r = (T)rew[i * A + a];                                                \
+                    qd[a] = dn[i * A + a] ? r : (T)(r + g * Vb[nx[a]]);                           \
+                }                                                                                 \
+                T best = 0;                                                                       \
+                int arg = 0;                                                                      \
+                if (slip) {                                                                       \
+                    T s6 = qd[0] + qd[1];                                                         \
+                    s6 = s6 + qd[2];                                                              \
+                    s6 = s6 + qd[3];                                                              \
+                    s6 = s6 + qd[4];                                                              \
+                    s6 = s6 + qd[5];                                                              \
+                    const T tail = cc * s6;                                                       \
+                    for (int a = 0; a < A; ++a) {                                                 \
+                        const T q = (T)(p * qd[a]) + tail;                                        \
+                        if (a == 0 || q > best) { best = q; arg = a; }                            \
+                    }                                                                             \
+                } else {                                                                          \
+                    for (int a = 0; a < A; ++a)                                                   \
+                        if (a == 0 || qd[a] > best) { best = qd[a]; arg = a; }                    \
+                }                                                                                 \
+                Vn[i] = best;                                                                     \
+                pi[i] = (int8_t)arg;                                                              \
+                const T diff = best > V[i] ? best - V[i] : V[i] - best;                           \
+                if ((double)diff > dvk) dvk = (double)diff;                                       \
+            }                                                                                     \
+            memcpy(V, Vn, sizeof(T) * BS);                                                        \
+            if (dv_trace) dv_trace[k - 1] = dvk;                                                  \
+            dv = dvk;                                                                             \
+            if (dvk < tol || k >= max_sweeps) break;                                              \
+        }                                                                                         \
+        *sweeps_out = k;                                                                          \
+        if (dv_last) *dv_last = dv;                                                               \
+        free(nxt); free(rew); free(dn); free(Vn);                                                 \
+        return 0;                                                                                 \
+    }
+
+DEFINE_VI(float, vi_f32)
+DEFINE_VI(double, vi_f64)
+
+/* dtype: 0 = fp32 (V is float*), 1 = fp64 (V is double*).  slip_p < 0 -> deterministic.
+ * dv_trace must hold max_sweeps doubles (or be NULL).  Returns 0 on success. */
+int orc_vi(int model, int dtype, int B, int W, int H, const uint8_t *cells, double gamma, double tol,
+           double slip_p, int max_sweeps, int nthreads, void *V, int8_t *pi, int *sweeps,
+           double *dv_trace, double *dv_last) {
+    if (model != 0 && model != 1) return -1;
+    if (B <= 0 || W < 3 || H < 3 || max_sweeps <= 0) return -1;
+    if (nthreads <= 0) nthreads = 1;
+    if (dtype == 0)
+        return vi_f32(model, B, W, H, cells, gamma, tol, slip_p, max_sweeps, nthreads, (float *)V, pi,
+                      sweeps, dv_trace, dv_last);
+    return vi_f64(model, B, W, H, cells, gamma, tol, slip_p, max_sweeps, nthreads, (double *)V, pi,
+                  sweeps, dv_trace, dv_last);
+}
+
+/* ------------------------------------------------------------------------------------------- */
+/* step() + gen_obs() restatement over (type, color, state) planes, row-major y*W+x.           */
+/* ------------------------------------------------------------------------------------------- */
+typedef struct { uint8_t t, c, s; } cell_t;
+
+static cell_t cell_at(const uint8_t *ty, const uint8_t *co, const uint8_t *st, int W, int H, int x,
+                      int y) {
+    cell_t v;
+    if (x < 0 || y < 0 || x >= W || y >= H) { /* Grid.slice: out of bounds -> Wall(), grid.py:136-139 */
+        v.t = T_WALL; v.c = C_GREY; v.s = 0;
+        return v;
+    }
+    int i = y * W + x;
+    v.t = ty[i]; v.c = co[i]; v.s = st[i];
+    return v;
+}
+
+/* see_behind: Wall false (world_object.py:165), Door iff open (:182-183), all else true. */
+static int see_behind(cell_t v) {
+    if (v.t == T_WALL) return 0;
+    if (v.t == T_DOOR) return v.s == D_OPEN;
+    return 1;
+}
+
+/* gen_obs_grid + encode, minigrid_env.py:592-645, restated step by step. vs = agent_view_size. */
+void orc_gen_obs(int W, int H, const uint8_t *ty, const uint8_t *co, const uint8_t *st, int ax, int ay,
+                 int adir, int carry_t, int carry_c, int see_through, int vs, uint8_t *image) {
+    cell_t g[2][32 * 32];
+    int cur = 0;
+    int topX, topY; /* get_view_exts, minigrid_env.py:448-479 */
+    if (adir == 0) { topX = ax; topY = ay - vs / 2; }
+    else if (adir == 1) { topX = ax - vs / 2; topY = ay; }
+    else if (adir == 2) { topX = ax - vs + 1; topY = ay - vs / 2; }
+    else { topX = ax - vs / 2; topY = ay - vs + 1; }
+    /* Grid.slice, grid.py:124-143 */
+    for (int j = 0; j < vs; ++j)
+        for (int i = 0; i < vs; ++i) g[cur][j * vs + i] = cell_at(ty, co, st, W, H, topX + i, topY + j);
+    /* rotate_left (agent_dir + 1) times, minigrid_env.py:606-607, grid.py:110-122 (square view) */
+    for (int r = 0; r < adir + 1; ++r) {
+        int nxt = cur ^ 1;
+        for (int i = 0; i < vs; ++i)
+            for (int j = 0; j < vs; ++j) g[nxt][(vs - 1 - i) * vs + j] = g[cur][j * vs + i];
+        cur = nxt;
+    }
+    cell_t *v = g[cur];
+    uint8_t mask[32 * 32];
+    /* process_vis, grid.py:291-328; mask is indexed [i][j] like the reference (x-major) */
+    if (!see_through) {
+        memset(mask, 0, sizeof(mask));
+        int apx = vs / 2, apy = vs - 1;
+        mask[apx * vs + apy] = 1;
+        for (int j = vs - 1; j >= 0; --j) {
+            for (int i = 0; i < vs - 1; ++i) {
+                if (!mask[i * vs + j]) continue;
+                cell_t cl = v[j * vs + i];
+                if (cl.t != T_EMPTY && !see_behind(cl)) continue;
+                mask[(i + 1) * vs + j] = 1;
+                if (j > 0) { mask[(i + 1) * vs + j - 1] = 1; mask[i * vs + j - 1] = 1; }
+            }
+            for (int i = vs - 1; i >= 1; --i) {
+                if (!mask[i * vs + j]) continue;
+                cell_t cl = v[j * vs + i];
+                if (cl.t != T_EMPTY && !see_behind(cl)) continue;
+                mask[(i - 1) * vs + j] = 1;
+                if (j > 0) { mask[(i - 1) * vs + j - 1] = 1; mask[i * vs + j - 1] = 1; }
+            }
+        }
+        /* process_vis clears invisible cells (grid.py:323-326); encode masks them anyway */
+    } else {
+        memset(mask, 1, sizeof(mask));
+    }
+    /* carried object (or None) at the agent's view position, minigrid_env.py:621-625 */
+    cell_t ac;
+    if (carry_t > 0) { ac.t = (uint8_t)carry_t; ac.c = (uint8_t)carry_c; ac.s = 0; }
+    else { ac.t = T_EMPTY; ac.c = 0; ac.s = 0; }
+    v[(vs - 1) * vs + vs / 2] = ac;
+    /* Grid.encode, grid.py:244-268: image[i][j][3], None -> (empty,0,0), hidden -> (0,0,0) */
+    for (int i = 0; i < vs; ++i)
+        for (int j = 0; j < vs; ++j) {
+            uint8_t *o = image + (i * vs + j) * 3;
+            if (mask[i * vs + j]) {
+                cell_t cl = v[j * vs + i];
+                if (cl.t == T_EMPTY) { o[0] = T_EMPTY; o[1] = 0; o[2] = 0; }
+                else { o[0] = cl.t; o[1] = cl.c; o[2] = cl.s; }
+            } else {
+                o[0] = 0; o[1] = 0; o[2] = 0;
+            }
+        }
+}
+
+/* _reward, minigrid_env.py:235-240: 1 - 0.9 * (step_count / max_steps) in fp64. */
+double orc_reward(int step_count, int max_steps) {
+    double q = (double)step_count / (double)max_steps;
+    double t = 0.9 * q;
+    return 1.0 - t;
+}
+
+/* MiniGridEnv.step, minigrid_env.py:520-590.  Mutates the planes / agent / carry in place.
+ * state[4] = {x, y, dir, step_count}; carry[2] = {type, color} (type 0 = nothing).
+ * Box contents are not modelled: toggling a Box leaves an empty cell (Box(contains=None)).
+ * Returns 0, or -1 for an unknown action (after step_count += 1, as the reference does), or -2
+ * when the front cell is outside the grid (the reference's Grid.get assertion). */
+int orc_step(int W, int H, uint8_t *ty, uint8_t *co, uint8_t *st, int32_t *state, int32_t *carry,
+             int max_steps, int see_through, int vs, int action, uint8_t *image, double *reward,
+             int *terminated, int *truncated) {
+    int ax = state[0], ay = state[1], d = state[2];
+    state[3] += 1;
+    *reward = 0.0;
+    *terminated = 0;
+    *truncated = 0;
+    if (action < 0 || action > 6) return -1;
+    int fx = ax + DX[d], fy = ay + DY[d];
+    if (fx < 0 || fy < 0 || fx >= W || fy >= H) return -2;
+    int fi = fy * W + fx;
+    int ft = ty[fi];
+    int fnone = ft == T_EMPTY;
+    if (action == 0) {
+        state[2] = (d + 3) & 3;
+    } else if (action == 1) {
+        state[2] = (d + 1) & 3;
+    } else if (action == 2) {
+        int overlap = ft == T_GOAL || ft == T_FLOOR || ft == T_LAVA || (ft == T_DOOR && st[fi] == D_OPEN);
+        if (fnone || overlap) { state[0] = fx; state[1] = fy; }
+        if (ft == T_GOAL) { *terminated = 1; *reward = orc_reward(state[3], max_steps); }
+        if (ft == T_LAVA) { *terminated = 1; }
+    } else if (action == 3) {
+        if (ft == T_KEY || ft == T_BALL || ft == T_BOX) {
+            if (carry[0] == 0) {
+                carry[0] = ft; carry[1] = co[fi];
+                ty[fi] = T_EMPTY; co[fi] = 0; st[fi] = 0;
+            }
+        }
+    } else if (action == 4) {
+        if (fnone && carry[0] != 0) {
+            ty[fi] = (uint8_t)carry[0]; co[fi] = (uint8_t)carry[1]; st[fi] = 0;
+            carry[0] = 0; carry[1] = 0;
+        }
+    } else if (action == 5) {
+        if (ft == T_DOOR) {
+            if (st[fi] == D_LOCKED) {
+                if (carry[0] == T_KEY && carry[1] == co[fi]) st[fi] = D_OPEN;
+            } else {
+                st[fi] = st[fi] == D_OPEN ? D_CLOSED : D_OPEN;
+            }
+        } else if (ft == T_BOX) {
+            ty[fi] = T_EMPTY; co[fi] = 0; st[fi] = 0;
+        }
+    }
+    if (state[3] >= max_steps) *truncated = 1;
+    orc_gen_obs(W, H, ty, co, st, state[0], state[1], state[2], carry[0], carry[1], see_through, vs, image);
+    return 0;
+}

@@ -1,0 +1,93 @@
+"""Pin the CPU oracle (oracle/) to golden vectors captured from the reference itself.
+
+Transition tables were extracted by driving the reference MiniGridEnv.step()
+(minigrid/minigrid_env.py:520-590) from every enumerated state; trajectories are 256-step rollouts
+of the reference env; V*/pi*/sweeps come from an independent numpy Jacobi over those tables.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle
+from tests.golden_util import SEE_THROUGH, cells_from_enc, load, table_names, traj_names
+
+
+@pytest.mark.parametrize("name", table_names())
+def test_transition_table_matches_reference(name):
+    t = load(f"table_{name}.npz")
+    model = int(t["model"])
+    nxt, rew, done = oracle.build_table(model, cells_from_enc(t["enc"]))
+    np.testing.assert_array_equal(nxt, t["nxt"])
+    np.testing.assert_array_equal(done, t["done"])
+    np.testing.assert_array_equal(rew, t["rew"])
+
+
+@pytest.mark.parametrize("name", table_names())
+def test_vi_fp64_matches_golden(name):
+    t = load(f"table_{name}.npz")
+    model = int(t["model"])
+    res = oracle.value_iteration(model, cells_from_enc(t["enc"]), 0.99, 1e-6, dtype="f64")
+    assert res["sweeps"] == int(t["sweeps"])
+    np.testing.assert_array_equal(res["pi"][0], t["pi"])
+    np.testing.assert_allclose(res["V"][0], t["V"], rtol=0, atol=1e-12)
+    if model == 0:
+        rs = oracle.value_iteration(model, cells_from_enc(t["enc"]), 0.99, 1e-6, slip_p=0.9, dtype="f64")
+        assert rs["sweeps"] == int(t["sweeps_slip"])
+        np.testing.assert_array_equal(rs["pi"][0], t["pi_slip"])
+        np.testing.assert_allclose(rs["V"][0], t["V_slip"], rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("name", table_names())
+def test_vi_fp32_within_tolerance(name):
+    t = load(f"table_{name}.npz")
+    model = int(t["model"])
+    res = oracle.value_iteration(model, cells_from_enc(t["enc"]), 0.99, 1e-6, dtype="f32")
+    assert res["sweeps"] == int(t["sweeps"])  # deterministic envs converge to dv == 0 exactly
+    np.testing.assert_allclose(res["V"][0], t["V"], rtol=0, atol=1e-6)
+    np.testing.assert_array_equal(res["pi"][0], t["pi"])
+
+
+def test_known_answer_empty16():
+    # analytic KAT: V*(start) = gamma^(k-1), k = 27 actions from (1,1,dir 0) to the goal at (14,14)
+    t = load("table_empty16_s0.npz")
+    res = oracle.value_iteration(0, cells_from_enc(t["enc"]))
+    s0 = (1 * 16 + 1) * 4 + 0
+    assert res["V"][0, s0] == pytest.approx(0.99 ** 26, abs=1e-12)
+    assert res["sweeps"] == 29
+
+
+def test_batched_vi_global_rule():
+    names = ["fourrooms_s0", "fourrooms_s1", "fourrooms_s2", "fourrooms_s3"]
+    tabs = [load(f"table_{n}.npz") for n in names]
+    cells = np.stack([cells_from_enc(t["enc"]) for t in tabs])
+    res = oracle.value_iteration(0, cells)
+    assert res["sweeps"] == max(int(t["sweeps"]) for t in tabs)
+    for b, t in enumerate(tabs):
+        np.testing.assert_allclose(res["V"][b], t["V"], atol=1e-12)
+
+
+@pytest.mark.parametrize("name", traj_names())
+def test_step_trajectory_matches_reference(name):
+    t = load(f"traj_{name}.npz")
+    for k in range(t["actions"].shape[0]):
+        env = oracle.OracleEnv(t["init_enc"][k], t["init_agent"][k], int(t["max_steps"][k]),
+                               SEE_THROUGH.get(name, False))
+        np.testing.assert_array_equal(env.obs(), t["init_image"][k])
+        for i, a in enumerate(t["actions"][k]):
+            img, r, te, tr = env.step(int(a))
+            ctx = f"{name} traj {k} step {i} action {a}"
+            np.testing.assert_array_equal(img, t["image"][k, i], err_msg=ctx)
+            assert r == t["reward"][k, i], ctx
+            assert te == bool(t["terminated"][k, i]), ctx
+            assert tr == bool(t["truncated"][k, i]), ctx
+            assert tuple(env.state[:3]) == tuple(t["agent"][k, i]), ctx
+            assert tuple(env.carry) == tuple(t["carry"][k, i]), ctx
+            assert env.state[3] == t["step_count"][k, i], ctx
+        np.testing.assert_array_equal(env.encode(), t["final_enc"][k])
+
+
+def test_unknown_action_raises():
+    t = load("traj_empty5.npz")
+    env = oracle.OracleEnv(t["init_enc"][0], t["init_agent"][0], 100, True)
+    with pytest.raises(ValueError):
+        env.step(7)
+    assert env.state[3] == 1  # step_count is incremented before the raise (minigrid_env.py:523,579)
