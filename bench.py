@@ -1,0 +1,293 @@
+#!/usr/bin/env python3
+"""Benchmark: state-action Bellman updates/s + sweeps-to-converge (BASELINE.json metric).
+
+One "step" = one complete value-iteration solve of the workload on every rank: V_0 = 0, Jacobi
+sweeps until the global rule max|V_k - V_{k-1}| < tol (gamma = 0.99, tol = 1e-6), policy
+extraction, sweep count returned to the host.  Inputs (grid cells) are resident in HBM before the
+timed region.  value = (sum over ranks of B_r * S * A * sweeps) * steps / max-over-ranks time.
+
+Workloads; default = BASELINE configs[1]:
+  empty16        MiniGrid-Empty-16x16-v0, 1 grid per GPU (N > 1: replicas only)
+  empty16x65536  Empty-16x16 x 65536 replicas per GPU (SURVEY 8(d) "R", the HBM-roofline sizing)
+  fourrooms4096  MiniGrid-FourRooms-v0, 4096 seeds per GPU
+  lava65536      MiniGrid-LavaCrossingS11N5-v0, 65536 seeds sharded over N GPUs (RCCL dV all-reduce)
+  doorkey65536   MiniGrid-DoorKey-16x16-v0 (pos, dir, has_key, door_open), 65536 seeds sharded
+
+Run:  python bench.py [--gpus N --steps K --warmup W --workload NAME --method fused|sweep ...]
+      N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "state-action Bellman updates/sec + DP sweeps-to-converge, Empty-16x16"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s peak
+
+WORKLOADS = {
+    "empty16": dict(env_id="MiniGrid-Empty-16x16-v0", per_gpu=1, replicate=True, sharded=False),
+    "empty16x65536": dict(env_id="MiniGrid-Empty-16x16-v0", per_gpu=65536, replicate=True, sharded=False),
+    "fourrooms4096": dict(env_id="MiniGrid-FourRooms-v0", per_gpu=4096, replicate=False, sharded=False),
+    "lava65536": dict(env_id="MiniGrid-LavaCrossingS11N5-v0", global_grids=65536, replicate=False, sharded=True),
+    "doorkey65536": dict(env_id="MiniGrid-DoorKey-16x16-v0", global_grids=65536, replicate=False, sharded=True),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def algorithmic_bytes_per_update(tsize: int, A: int) -> float:
+    """read V'[s'] (sizeof V) + 1 B cell type + write V[s] amortised over A."""
+    return tsize + 1 + tsize / A
+
+
+def compulsory_bytes_per_sweep(S: int, HW: int, tsize: int) -> int:
+    """2*S*sizeof(V) + W*H per grid-sweep (read V once, write V once, read cells)."""
+    return 2 * S * tsize + HW
+
+
+def make_cells(spec, rank, world):
+    from minigrid_dynamicprogramming_amd import make
+    from minigrid_dynamicprogramming_amd.distributed import shard_range
+
+    env = make(spec["env_id"])
+    if spec.get("sharded"):
+        lo, hi = shard_range(spec["global_grids"], rank, world)
+    else:
+        lo, hi = rank * spec["per_gpu"], (rank + 1) * spec["per_gpu"]
+    if spec.get("replicate"):
+        enc, _ = env.generate(seed=0)
+        one = np.ascontiguousarray(enc[..., 0].T)
+        return np.broadcast_to(one, (hi - lo,) + one.shape).copy(), (lo, hi)
+    cells = np.empty((hi - lo, env.height, env.width), np.uint8)
+    for i, s in enumerate(range(lo, hi)):
+        enc, _ = env.generate(seed=s)
+        cells[i] = enc[..., 0].T
+    return cells, (lo, hi)
+
+
+def cpu_baseline(cells, model, gamma, tol, dtype, budget_s=8.0, nthreads=1):
+    """Time the oracle (oracle/, a C restatement of the same algorithm) on a bounded sample."""
+    from oracle import oracle
+
+    model_id = 0 if model == "xyd" else 1
+    sample = cells[: min(len(cells), 32)]
+    S = sample.shape[1] * sample.shape[2] * (4 if model_id == 0 else 16)
+    A = 7 if model_id == 0 else 5
+    updates = 0
+    solves = 0
+    t0 = time.perf_counter()
+    while True:
+        r = oracle.value_iteration(model_id, sample, gamma, tol, dtype=dtype, nthreads=nthreads)
+        updates += len(sample) * S * A * r["sweeps"]
+        solves += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": updates / el, "unit": "updates/s", "cores": nthreads, "kind": "port",
+            "sample": f"{solves} full solves of {len(sample)} grid(s) of the same workload "
+                      f"({r['sweeps']} sweeps each, {dtype}), oracle/mgdp_oracle.c, {el:.1f} s"}
+
+
+def load_traffic(key):
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    v = d.get(key)
+    return None if v is None else v.get("bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="empty16", choices=sorted(WORKLOADS))
+    ap.add_argument("--method", default="fused", choices=["fused", "sweep"])
+    ap.add_argument("--mapping", default="cell", choices=["cell", "sa"])
+    ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
+    ap.add_argument("--gamma", type=float, default=0.99)
+    ap.add_argument("--tol", type=float, default=1e-6)
+    ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of CPU baseline sampling")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-hbm", action="store_true", help="skip the HBM-roofline side measurement")
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import minigrid_dynamicprogramming_amd as mg
+    from minigrid_dynamicprogramming_amd.distributed import solve_sharded
+
+    spec = WORKLOADS[args.workload]
+    t_gen = time.perf_counter()
+    cells, (lo, hi) = make_cells(spec, rank, world)
+    log(f"[rank {rank}] {args.workload}: grids [{lo},{hi}) generated in {time.perf_counter() - t_gen:.1f}s")
+    vi = mg.ValueIteration(cells, gamma=args.gamma, tol=args.tol, dtype=args.dtype, method=args.method,
+                           mapping=args.mapping, device=local)
+    sharded = spec["sharded"] and world > 1
+
+    def one_solve():
+        if sharded:
+            return solve_sharded(vi)["sweeps"]
+        return vi.solve()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        one_solve()
+    vi.enable_timing(True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sweeps = []
+    for _ in range(args.steps):
+        sweeps.append(one_solve())
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms, launches = vi.kernel_time()
+    vi.enable_timing(False)
+
+    A = 7 if vi.model == "xyd" else 5
+    upd_rank = float(vi.updates_per_sweep) * float(sum(sweeps))
+    if dist is not None:
+        t = torch.tensor([elapsed, upd_rank], dtype=torch.float64, device="cuda")
+        tmax = t[0:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        usum = t[1:2].clone()
+        dist.all_reduce(usum, op=dist.ReduceOp.SUM)
+        elapsed_max, upd_total = float(tmax.item()), float(usum.item())
+    else:
+        elapsed_max, upd_total = elapsed, upd_rank
+
+    if rank != 0:
+        vi.close()
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    tsize = 4 if args.dtype == "f32" else 8
+    bpu = algorithmic_bytes_per_update(tsize, A)
+    HW = vi.W * vi.H
+    bytes_alg = upd_rank * bpu
+    avg_launch_s = (kern_ms / 1000.0) / max(launches, 1)
+    achieved = bytes_alg / max(launches, 1) / avg_launch_s / 1e9 if launches else 0.0
+    comp_bytes = compulsory_bytes_per_sweep(vi.S, HW, tsize) * vi.B * (sum(sweeps))
+    kernel_name = "vi_fused_kernel" if args.method == "fused" else "vi_sweep_kernel"
+    key = f"{args.workload}/{args.method}/{args.mapping}/{args.dtype}"
+    roofline = {
+        "bound": "hbm", "kernel": kernel_name,
+        "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+        "traffic": load_traffic(key),
+        "launches": launches, "avg_launch_us": avg_launch_s * 1e6,
+        "alg_bytes_per_launch": bytes_alg / max(launches, 1),
+        "alg_bytes_per_update": bpu,
+        "compulsory_gbs": comp_bytes / max(launches, 1) / avg_launch_s / 1e9 if launches else 0.0,
+        "note": ("algorithmic bytes per SURVEY 8(d): (sizeof V + 1 + sizeof V / A) per (s,a) update; "
+                 "compulsory = 2*S*sizeof V + W*H per grid-sweep"),
+    }
+    if args.workload == "empty16":
+        roofline["regime"] = ("single 8 KiB grid on one workgroup: latency/LDS bound, HBM-roofline fraction "
+                              "is not meaningful here (SURVEY 8(d) caveats); see roofline_hbm")
+    out = {
+        "metric": METRIC,
+        "value": upd_total / elapsed_max,
+        "unit": "updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed_max * 1000.0 / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong" if spec["sharded"] else "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": f"synthetic: {spec['env_id']} grids from the reference-exact host generator "
+                f"({'seed 0 replicated' if spec['replicate'] else 'seeds ' + str(lo) + '..'})",
+        "config": {
+            "workload": args.workload, "env_id": spec["env_id"], "grids_per_gpu": hi - lo,
+            "global_grids": (hi - lo) * world if not spec["sharded"] else spec["global_grids"],
+            "states_per_grid": vi.S, "actions": A, "gamma": args.gamma, "tol": args.tol,
+            "method": args.method, "mapping": args.mapping,
+            "parallelism": (f"shard{world} + RCCL dV all-reduce" if sharded else
+                            ("replicas only" if spec["replicate"] else f"independent batches x{world}")),
+        },
+        "sweeps": int(sweeps[-1]),
+        "roofline": roofline,
+    }
+    vi.close()
+
+    if world == 1 and not args.no_hbm and args.workload == "empty16":
+        out["roofline_hbm"] = hbm_side_measurement(args)
+    if world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(cells, vi.model, args.gamma, args.tol, args.dtype, args.cpu_budget)
+        out["cpu_baseline_all_cores"] = cpu_baseline(
+            cells, vi.model, args.gamma, args.tol, args.dtype, max(2.0, args.cpu_budget / 4),
+            nthreads=min(16, os.cpu_count() or 1))
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def hbm_side_measurement(args, n_solves=3):
+    """Per-sweep HBM kernel on SURVEY 8(d) config R (Empty-16x16 x 65536, 537 MB of V > MALL)."""
+    import torch
+
+    import minigrid_dynamicprogramming_amd as mg
+
+    cells, _ = make_cells(WORKLOADS["empty16x65536"], 0, 1)
+    res = {}
+    for method in ("sweep", "fused"):
+        vi = mg.ValueIteration(cells, gamma=args.gamma, tol=args.tol, dtype=args.dtype, method=method,
+                               mapping=args.mapping)
+        vi.solve()
+        vi.enable_timing(True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ks = [vi.solve() for _ in range(n_solves)]
+        el = time.perf_counter() - t0
+        ms, n = vi.kernel_time()
+        tsize = 4 if args.dtype == "f32" else 8
+        upd = vi.updates_per_sweep * sum(ks)
+        bpu = algorithmic_bytes_per_update(tsize, 7)
+        avg = ms / 1000.0 / max(n, 1)
+        ach = upd * bpu / max(n, 1) / avg / 1e9
+        comp = compulsory_bytes_per_sweep(vi.S, vi.W * vi.H, tsize) * vi.B * sum(ks) / max(n, 1) / avg / 1e9
+        res[method] = {"kernel": "vi_sweep_kernel" if method == "sweep" else "vi_fused_kernel",
+                       "updates_per_s": upd / el, "sweeps": ks[-1], "launches": n, "avg_launch_us": avg * 1e6,
+                       "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                       "compulsory_gbs": comp, "compulsory_frac": comp / HBM_PEAK_GBS,
+                       "traffic": load_traffic(f"empty16x65536/{method}/{args.mapping}/{args.dtype}")}
+        vi.close()
+    res["workload"] = "empty16x65536"
+    return res
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,174 @@
+/*
+ * mgdp.h -- C ABI of the MI355X Minigrid step / value-iteration engine (libmgdp.so).
+ *
+ * The reference (Farama Minigrid 2.3.1, /root/reference) is pure Python: its operator surface is
+ * the gymnasium.Env plugin MiniGridEnv (minigrid/minigrid_env.py:24) registered under the
+ * "gymnasium.envs" entry point (pyproject.toml:47-48 -> minigrid/__init__.py:23).  This header is
+ * the native boundary behind that surface.  Each entry point cites the reference interface it
+ * replaces.  The reference has no value-iteration code; the mgdp_vi_* entry
+ * points implement the build-defined DP of DESIGN.md "A9" whose transition is the reference step().
+ *
+ * Conventions
+ *   - Plain C types only; no C++ or Python types cross this boundary.
+ *   - Every function returns int: MGDP_OK (0) or a negative MGDP_E_* code; mgdp_last_error()
+ *     returns a thread-local message for the last failure on the calling thread.
+ *   - The caller owns host buffers; the library owns the device buffers of a handle.  Entry points
+ *     named *_device take device pointers and run asynchronously on the handle's stream.
+ *   - A handle is bound to one HIP device and is not thread-safe (like MiniGridEnv,
+ *     tests/test_envs.py:42-43).  Multi-GPU = one process and one handle per GPU.
+ *   - Grid cells use the reference codes OBJECT_TO_IDX / COLOR_TO_IDX / door state
+ *     (minigrid/core/constants.py:20-46).  "cells" arrays are row-major [y][x] like Grid.grid
+ *     (minigrid/core/grid.py:35,72); "enc" arrays are the x-major [x][y][3] layout of
+ *     Grid.encode() (minigrid/core/grid.py:244-268).
+ */
+#ifndef MGDP_H
+#define MGDP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MGDP_ABI_VERSION 1
+
+enum {
+    MGDP_OK = 0,
+    MGDP_E_INVALID = -1,     /* bad argument                             (Python: ValueError)      */
+    MGDP_E_HIP = -2,         /* HIP runtime failure / no device          (Python: RuntimeError)    */
+    MGDP_E_UNSUPPORTED = -3, /* grid contents outside the selected model (Python: ValueError)      */
+    MGDP_E_ACTION = -4,      /* "Unknown action", minigrid_env.py:579-580 (Python: ValueError)      */
+    MGDP_E_BOUNDS = -5,      /* grid access out of range, grid.py:66-77  (Python: AssertionError)  */
+};
+
+/* ---------------------------------------------------------------------------------------------- */
+/* Library                                                                                          */
+/* ---------------------------------------------------------------------------------------------- */
+const char *mgdp_last_error(void);
+int mgdp_abi_version(void);
+/* Number of visible HIP devices (0 when none). */
+int mgdp_device_count(int32_t *n);
+
+/* ---------------------------------------------------------------------------------------------- */
+/* Value iteration over batches of grids (build-defined DP; transition = MiniGridEnv.step,          */
+/* minigrid_env.py:520-583).  DESIGN.md "A9" fixes every convention:                                */
+/*   MGDP_MODEL_XYD      s = (y*W + x)*4 + dir, A = 7 (Discrete(7), minigrid_env.py:63);             */
+/*                       cells in {empty, wall, floor, goal, lava} (Empty/FourRooms/LavaCrossing)   */
+/*   MGDP_MODEL_DOORKEY  s = (((y*W + x)*4 + dir)*2 + has_key)*2 + door_open, A = 5 lanes            */
+/*                       (left, right, forward, pickup, toggle; doorkey.py:25-33); exactly one       */
+/*                       door and one key of its colour                                             */
+/*   R = 1 on entering the goal (terminal), lava terminal with R = 0; absorbing states V = 0, pi=-1 */
+/*   Jacobi V_{k+1} = max_a Q_k, lowest action index wins ties; stop after sweep k when             */
+/*   max |V_k - V_{k-1}| over all grids of the run < tol (one global rule, also across GPUs).       */
+/*   slip_p >= 0 applies StochasticActionWrapper (wrappers.py:775-796) transition probabilities     */
+/*   (XYD only): Q = p*Qd[a] + ((1-p)/6) * (((((Qd0+Qd1)+Qd2)+Qd3)+Qd4)+Qd5).                       */
+/* ---------------------------------------------------------------------------------------------- */
+enum { MGDP_MODEL_XYD = 0, MGDP_MODEL_DOORKEY = 1 };
+enum { MGDP_F32 = 0, MGDP_F64 = 1 };
+enum {
+    MGDP_METHOD_FUSED = 0, /* LDS-resident: one workgroup per grid runs many sweeps on chip        */
+    MGDP_METHOD_SWEEP = 1, /* one launch per Jacobi sweep, V double-buffered in HBM                */
+};
+enum {
+    MGDP_MAP_CELL = 0, /* one thread per grid cell updates that cell's 4 (or 16) states            */
+    MGDP_MAP_SA = 1,   /* one thread per (state, action), 8 lanes per state, wave max-reduce      */
+};
+
+typedef struct {
+    int32_t model;      /* MGDP_MODEL_*                                                            */
+    int32_t dtype;      /* MGDP_F32 | MGDP_F64: arithmetic and storage type of V                    */
+    int32_t method;     /* MGDP_METHOD_*                                                           */
+    int32_t mapping;    /* MGDP_MAP_*                                                              */
+    int32_t B, W, H;    /* grids in this handle and their size                                     */
+    int32_t max_sweeps; /* hard cap on sweeps                                                      */
+    int32_t device;     /* HIP device ordinal                                                      */
+    int32_t reserved;
+    double gamma;       /* discount                                                                */
+    double tol;         /* stopping threshold on max|V_k - V_{k-1}|                                 */
+    double slip_p;      /* < 0: deterministic; else keep-action probability (XYD only)            */
+} mgdp_vi_desc;
+
+typedef struct mgdp_vi mgdp_vi;
+
+int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out);
+int mgdp_vi_destroy(mgdp_vi *vi);
+/* Launch on this hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL = own stream. */
+int mgdp_vi_set_stream(mgdp_vi *vi, void *hip_stream);
+/* Upload B*H*W row-major OBJECT_TO_IDX cell codes (host).  Validates them against the model:
+ * MGDP_E_UNSUPPORTED if a cell type is outside the model or a border cell is walkable. */
+int mgdp_vi_load_cells(mgdp_vi *vi, const uint8_t *cells);
+/* Same from device memory (already validated by the caller); async on the handle's stream. */
+int mgdp_vi_load_cells_device(mgdp_vi *vi, const uint8_t *d_cells);
+
+/* Whole solve on one device: V_0 = 0, sweeps until the global rule stops.  Synchronous. */
+int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *converged_out);
+
+/* Multi-device protocol (DESIGN.md "convergence across GPUs"): every rank calls
+ *   mgdp_vi_reset -> mgdp_vi_run_local(&k_local) -> all-reduce(MAX) k -> mgdp_vi_run_to(k, &dv)
+ *   -> all-reduce(MAX) dv; while (dv >= tol && k < max_sweeps) { mgdp_vi_sweep(&dv); all-reduce; }
+ *   -> mgdp_vi_finish(k).
+ * Because each grid's Jacobi trajectory is independent of the others, this yields exactly the
+ * V_k of the single global rule; the all-reduces carry one scalar each over RCCL/xGMI. */
+int mgdp_vi_reset(mgdp_vi *vi);
+/* Each grid sweeps until its own max|dV| < tol (or max_sweeps); returns max sweeps over grids. */
+int mgdp_vi_run_local(mgdp_vi *vi, int32_t *k_local_max);
+/* Continue every grid to exactly k_target sweeps; dv_out = max over grids of |dV| at sweep k. */
+int mgdp_vi_run_to(mgdp_vi *vi, int32_t k_target, double *dv_out);
+/* One more Jacobi sweep of every grid (all at the same sweep index); dv_out as above. */
+int mgdp_vi_sweep(mgdp_vi *vi, double *dv_out);
+/* Extract pi from the last sweep and publish sweeps/converged for mgdp_vi_get_*. */
+int mgdp_vi_finish(mgdp_vi *vi, int32_t sweeps);
+
+/* Results (host).  V: B*S of float or double per dtype; pi: B*S int8 (-1 = absorbing state). */
+int mgdp_vi_get_values(mgdp_vi *vi, void *V);
+int mgdp_vi_get_policy(mgdp_vi *vi, int8_t *pi);
+/* Per-sweep global max|dV| (method SWEEP only; fused runs record only the last): n <= max_sweeps */
+int mgdp_vi_get_dv_trace(mgdp_vi *vi, double *trace, int32_t n);
+/* Device pointers of the handle's V (current) and pi buffers, for zero-copy consumers. */
+int mgdp_vi_device_buffers(mgdp_vi *vi, void **d_V, void **d_pi);
+int mgdp_vi_num_states(const mgdp_vi_desc *desc, int64_t *S);
+
+/* HIP-event timing of the dominant kernel (fused solve or sweep), on the stream it runs on. */
+int mgdp_vi_enable_timing(mgdp_vi *vi, int32_t on);
+int mgdp_vi_kernel_time(mgdp_vi *vi, double *total_ms, int64_t *launches);
+
+/* ---------------------------------------------------------------------------------------------- */
+/* Batched env stepping: the gymnasium Env reset()/step() surface (minigrid_env.py:119-157,         */
+/* :520-590, gen_obs :592-645) for B envs resident on one device.                                  */
+/* ---------------------------------------------------------------------------------------------- */
+typedef struct mgdp_envs mgdp_envs;
+
+/* view_size: agent_view_size (odd, 3..7, minigrid_env.py:66-68). */
+int mgdp_envs_create(int32_t device, int32_t B, int32_t W, int32_t H, int32_t view_size,
+                     mgdp_envs **out);
+int mgdp_envs_destroy(mgdp_envs *envs);
+int mgdp_envs_set_stream(mgdp_envs *envs, void *hip_stream);
+/* reset(): upload grids + agent of the envs whose mask byte is 1 (mask NULL = all).
+ * enc: B*W*H*3 x-major (Grid.encode()), agent: B*3 (x, y, dir), max_steps: B,
+ * see_through: B (see_through_walls, minigrid_env.py:41,103).  step_count and carrying reset to 0. */
+int mgdp_envs_load(mgdp_envs *envs, const uint8_t *enc, const int32_t *agent,
+                   const int32_t *max_steps, const uint8_t *see_through, const uint8_t *mask);
+/* gen_obs() of every env without stepping (the reset() observation). obs: B*V*V*3, dir: B. */
+int mgdp_envs_observe(mgdp_envs *envs, uint8_t *obs, int32_t *direction);
+/* step(actions) for all B envs (host buffers).  reward fp64 (_reward, minigrid_env.py:235-240).
+ * Returns MGDP_E_ACTION / MGDP_E_BOUNDS if any env failed; status (B, may be NULL) says which. */
+int mgdp_envs_step(mgdp_envs *envs, const int32_t *actions, uint8_t *obs, int32_t *direction,
+                   double *reward, uint8_t *terminated, uint8_t *truncated, int32_t *status);
+/* Device-pointer variant, asynchronous on the handle's stream; status per env in d_status. */
+int mgdp_envs_step_device(mgdp_envs *envs, const int32_t *d_actions, uint8_t *d_obs,
+                          int32_t *d_direction, double *d_reward, uint8_t *d_terminated,
+                          uint8_t *d_truncated, int32_t *d_status);
+/* Read back env state: enc B*W*H*3 (x-major), agent B*3, carry B*2 (type,color; 0 = none),
+ * step_count B.  Any pointer may be NULL. */
+int mgdp_envs_get_state(mgdp_envs *envs, uint8_t *enc, int32_t *agent, int32_t *carry,
+                        int32_t *step_count);
+/* Overwrite agent (B*3), carry (B*2) and step_count (B) of the masked envs (NULL = unchanged). */
+int mgdp_envs_set_state(mgdp_envs *envs, const int32_t *agent, const int32_t *carry,
+                        const int32_t *step_count, const uint8_t *mask);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MGDP_H */

@@ -1,0 +1,152 @@
+"""ctypes binding of libmgdp.so (include/mgdp.h) -- the only route from Python to the HIP kernels.
+
+There is no CPU fallback: if the library is missing or no GPU is visible, the product raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmgdp.so")
+
+MGDP_OK = 0
+MGDP_E_INVALID = -1
+MGDP_E_HIP = -2
+MGDP_E_UNSUPPORTED = -3
+MGDP_E_ACTION = -4
+MGDP_E_BOUNDS = -5
+
+MODEL_XYD = 0
+MODEL_DOORKEY = 1
+F32 = 0
+F64 = 1
+METHOD_FUSED = 0
+METHOD_SWEEP = 1
+MAP_CELL = 0
+MAP_SA = 1
+
+
+class MgdpError(RuntimeError):
+    pass
+
+
+class ViDesc(ctypes.Structure):
+    _fields_ = [
+        ("model", ctypes.c_int32),
+        ("dtype", ctypes.c_int32),
+        ("method", ctypes.c_int32),
+        ("mapping", ctypes.c_int32),
+        ("B", ctypes.c_int32),
+        ("W", ctypes.c_int32),
+        ("H", ctypes.c_int32),
+        ("max_sweeps", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("gamma", ctypes.c_double),
+        ("tol", ctypes.c_double),
+        ("slip_p", ctypes.c_double),
+    ]
+
+
+# name -> (restype, argtypes); the full export list of include/mgdp.h
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64P = ctypes.POINTER(ctypes.c_int64)
+_I32P = ctypes.POINTER(ctypes.c_int32)
+_DP = ctypes.POINTER(ctypes.c_double)
+SIGNATURES = {
+    "mgdp_last_error": (ctypes.c_char_p, []),
+    "mgdp_abi_version": (ctypes.c_int, []),
+    "mgdp_device_count": (ctypes.c_int, [_I32P]),
+    "mgdp_vi_create": (ctypes.c_int, [ctypes.POINTER(ViDesc), ctypes.POINTER(_P)]),
+    "mgdp_vi_destroy": (ctypes.c_int, [_P]),
+    "mgdp_vi_set_stream": (ctypes.c_int, [_P, _P]),
+    "mgdp_vi_load_cells": (ctypes.c_int, [_P, _P]),
+    "mgdp_vi_load_cells_device": (ctypes.c_int, [_P, _P]),
+    "mgdp_vi_solve": (ctypes.c_int, [_P, _I32P, _DP, _I32P]),
+    "mgdp_vi_reset": (ctypes.c_int, [_P]),
+    "mgdp_vi_run_local": (ctypes.c_int, [_P, _I32P]),
+    "mgdp_vi_run_to": (ctypes.c_int, [_P, _I32, _DP]),
+    "mgdp_vi_sweep": (ctypes.c_int, [_P, _DP]),
+    "mgdp_vi_finish": (ctypes.c_int, [_P, _I32]),
+    "mgdp_vi_get_values": (ctypes.c_int, [_P, _P]),
+    "mgdp_vi_get_policy": (ctypes.c_int, [_P, _P]),
+    "mgdp_vi_get_dv_trace": (ctypes.c_int, [_P, _P, _I32]),
+    "mgdp_vi_device_buffers": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
+    "mgdp_vi_num_states": (ctypes.c_int, [ctypes.POINTER(ViDesc), _I64P]),
+    "mgdp_vi_enable_timing": (ctypes.c_int, [_P, _I32]),
+    "mgdp_vi_kernel_time": (ctypes.c_int, [_P, _DP, _I64P]),
+    "mgdp_envs_create": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, ctypes.POINTER(_P)]),
+    "mgdp_envs_destroy": (ctypes.c_int, [_P]),
+    "mgdp_envs_set_stream": (ctypes.c_int, [_P, _P]),
+    "mgdp_envs_load": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
+    "mgdp_envs_observe": (ctypes.c_int, [_P, _P, _P]),
+    "mgdp_envs_step": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P]),
+    "mgdp_envs_step_device": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P]),
+    "mgdp_envs_get_state": (ctypes.c_int, [_P, _P, _P, _P, _P]),
+    "mgdp_envs_set_state": (ctypes.c_int, [_P, _P, _P, _P, _P]),
+}
+
+_lib = None
+
+
+def lib_path() -> str:
+    return LIB_PATH
+
+
+def load():
+    """Load libmgdp.so (raises if it has not been built; see minigrid_dynamicprogramming_amd.build)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MgdpError(
+            f"{LIB_PATH} is missing: build the HIP library first "
+            "(python -c 'import __graft_entry__ as g; g.build()')")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    if L.mgdp_abi_version() != 1:
+        raise MgdpError("libmgdp ABI version mismatch")
+    _lib = L
+    return L
+
+
+def last_error() -> str:
+    msg = load().mgdp_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str = ""):
+    """Map an MGDP status code to the reference's exception types (include/mgdp.h)."""
+    if rc == MGDP_OK:
+        return
+    msg = last_error() or what
+    if rc in (MGDP_E_INVALID, MGDP_E_UNSUPPORTED, MGDP_E_ACTION):
+        raise ValueError(msg)
+    if rc == MGDP_E_BOUNDS:
+        raise AssertionError(msg)
+    raise MgdpError(f"{what}: {msg} (rc={rc})")
+
+
+def device_count() -> int:
+    n = ctypes.c_int32(0)
+    check(load().mgdp_device_count(ctypes.byref(n)), "mgdp_device_count")
+    return n.value
+
+
+def require_gpu():
+    if device_count() <= 0:
+        raise MgdpError("no HIP device visible: the MI355X engine has no CPU fallback")
+
+
+def ptr(a) -> ctypes.c_void_p:
+    """Pointer of a contiguous numpy array or a torch tensor (host or device)."""
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):
+        return ctypes.c_void_p(a.data_ptr())
+    return a.ctypes.data_as(ctypes.c_void_p)

@@ -1,0 +1,456 @@
+// envs.hip -- batched MiniGridEnv.step / gen_obs on MI355X (gfx950).
+//
+// Restates minigrid/minigrid_env.py:520-590 (step), :592-645 (gen_obs_grid / gen_obs),
+// :448-479 (get_view_exts), :235-240 (_reward); minigrid/core/grid.py:110-143 (rotate_left,
+// slice), :244-268 (encode), :291-328 (process_vis); minigrid/core/world_object.py (cell
+// predicates, Door.toggle :185-195, Box.toggle :291-294).  Pinned by tests/test_gpu_step.py against
+// 256-step trajectories captured from the reference (tests/golden/traj_*.npz).
+//
+// Layout in HBM (B envs of W x H):
+//   ty, co, st  uint8 [B][HWp]   OBJECT_TO_IDX / COLOR_TO_IDX / door state per cell, row-major
+//   agent       int32 [B][4]     x, y, dir, step_count
+//   carry       int32 [B][2]     carried (type, colour); type 0 = nothing
+//   max_steps   int32 [B], see uint8 [B] (see_through_walls)
+// One thread per env.  The V x V view is never materialised: view cell (i, j) maps to world
+// top_left - f*j + r*i (f = DIR_TO_VEC[dir], r = right_vec, minigrid_env.py:421-446), which equals
+// the reference's slice + (dir+1) x rotate_left; process_vis runs on a 64-bit visibility mask.
+// Observations are assembled in LDS and leave with 16-byte coalesced stores.
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+
+namespace mgdp {
+
+__constant__ int kDX[4] = {1, 0, -1, 0};
+__constant__ int kDY[4] = {0, 1, 0, -1};
+
+struct EnvGeo {
+    int B, W, H, HWp, vs;
+};
+
+constexpr int kStepBlock = 64;  // envs per workgroup; obs staging = 64 * 147 B (16-B multiple)
+
+__device__ __forceinline__ bool see_behind(int t, int s) {
+    if (t == T_WALL) return false;
+    if (t == T_DOOR) return s == D_OPEN;
+    return true;
+}
+
+// gen_obs for one env into `img` (vs*vs*3 bytes, x-major [i][j][3]) in LDS.
+__device__ void gen_obs_one(const EnvGeo &g, const uint8_t *ty, const uint8_t *co, const uint8_t *st,
+                            int ax, int ay, int d, int ct, int cc, bool see_through, uint8_t *img) {
+    const int vs = g.vs, hs = vs / 2;
+    const int fx = kDX[d], fy = kDY[d];
+    const int rx = -fy, ry = fx;
+    const int tlx = ax + fx * (vs - 1) - rx * hs;
+    const int tly = ay + fy * (vs - 1) - ry * hs;
+    // see-behind mask, bit (j*8 + i)
+    unsigned long long sb = 0, mask = 0;
+    for (int j = 0; j < vs; ++j)
+        for (int i = 0; i < vs; ++i) {
+            const int wx = tlx - fx * j + rx * i, wy = tly - fy * j + ry * i;
+            bool s = false;  // out of bounds -> Wall (grid.py:136-139)
+            if (wx >= 0 && wy >= 0 && wx < g.W && wy < g.H) {
+                const int idx = wy * g.W + wx;
+                s = see_behind(ty[idx], st[idx]);
+            }
+            if (s) sb |= 1ull << (j * 8 + i);
+        }
+    if (see_through) {
+        mask = ~0ull;
+    } else {  // process_vis, grid.py:291-328, literal loop order
+        mask = 1ull << ((vs - 1) * 8 + hs);
+        for (int j = vs - 1; j >= 0; --j) {
+            for (int i = 0; i < vs - 1; ++i) {
+                const unsigned long long b = 1ull << (j * 8 + i);
+                if (!(mask & b) || !(sb & b)) continue;
+                mask |= b << 1;
+                if (j > 0) mask |= (b << 1 >> 8) | (b >> 8);
+            }
+            for (int i = vs - 1; i >= 1; --i) {
+                const unsigned long long b = 1ull << (j * 8 + i);
+                if (!(mask & b) || !(sb & b)) continue;
+                mask |= b >> 1;
+                if (j > 0) mask |= (b >> 1 >> 8) | (b >> 8);
+            }
+        }
+    }
+    // encode, grid.py:244-268 (None -> (1,0,0), hidden -> (0,0,0)); carried object at (hs, vs-1)
+    for (int i = 0; i < vs; ++i)
+        for (int j = 0; j < vs; ++j) {
+            uint8_t *o = img + (i * vs + j) * 3;
+            int t = 0, c = 0, s = 0;
+            if (mask & (1ull << (j * 8 + i))) {
+                if (i == hs && j == vs - 1) {
+                    if (ct > 0) { t = ct; c = cc; } else { t = T_EMPTY; }
+                } else {
+                    const int wx = tlx - fx * j + rx * i, wy = tly - fy * j + ry * i;
+                    if (wx >= 0 && wy >= 0 && wx < g.W && wy < g.H) {
+                        const int idx = wy * g.W + wx;
+                        t = ty[idx];
+                        if (t != T_EMPTY) { c = co[idx]; s = st[idx]; }
+                    } else {
+                        t = T_WALL; c = C_GREY;
+                    }
+                }
+            }
+            o[0] = (uint8_t)t; o[1] = (uint8_t)c; o[2] = (uint8_t)s;
+        }
+}
+
+__device__ __forceinline__ void copy_out(uint8_t *dst, const uint8_t *src, int bytes) {
+    // dst is 16-B aligned when the block starts at a multiple of kStepBlock envs (147*64 = 9408)
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0 && (bytes & 15) == 0) {
+        const uint4 *s = reinterpret_cast<const uint4 *>(src);
+        uint4 *d = reinterpret_cast<uint4 *>(dst);
+        for (int i = threadIdx.x; i < (bytes >> 4); i += blockDim.x) d[i] = s[i];
+    } else {
+        for (int i = threadIdx.x; i < bytes; i += blockDim.x) dst[i] = src[i];
+    }
+}
+
+// _reward: 1 - 0.9 * (step_count / max_steps), fp64, no contraction (minigrid_env.py:240)
+__device__ __forceinline__ double reward_fn(int sc, int ms) {
+    const double q = (double)sc / (double)ms;
+    const double t = 0.9 * q;
+    return 1.0 - t;
+}
+
+__global__ void __launch_bounds__(kStepBlock)
+envs_step_kernel(EnvGeo g, uint8_t *__restrict__ TY, uint8_t *__restrict__ CO, uint8_t *__restrict__ ST,
+                 int32_t *__restrict__ agent, int32_t *__restrict__ carry,
+                 const int32_t *__restrict__ max_steps, const uint8_t *__restrict__ see,
+                 const int32_t *__restrict__ actions, uint8_t *__restrict__ obs,
+                 int32_t *__restrict__ direction, double *__restrict__ reward,
+                 uint8_t *__restrict__ terminated, uint8_t *__restrict__ truncated,
+                 int32_t *__restrict__ status, int observe_only) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int obs_bytes = g.vs * g.vs * 3;
+    const int e0 = blockIdx.x * kStepBlock;
+    const int e = e0 + threadIdx.x;
+    uint8_t *img = smem + threadIdx.x * obs_bytes;
+    if (e < g.B) {
+        uint8_t *ty = TY + (long long)e * g.HWp;
+        uint8_t *co = CO + (long long)e * g.HWp;
+        uint8_t *st = ST + (long long)e * g.HWp;
+        int x = agent[e * 4 + 0], y = agent[e * 4 + 1], d = agent[e * 4 + 2], sc = agent[e * 4 + 3];
+        int ct = carry[e * 2 + 0], cc = carry[e * 2 + 1];
+        int stat = MGDP_OK;
+        double r = 0.0;
+        int term = 0, trunc = 0;
+        if (!observe_only) {
+            const int a = actions[e];
+            sc += 1;  // minigrid_env.py:523, before the action is validated
+            const int fx = x + kDX[d], fy = y + kDY[d];
+            // Grid.get asserts on the front cell (minigrid_env.py:533) before the action branch
+            if (fx < 0 || fy < 0 || fx >= g.W || fy >= g.H) {
+                stat = MGDP_E_BOUNDS;
+            } else if (a < 0 || a > 6) {
+                stat = MGDP_E_ACTION;
+            } else {
+                const int fi = fy * g.W + fx;
+                const int ft = ty[fi];
+                const bool fnone = ft == T_EMPTY;
+                if (a == 0) {
+                    d = (d + 3) & 3;
+                } else if (a == 1) {
+                    d = (d + 1) & 3;
+                } else if (a == 2) {
+                    const bool overlap = ft == T_GOAL || ft == T_FLOOR || ft == T_LAVA ||
+                                         (ft == T_DOOR && st[fi] == D_OPEN);
+                    if (fnone || overlap) { x = fx; y = fy; }
+                    if (ft == T_GOAL) { term = 1; r = reward_fn(sc, max_steps[e]); }
+                    if (ft == T_LAVA) term = 1;
+                } else if (a == 3) {
+                    if ((ft == T_KEY || ft == T_BALL || ft == T_BOX) && ct == 0) {
+                        ct = ft; cc = co[fi];
+                        ty[fi] = T_EMPTY; co[fi] = 0; st[fi] = 0;
+                    }
+                } else if (a == 4) {
+                    if (fnone && ct != 0) {
+                        ty[fi] = (uint8_t)ct; co[fi] = (uint8_t)cc; st[fi] = 0;
+                        ct = 0; cc = 0;
+                    }
+                } else if (a == 5) {
+                    if (ft == T_DOOR) {
+                        const int s = st[fi];
+                        if (s == D_LOCKED) {
+                            if (ct == T_KEY && cc == co[fi]) st[fi] = D_OPEN;
+                        } else {
+                            st[fi] = s == D_OPEN ? D_CLOSED : D_OPEN;
+                        }
+                    } else if (ft == T_BOX) {  // Box(contains=None).toggle -> empty cell
+                        ty[fi] = T_EMPTY; co[fi] = 0; st[fi] = 0;
+                    }
+                }
+                if (sc >= max_steps[e]) trunc = 1;
+            }
+            agent[e * 4 + 0] = x; agent[e * 4 + 1] = y; agent[e * 4 + 2] = d; agent[e * 4 + 3] = sc;
+            carry[e * 2 + 0] = ct; carry[e * 2 + 1] = cc;
+            reward[e] = r;
+            terminated[e] = (uint8_t)term;
+            truncated[e] = (uint8_t)trunc;
+            status[e] = stat;
+        }
+        if (stat == MGDP_OK) gen_obs_one(g, ty, co, st, x, y, d, ct, cc, see[e] != 0, img);
+        else for (int i = 0; i < obs_bytes; ++i) img[i] = 0;
+        direction[e] = d;
+    }
+    __syncthreads();
+    const int n = min(kStepBlock, g.B - e0);
+    copy_out(obs + (long long)e0 * obs_bytes, smem, n * obs_bytes);
+}
+
+}  // namespace mgdp
+
+using namespace mgdp;
+
+struct mgdp_envs {
+    int device = 0, B = 0, W = 0, H = 0, HW = 0, HWp = 0, vs = 7;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    uint8_t *d_ty = nullptr, *d_co = nullptr, *d_st = nullptr, *d_see = nullptr;
+    int32_t *d_agent = nullptr, *d_carry = nullptr, *d_max = nullptr, *d_act = nullptr, *d_dir = nullptr,
+            *d_status = nullptr;
+    uint8_t *d_obs = nullptr, *d_term = nullptr, *d_trunc = nullptr;
+    double *d_rew = nullptr;
+};
+
+namespace {
+
+EnvGeo env_geo(const mgdp_envs *E) { return EnvGeo{E->B, E->W, E->H, E->HWp, E->vs}; }
+
+int launch_step(mgdp_envs *E, const int32_t *d_act, uint8_t *d_obs, int32_t *d_dir, double *d_rew,
+                uint8_t *d_term, uint8_t *d_trunc, int32_t *d_status, int observe_only) {
+    const int grid = (E->B + kStepBlock - 1) / kStepBlock;
+    const int smem = kStepBlock * E->vs * E->vs * 3;
+    hipLaunchKernelGGL(envs_step_kernel, dim3(grid), dim3(kStepBlock), smem, E->stream, env_geo(E),
+                       E->d_ty, E->d_co, E->d_st, E->d_agent, E->d_carry, E->d_max, E->d_see, d_act,
+                       d_obs, d_dir, d_rew, d_term, d_trunc, d_status, observe_only);
+    MGDP_HIP(hipGetLastError());
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mgdp_envs_create(int32_t device, int32_t B, int32_t W, int32_t H, int32_t view_size, mgdp_envs **out) {
+    MGDP_CHECK(out, MGDP_E_INVALID, "null argument");
+    MGDP_CHECK(B > 0 && W >= 3 && H >= 3, MGDP_E_INVALID, "bad shape B=%d W=%d H=%d", B, W, H);
+    MGDP_CHECK(view_size >= 3 && view_size <= 7 && (view_size & 1), MGDP_E_INVALID,
+               "agent_view_size must be odd and in [3, 7] (got %d)", view_size);
+    int ndev = 0;
+    MGDP_HIP(hipGetDeviceCount(&ndev));
+    MGDP_CHECK(device >= 0 && device < ndev, MGDP_E_HIP, "device %d not available (%d visible)", device, ndev);
+    DeviceGuard guard(device);
+    mgdp_envs *E = new mgdp_envs();
+    E->device = device; E->B = B; E->W = W; E->H = H; E->HW = W * H; E->HWp = (int)round_up(W * H, 16);
+    E->vs = view_size;
+    const size_t P = (size_t)B * E->HWp;
+    hipError_t e = hipSuccess;
+    auto al = [&](void **p, size_t n) { if (e == hipSuccess) e = hipMalloc(p, n); };
+    al((void **)&E->d_ty, P); al((void **)&E->d_co, P); al((void **)&E->d_st, P);
+    al((void **)&E->d_see, B);
+    al((void **)&E->d_agent, sizeof(int32_t) * 4 * B);
+    al((void **)&E->d_carry, sizeof(int32_t) * 2 * B);
+    al((void **)&E->d_max, sizeof(int32_t) * B);
+    al((void **)&E->d_act, sizeof(int32_t) * B);
+    al((void **)&E->d_dir, sizeof(int32_t) * B);
+    al((void **)&E->d_status, sizeof(int32_t) * B);
+    al((void **)&E->d_obs, (size_t)B * view_size * view_size * 3);
+    al((void **)&E->d_term, B); al((void **)&E->d_trunc, B);
+    al((void **)&E->d_rew, sizeof(double) * B);
+    if (e == hipSuccess) { e = hipStreamCreateWithFlags(&E->stream, hipStreamNonBlocking); E->own_stream = e == hipSuccess; }
+    if (e == hipSuccess) e = hipMemset(E->d_ty, T_WALL, P);
+    if (e == hipSuccess) e = hipMemset(E->d_co, C_GREY, P);
+    if (e == hipSuccess) e = hipMemset(E->d_st, 0, P);
+    if (e == hipSuccess) e = hipMemset(E->d_agent, 0, sizeof(int32_t) * 4 * B);
+    if (e == hipSuccess) e = hipMemset(E->d_carry, 0, sizeof(int32_t) * 2 * B);
+    if (e != hipSuccess) {
+        mgdp_envs_destroy(E);
+        return hip_fail(e, "mgdp_envs_create allocation", __FILE__, __LINE__);
+    }
+    *out = E;
+    return 0;
+}
+
+int mgdp_envs_destroy(mgdp_envs *E) {
+    if (!E) return 0;
+    DeviceGuard guard(E->device);
+    if (E->stream) (void)hipStreamSynchronize(E->stream);
+    void *ps[] = {E->d_ty, E->d_co, E->d_st, E->d_see, E->d_agent, E->d_carry, E->d_max, E->d_act,
+                  E->d_dir, E->d_status, E->d_obs, E->d_term, E->d_trunc, E->d_rew};
+    for (void *p : ps) (void)hipFree(p);
+    if (E->own_stream) (void)hipStreamDestroy(E->stream);
+    delete E;
+    return 0;
+}
+
+int mgdp_envs_set_stream(mgdp_envs *E, void *s) {
+    MGDP_CHECK(E, MGDP_E_INVALID, "null handle");
+    DeviceGuard guard(E->device);
+    MGDP_HIP(hipStreamSynchronize(E->stream));
+    if (E->own_stream) { (void)hipStreamDestroy(E->stream); E->own_stream = false; E->stream = nullptr; }
+    if (s) E->stream = (hipStream_t)s;
+    else { MGDP_HIP(hipStreamCreateWithFlags(&E->stream, hipStreamNonBlocking)); E->own_stream = true; }
+    return 0;
+}
+
+int mgdp_envs_load(mgdp_envs *E, const uint8_t *enc, const int32_t *agent, const int32_t *max_steps,
+                   const uint8_t *see_through, const uint8_t *mask) {
+    MGDP_CHECK(E && enc && agent && max_steps && see_through, MGDP_E_INVALID, "null argument");
+    DeviceGuard guard(E->device);
+    const int B = E->B, W = E->W, H = E->H, HWp = E->HWp;
+    for (int b = 0; b < B; ++b) {
+        if (mask && !mask[b]) continue;
+        MGDP_CHECK(max_steps[b] > 0, MGDP_E_INVALID, "env %d: max_steps must be > 0", b);
+        const int x = agent[3 * b], y = agent[3 * b + 1], d = agent[3 * b + 2];
+        MGDP_CHECK(x >= 0 && y >= 0 && x < W && y < H && d >= 0 && d < 4, MGDP_E_BOUNDS,
+                   "env %d: agent (%d,%d,%d) outside the grid", b, x, y, d);
+    }
+    // x-major (W,H,3) -> row-major planes
+    std::vector<uint8_t> ty((size_t)B * HWp, T_WALL), co((size_t)B * HWp, C_GREY), st((size_t)B * HWp, 0);
+    std::vector<int32_t> ag((size_t)B * 4), cr((size_t)B * 2, 0);
+    for (int b = 0; b < B; ++b) {
+        if (mask && !mask[b]) continue;
+        const uint8_t *eb = enc + (size_t)b * W * H * 3;
+        for (int x = 0; x < W; ++x)
+            for (int y = 0; y < H; ++y) {
+                const uint8_t *c = eb + (x * H + y) * 3;
+                const size_t i = (size_t)b * HWp + y * W + x;
+                ty[i] = c[0];
+                co[i] = c[0] == T_EMPTY ? 0 : c[1];
+                st[i] = c[0] == T_EMPTY ? 0 : c[2];
+            }
+        ag[4 * b] = agent[3 * b]; ag[4 * b + 1] = agent[3 * b + 1]; ag[4 * b + 2] = agent[3 * b + 2]; ag[4 * b + 3] = 0;
+    }
+    std::vector<int32_t> ms(max_steps, max_steps + B);
+    std::vector<uint8_t> se(see_through, see_through + B);
+    if (!mask) {
+        MGDP_HIP(hipMemcpyAsync(E->d_ty, ty.data(), ty.size(), hipMemcpyHostToDevice, E->stream));
+        MGDP_HIP(hipMemcpyAsync(E->d_co, co.data(), co.size(), hipMemcpyHostToDevice, E->stream));
+        MGDP_HIP(hipMemcpyAsync(E->d_st, st.data(), st.size(), hipMemcpyHostToDevice, E->stream));
+        MGDP_HIP(hipMemcpyAsync(E->d_agent, ag.data(), ag.size() * 4, hipMemcpyHostToDevice, E->stream));
+        MGDP_HIP(hipMemcpyAsync(E->d_carry, cr.data(), cr.size() * 4, hipMemcpyHostToDevice, E->stream));
+        MGDP_HIP(hipMemcpyAsync(E->d_max, ms.data(), ms.size() * 4, hipMemcpyHostToDevice, E->stream));
+        MGDP_HIP(hipMemcpyAsync(E->d_see, se.data(), se.size(), hipMemcpyHostToDevice, E->stream));
+    } else {
+        for (int b = 0; b < B; ++b) {
+            if (!mask[b]) continue;
+            const size_t o = (size_t)b * HWp;
+            MGDP_HIP(hipMemcpyAsync(E->d_ty + o, &ty[o], HWp, hipMemcpyHostToDevice, E->stream));
+            MGDP_HIP(hipMemcpyAsync(E->d_co + o, &co[o], HWp, hipMemcpyHostToDevice, E->stream));
+            MGDP_HIP(hipMemcpyAsync(E->d_st + o, &st[o], HWp, hipMemcpyHostToDevice, E->stream));
+            MGDP_HIP(hipMemcpyAsync(E->d_agent + 4 * b, &ag[4 * b], 16, hipMemcpyHostToDevice, E->stream));
+            MGDP_HIP(hipMemcpyAsync(E->d_carry + 2 * b, &cr[2 * b], 8, hipMemcpyHostToDevice, E->stream));
+            MGDP_HIP(hipMemcpyAsync(E->d_max + b, &ms[b], 4, hipMemcpyHostToDevice, E->stream));
+            MGDP_HIP(hipMemcpyAsync(E->d_see + b, &se[b], 1, hipMemcpyHostToDevice, E->stream));
+        }
+    }
+    MGDP_HIP(hipStreamSynchronize(E->stream));
+    return 0;
+}
+
+int mgdp_envs_observe(mgdp_envs *E, uint8_t *obs, int32_t *direction) {
+    MGDP_CHECK(E && obs, MGDP_E_INVALID, "null argument");
+    DeviceGuard guard(E->device);
+    if (int rc = launch_step(E, nullptr, E->d_obs, E->d_dir, E->d_rew, E->d_term, E->d_trunc, E->d_status, 1)) return rc;
+    const size_t ob = (size_t)E->B * E->vs * E->vs * 3;
+    MGDP_HIP(hipMemcpyAsync(obs, E->d_obs, ob, hipMemcpyDeviceToHost, E->stream));
+    if (direction) MGDP_HIP(hipMemcpyAsync(direction, E->d_dir, 4 * (size_t)E->B, hipMemcpyDeviceToHost, E->stream));
+    MGDP_HIP(hipStreamSynchronize(E->stream));
+    return 0;
+}
+
+int mgdp_envs_step_device(mgdp_envs *E, const int32_t *d_actions, uint8_t *d_obs, int32_t *d_direction,
+                          double *d_reward, uint8_t *d_terminated, uint8_t *d_truncated, int32_t *d_status) {
+    MGDP_CHECK(E && d_actions && d_obs && d_direction && d_reward && d_terminated && d_truncated && d_status,
+               MGDP_E_INVALID, "null argument");
+    DeviceGuard guard(E->device);
+    return launch_step(E, d_actions, d_obs, d_direction, d_reward, d_terminated, d_truncated, d_status, 0);
+}
+
+int mgdp_envs_step(mgdp_envs *E, const int32_t *actions, uint8_t *obs, int32_t *direction, double *reward,
+                   uint8_t *terminated, uint8_t *truncated, int32_t *status) {
+    MGDP_CHECK(E && actions, MGDP_E_INVALID, "null argument");
+    DeviceGuard guard(E->device);
+    const size_t B = E->B;
+    MGDP_HIP(hipMemcpyAsync(E->d_act, actions, 4 * B, hipMemcpyHostToDevice, E->stream));
+    if (int rc = launch_step(E, E->d_act, E->d_obs, E->d_dir, E->d_rew, E->d_term, E->d_trunc, E->d_status, 0)) return rc;
+    std::vector<int32_t> st_local;
+    int32_t *stat = status;
+    if (!stat) { st_local.resize(B); stat = st_local.data(); }
+    if (obs) MGDP_HIP(hipMemcpyAsync(obs, E->d_obs, B * E->vs * E->vs * 3, hipMemcpyDeviceToHost, E->stream));
+    if (direction) MGDP_HIP(hipMemcpyAsync(direction, E->d_dir, 4 * B, hipMemcpyDeviceToHost, E->stream));
+    if (reward) MGDP_HIP(hipMemcpyAsync(reward, E->d_rew, 8 * B, hipMemcpyDeviceToHost, E->stream));
+    if (terminated) MGDP_HIP(hipMemcpyAsync(terminated, E->d_term, B, hipMemcpyDeviceToHost, E->stream));
+    if (truncated) MGDP_HIP(hipMemcpyAsync(truncated, E->d_trunc, B, hipMemcpyDeviceToHost, E->stream));
+    MGDP_HIP(hipMemcpyAsync(stat, E->d_status, 4 * B, hipMemcpyDeviceToHost, E->stream));
+    MGDP_HIP(hipStreamSynchronize(E->stream));
+    for (size_t b = 0; b < B; ++b) {
+        if (stat[b] == MGDP_E_ACTION) { set_error("Unknown action: %d (env %zu)", actions[b], b); return MGDP_E_ACTION; }
+        if (stat[b] == MGDP_E_BOUNDS) { set_error("env %zu: front cell outside the grid", b); return MGDP_E_BOUNDS; }
+    }
+    return 0;
+}
+
+int mgdp_envs_get_state(mgdp_envs *E, uint8_t *enc, int32_t *agent, int32_t *carry, int32_t *step_count) {
+    MGDP_CHECK(E, MGDP_E_INVALID, "null handle");
+    DeviceGuard guard(E->device);
+    const int B = E->B, W = E->W, H = E->H, HWp = E->HWp;
+    std::vector<int32_t> ag((size_t)B * 4);
+    MGDP_HIP(hipMemcpyAsync(ag.data(), E->d_agent, ag.size() * 4, hipMemcpyDeviceToHost, E->stream));
+    if (carry) MGDP_HIP(hipMemcpyAsync(carry, E->d_carry, 8 * (size_t)B, hipMemcpyDeviceToHost, E->stream));
+    std::vector<uint8_t> ty, co, st;
+    if (enc) {
+        ty.resize((size_t)B * HWp); co.resize(ty.size()); st.resize(ty.size());
+        MGDP_HIP(hipMemcpyAsync(ty.data(), E->d_ty, ty.size(), hipMemcpyDeviceToHost, E->stream));
+        MGDP_HIP(hipMemcpyAsync(co.data(), E->d_co, co.size(), hipMemcpyDeviceToHost, E->stream));
+        MGDP_HIP(hipMemcpyAsync(st.data(), E->d_st, st.size(), hipMemcpyDeviceToHost, E->stream));
+    }
+    MGDP_HIP(hipStreamSynchronize(E->stream));
+    for (int b = 0; b < B; ++b) {
+        if (agent) { agent[3 * b] = ag[4 * b]; agent[3 * b + 1] = ag[4 * b + 1]; agent[3 * b + 2] = ag[4 * b + 2]; }
+        if (step_count) step_count[b] = ag[4 * b + 3];
+        if (enc) {
+            uint8_t *eb = enc + (size_t)b * W * H * 3;
+            for (int x = 0; x < W; ++x)
+                for (int y = 0; y < H; ++y) {
+                    const size_t i = (size_t)b * HWp + y * W + x;
+                    uint8_t *c = eb + (x * H + y) * 3;
+                    c[0] = ty[i]; c[1] = co[i]; c[2] = st[i];
+                }
+        }
+    }
+    return 0;
+}
+
+int mgdp_envs_set_state(mgdp_envs *E, const int32_t *agent, const int32_t *carry, const int32_t *step_count,
+                        const uint8_t *mask) {
+    MGDP_CHECK(E, MGDP_E_INVALID, "null handle");
+    DeviceGuard guard(E->device);
+    const int B = E->B;
+    std::vector<int32_t> ag((size_t)B * 4), cr((size_t)B * 2);
+    MGDP_HIP(hipMemcpyAsync(ag.data(), E->d_agent, ag.size() * 4, hipMemcpyDeviceToHost, E->stream));
+    MGDP_HIP(hipMemcpyAsync(cr.data(), E->d_carry, cr.size() * 4, hipMemcpyDeviceToHost, E->stream));
+    MGDP_HIP(hipStreamSynchronize(E->stream));
+    for (int b = 0; b < B; ++b) {
+        if (mask && !mask[b]) continue;
+        if (agent) {
+            MGDP_CHECK(agent[3 * b] >= 0 && agent[3 * b] < E->W && agent[3 * b + 1] >= 0 && agent[3 * b + 1] < E->H &&
+                           agent[3 * b + 2] >= 0 && agent[3 * b + 2] < 4,
+                       MGDP_E_BOUNDS, "env %d: agent outside the grid", b);
+            ag[4 * b] = agent[3 * b]; ag[4 * b + 1] = agent[3 * b + 1]; ag[4 * b + 2] = agent[3 * b + 2];
+        }
+        if (step_count) ag[4 * b + 3] = step_count[b];
+        if (carry) { cr[2 * b] = carry[2 * b]; cr[2 * b + 1] = carry[2 * b + 1]; }
+    }
+    MGDP_HIP(hipMemcpyAsync(E->d_agent, ag.data(), ag.size() * 4, hipMemcpyHostToDevice, E->stream));
+    MGDP_HIP(hipMemcpyAsync(E->d_carry, cr.data(), cr.size() * 4, hipMemcpyHostToDevice, E->stream));
+    MGDP_HIP(hipStreamSynchronize(E->stream));
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,1017 @@
+// vi.hip -- Jacobi value iteration over batches of Minigrid grids on MI355X (gfx950).
+//
+// DP semantics (DESIGN.md "A9"): the transition is MiniGridEnv.step, minigrid/minigrid_env.py:520-583
+// (front_pos :392-419, DIR_TO_VEC minigrid/core/constants.py:49-58, cell predicates
+// minigrid/core/world_object.py:46-64,114,129,142,165,178-195,244); the value-iteration rule is
+// build-defined because the reference has none.  The CPU oracle
+// (oracle/mgdp_oracle.c) states the same arithmetic in the same order; both are compiled with
+// -ffp-contract=off so fp32 and fp64 results agree bit for bit.
+//
+// Data layout in HBM (one handle = B grids of W x H on one device):
+//   cells  uint8  [B][HWp]      OBJECT_TO_IDX per cell, row-major y*W+x, padded to 16 B per grid
+//   V      T      [2][B][S]     value double-buffer (fused method uses buffer 0 in place)
+//   pi     int8   [B][S]        greedy action of the last sweep (-1 = absorbing state)
+//   kenv   int32  [B], dvenv f64 [B]   sweeps done / last max|dV| per grid (fused method)
+//   shards u64    [max_sweeps][8]      per-sweep global max|dV| as f64 bits (sweep method),
+//                                      8 atomic shards (blockIdx & 7) to spread contention
+//
+// Kernels
+//   vi_fused_kernel   one workgroup per grid: cells + both V buffers + pi live in LDS for the
+//                     whole solve; many sweeps per launch, one __syncthreads per sweep.
+//   vi_sweep_kernel   one Jacobi sweep of every grid: per grid, V'[grid] is staged HBM->LDS with
+//                     16-B coalesced loads, updated from LDS, written back LDS->HBM.
+//   vi_reduce_kernel  max over grids of (kenv, dvenv).
+// Thread mappings (template MAP): MGDP_MAP_CELL = one thread per cell updating its 4 (XYD) or
+// 16 (DoorKey) states from 16-B LDS vectors; MGDP_MAP_SA = one thread per (state, action),
+// 8 lanes per state, wave shuffle max-reduce with the lowest action index winning ties.
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+
+namespace mgdp {
+
+struct Geo {
+    int B, W, H, HW, HWp, S;
+    int off[4];  // cell offset of the front cell for dir 0..3 (+x, +y, -x, -y)
+    int max_sweeps;
+    double tol;
+};
+
+template <typename T>
+struct Coef {
+    T g, p, c;  // gamma, slip keep-prob, (1-p)/6   (all rounded to T once on the host)
+};
+
+template <typename T>
+struct alignas(4 * sizeof(T)) V4 {
+    T v[4];
+};
+
+__device__ __forceinline__ bool xyd_free(int t) { return t == T_EMPTY || t == T_FLOOR; }
+__device__ __forceinline__ bool dk_walk(int t, int hk, int dop) {
+    return t == T_EMPTY || t == T_FLOOR || (t == T_DOOR && dop) || (t == T_KEY && hk);
+}
+
+template <typename T>
+__device__ __forceinline__ T tmax(T a, T b) { return a > b ? a : b; }
+template <typename T>
+__device__ __forceinline__ T tabs_diff(T a, T b) { return a > b ? a - b : b - a; }
+
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = tmax(v, (T)__shfl_xor(v, o));
+    return v;
+}
+
+// Block-wide max with ONE barrier; slots = [2][16] alternating by parity so that consecutive
+// calls never race (a slot set is rewritten only after every thread passed the next barrier).
+template <typename T>
+__device__ __forceinline__ T block_max(T v, T *slots, int parity) {
+    v = wave_max(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) slots[parity * 16 + w] = v;
+    __syncthreads();
+    const int nw = blockDim.x >> 6;
+    T m = slots[parity * 16];
+    for (int i = 1; i < nw; ++i) m = tmax(m, slots[parity * 16 + i]);
+    return m;
+}
+
+// ------------------------------------------------------------------------------------------------
+// One cell of the XYD model (4 states, actions 0..6).  Returns max |dV| over the cell's states.
+// Q_det: left/right/self (= pickup/drop/toggle/done) = g*V, forward per minigrid_env.py:546-553.
+// ------------------------------------------------------------------------------------------------
+template <typename T, bool SLIP, bool WRITE_V>
+__device__ __forceinline__ T xyd_cell(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
+                                      const T *Vin, T *Vout, int8_t *pis, int c) {
+    const int t = cl[c];
+    if (!xyd_free(t)) {
+        if (WRITE_V) *reinterpret_cast<V4<T> *>(Vout + c * 4) = V4<T>{{(T)0, (T)0, (T)0, (T)0}};
+        *reinterpret_cast<int32_t *>(pis + c * 4) = -1;
+        return (T)0;
+    }
+    const V4<T> own = *reinterpret_cast<const V4<T> *>(Vin + c * 4);
+    T gv[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) gv[d] = cf.g * own.v[d];
+    V4<T> out;
+    uint32_t pk = 0;
+    T dv = (T)0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const int cfr = c + geo.off[d];
+        const int tf = cl[cfr];
+        T qF;
+        if (tf == T_GOAL) qF = (T)1;
+        else if (tf == T_LAVA) qF = (T)0;
+        else if (xyd_free(tf)) qF = cf.g * Vin[cfr * 4 + d];
+        else qF = gv[d];
+        const T qL = gv[(d + 3) & 3], qR = gv[(d + 1) & 3], qS = gv[d];
+        T best;
+        int arg;
+        if (!SLIP) {
+            best = qL; arg = 0;
+            if (qR > best) { best = qR; arg = 1; }
+            if (qF > best) { best = qF; arg = 2; }
+            if (qS > best) { best = qS; arg = 3; }
+        } else {
+            T s6 = qL + qR;
+            s6 = s6 + qF;
+            s6 = s6 + qS;
+            s6 = s6 + qS;
+            s6 = s6 + qS;
+            const T tail = cf.c * s6;
+            const T Q0 = cf.p * qL + tail, Q1 = cf.p * qR + tail, Q2 = cf.p * qF + tail,
+                    Q3 = cf.p * qS + tail;
+            best = Q0; arg = 0;
+            if (Q1 > best) { best = Q1; arg = 1; }
+            if (Q2 > best) { best = Q2; arg = 2; }
+            if (Q3 > best) { best = Q3; arg = 3; }
+        }
+        out.v[d] = best;
+        pk |= (uint32_t)(uint8_t)arg << (8 * d);
+        dv = tmax(dv, tabs_diff(best, own.v[d]));
+    }
+    if (WRITE_V) *reinterpret_cast<V4<T> *>(Vout + c * 4) = out;
+    *reinterpret_cast<uint32_t *>(pis + c * 4) = pk;
+    return dv;
+}
+
+// ------------------------------------------------------------------------------------------------
+// One cell of the DoorKey product model: 16 states l = (dir*2 + has_key)*2 + door_open,
+// action lanes left, right, forward, pickup, toggle (world_object.py:185-195, 244).
+// ------------------------------------------------------------------------------------------------
+template <typename T, bool WRITE_V>
+__device__ __forceinline__ T dk_cell(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
+                                     const T *Vin, T *Vout, int8_t *pis, int c) {
+    const int t = cl[c];
+    const T *vc = Vin + c * 16;
+    T own[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const V4<T> x = *reinterpret_cast<const V4<T> *>(vc + 4 * q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) own[4 * q + j] = x.v[j];
+    }
+    T gv[16];
+#pragma unroll
+    for (int l = 0; l < 16; ++l) gv[l] = cf.g * own[l];
+    T outv[16];
+    int8_t outp[16];
+    T dv = (T)0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const int cfr = c + geo.off[d];
+        const int tf = cl[cfr];
+        const V4<T> nb = *reinterpret_cast<const V4<T> *>(Vin + cfr * 16 + d * 4);
+#pragma unroll
+        for (int hk = 0; hk < 2; ++hk) {
+#pragma unroll
+            for (int dop = 0; dop < 2; ++dop) {
+                const int l = (d * 2 + hk) * 2 + dop;
+                if (!dk_walk(t, hk, dop)) { outv[l] = (T)0; outp[l] = -1; continue; }
+                const T qS = gv[l];
+                const T qL = gv[(((d + 3) & 3) * 2 + hk) * 2 + dop];
+                const T qR = gv[(((d + 1) & 3) * 2 + hk) * 2 + dop];
+                T qF;
+                if (tf == T_GOAL) qF = (T)1;
+                else if (tf == T_LAVA) qF = (T)0;
+                else if (dk_walk(tf, hk, dop)) qF = cf.g * nb.v[hk * 2 + dop];
+                else qF = qS;
+                const T qP = (tf == T_KEY && !hk) ? gv[(d * 2 + 1) * 2 + dop] : qS;
+                T qT = qS;
+                if (tf == T_DOOR) {
+                    if (dop) qT = gv[(d * 2 + hk) * 2 + 0];
+                    else if (hk) qT = gv[(d * 2 + hk) * 2 + 1];
+                }
+                T best = qL;
+                int arg = 0;
+                if (qR > best) { best = qR; arg = 1; }
+                if (qF > best) { best = qF; arg = 2; }
+                if (qP > best) { best = qP; arg = 3; }
+                if (qT > best) { best = qT; arg = 4; }
+                outv[l] = best;
+                outp[l] = (int8_t)arg;
+                dv = tmax(dv, tabs_diff(best, own[l]));
+            }
+        }
+    }
+    if (WRITE_V) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<V4<T> *>(Vout + c * 16 + 4 * q) =
+                V4<T>{{outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]}};
+    }
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        w[q] = (uint32_t)(uint8_t)outp[4 * q] | ((uint32_t)(uint8_t)outp[4 * q + 1] << 8) |
+               ((uint32_t)(uint8_t)outp[4 * q + 2] << 16) | ((uint32_t)(uint8_t)outp[4 * q + 3] << 24);
+    *reinterpret_cast<uint4 *>(pis + c * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+    return dv;
+}
+
+// ------------------------------------------------------------------------------------------------
+// (state, action) lane mapping: 8 lanes per state, lane a evaluates action a, a wave shuffle
+// max-reduce over the 8 lanes keeps the lowest index among exact maxima (numpy argmax rule).
+// ------------------------------------------------------------------------------------------------
+template <typename T, int MODEL, bool SLIP, bool WRITE_V>
+__device__ __forceinline__ T sa_sweep(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
+                                      const T *Vin, T *Vout, int8_t *pis) {
+    const int a = threadIdx.x & 7;
+    const int groups = blockDim.x >> 3;
+    const int S = geo.S;
+    const int bound = (S + groups - 1) / groups * groups;
+    const int A = MODEL == MGDP_MODEL_XYD ? 7 : 5;
+    const T NEG = -INFINITY;
+    T dv = (T)0;
+    for (int s = threadIdx.x >> 3; s < bound; s += groups) {
+        const bool inr = s < S;
+        const int ss = inr ? s : 0;
+        bool valid;
+        T q = NEG;
+        if (MODEL == MGDP_MODEL_XYD) {
+            const int c = ss >> 2, d = ss & 3;
+            valid = inr && xyd_free(cl[c]);
+            if (valid && a < A) {
+                if (a == 0) q = cf.g * Vin[c * 4 + ((d + 3) & 3)];
+                else if (a == 1) q = cf.g * Vin[c * 4 + ((d + 1) & 3)];
+                else if (a == 2) {
+                    const int cfr = c + geo.off[d];
+                    const int tf = cl[cfr];
+                    if (tf == T_GOAL) q = (T)1;
+                    else if (tf == T_LAVA) q = (T)0;
+                    else if (xyd_free(tf)) q = cf.g * Vin[cfr * 4 + d];
+                    else q = cf.g * Vin[ss];
+                } else q = cf.g * Vin[ss];
+            }
+            if (SLIP) {
+                const int base = (threadIdx.x & 63) & ~7;
+                const T q0 = __shfl(q, base + 0), q1 = __shfl(q, base + 1), q2 = __shfl(q, base + 2),
+                        q3 = __shfl(q, base + 3), q4 = __shfl(q, base + 4), q5 = __shfl(q, base + 5);
+                T s6 = q0 + q1;
+                s6 = s6 + q2;
+                s6 = s6 + q3;
+                s6 = s6 + q4;
+                s6 = s6 + q5;
+                if (valid && a < A) q = cf.p * q + cf.c * s6;
+            }
+        } else {
+            const int c = ss >> 4, l = ss & 15, d = l >> 2, hk = (l >> 1) & 1, dop = l & 1;
+            valid = inr && dk_walk(cl[c], hk, dop);
+            if (valid && a < A) {
+                const T *vc = Vin + c * 16;
+                if (a == 0) q = cf.g * vc[(((d + 3) & 3) * 2 + hk) * 2 + dop];
+                else if (a == 1) q = cf.g * vc[(((d + 1) & 3) * 2 + hk) * 2 + dop];
+                else {
+                    const int cfr = c + geo.off[d];
+                    const int tf = cl[cfr];
+                    int tgt = l;  // self loop unless the action changes the state
+                    if (a == 2) {
+                        if (tf == T_GOAL) tgt = -2;
+                        else if (tf == T_LAVA) tgt = -3;
+                        else if (dk_walk(tf, hk, dop)) tgt = -1;
+                    } else if (a == 3) {
+                        if (tf == T_KEY && !hk) tgt = (d * 2 + 1) * 2 + dop;
+                    } else {
+                        if (tf == T_DOOR) {
+                            if (dop) tgt = (d * 2 + hk) * 2 + 0;
+                            else if (hk) tgt = (d * 2 + hk) * 2 + 1;
+                        }
+                    }
+                    if (tgt == -2) q = (T)1;
+                    else if (tgt == -3) q = (T)0;
+                    else if (tgt == -1) q = cf.g * Vin[cfr * 16 + l];
+                    else q = cf.g * vc[tgt];
+                }
+            }
+        }
+        int arg = a;
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+            const T qo = __shfl_xor(q, o);
+            const int ao = __shfl_xor(arg, o);
+            if (qo > q || (qo == q && ao < arg)) { q = qo; arg = ao; }
+        }
+        if (a == 0 && inr) {
+            const T old = Vin[ss];
+            const T nv = valid ? q : (T)0;
+            if (WRITE_V) Vout[ss] = nv;
+            pis[ss] = valid ? (int8_t)arg : (int8_t)-1;
+            dv = tmax(dv, tabs_diff(nv, old));
+        }
+    }
+    return dv;
+}
+
+template <typename T, int MODEL, bool SLIP, int MAP, bool WRITE_V>
+__device__ __forceinline__ T sweep_lds(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
+                                       const T *Vin, T *Vout, int8_t *pis) {
+    if (MAP == MGDP_MAP_SA) return sa_sweep<T, MODEL, SLIP, WRITE_V>(geo, cf, cl, Vin, Vout, pis);
+    T dv = (T)0;
+    for (int c = threadIdx.x; c < geo.HW; c += blockDim.x) {
+        if (MODEL == MGDP_MODEL_XYD) dv = tmax(dv, xyd_cell<T, SLIP, WRITE_V>(geo, cf, cl, Vin, Vout, pis, c));
+        else dv = tmax(dv, dk_cell<T, WRITE_V>(geo, cf, cl, Vin, Vout, pis, c));
+    }
+    return dv;
+}
+
+// 16-byte cooperative copies between HBM and LDS (bytes is a multiple of 16).
+__device__ __forceinline__ void copy16(void *dst, const void *src, int bytes) {
+    const uint4 *s = reinterpret_cast<const uint4 *>(src);
+    uint4 *d = reinterpret_cast<uint4 *>(dst);
+    for (int i = threadIdx.x; i < (bytes >> 4); i += blockDim.x) d[i] = s[i];
+}
+__device__ __forceinline__ void zero16(void *dst, int bytes) {
+    uint4 *d = reinterpret_cast<uint4 *>(dst);
+    for (int i = threadIdx.x; i < (bytes >> 4); i += blockDim.x) d[i] = make_uint4(0, 0, 0, 0);
+}
+
+struct Smem {
+    int v_bytes, pi_bytes, cells_bytes, slot_bytes;
+    __host__ __device__ int total() const { return 2 * v_bytes + pi_bytes + cells_bytes + slot_bytes; }
+};
+
+__host__ __device__ inline Smem smem_layout(int S, int HWp, int tsize) {
+    Smem m;
+    m.v_bytes = S * tsize;  // S is a multiple of 4 -> 16-B multiple for f32, f64
+    m.pi_bytes = (S + 15) / 16 * 16;
+    m.cells_bytes = HWp;
+    m.slot_bytes = 2 * 16 * 8;
+    return m;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fused solve: blockIdx.x = grid index.  k_target < 0: sweep until this grid's own max|dV| < tol
+// (or max_sweeps).  k_target >= 0: sweep until exactly k_target sweeps have been done.
+// ------------------------------------------------------------------------------------------------
+template <typename T, int MODEL, bool SLIP, int MAP>
+__global__ void __launch_bounds__(1024)
+vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
+                int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
+                int k_target) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int e = blockIdx.x;
+    const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T));
+    T *V0 = reinterpret_cast<T *>(smem);
+    T *V1 = reinterpret_cast<T *>(smem + L.v_bytes);
+    int8_t *pis = reinterpret_cast<int8_t *>(smem + 2 * L.v_bytes);
+    uint8_t *cl = reinterpret_cast<uint8_t *>(smem + 2 * L.v_bytes + L.pi_bytes);
+    T *slots = reinterpret_cast<T *>(smem + 2 * L.v_bytes + L.pi_bytes + L.cells_bytes);
+
+    int k = kenv[e];
+    double dvl = dvenv[e];
+    const bool work = k_target < 0 ? (!(k > 0 && dvl < geo.tol) && k < geo.max_sweeps) : (k < k_target);
+    if (!work) return;
+
+    const long long vb = (long long)e * geo.S;
+    copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
+    if (k == 0) zero16(V0, L.v_bytes);
+    else copy16(V0, V + vb, L.v_bytes);
+    __syncthreads();
+
+    int cur = 0, parity = 0;
+    while (true) {
+        const T *Vin = cur ? V1 : V0;
+        T *Vout = cur ? V0 : V1;
+        const T dv = sweep_lds<T, MODEL, SLIP, MAP, true>(geo, cf, cl, Vin, Vout, pis);
+        const T bdv = block_max(dv, slots, parity);
+        parity ^= 1;
+        cur ^= 1;
+        ++k;
+        dvl = (double)bdv;
+        if (k_target < 0) {
+            if (dvl < geo.tol || k >= geo.max_sweeps) break;
+        } else if (k >= k_target) {
+            break;
+        }
+    }
+    copy16(V + vb, cur ? V1 : V0, L.v_bytes);
+    {   // S is a multiple of 4, so pi rows are 4-byte aligned
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(pis);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(pi + vb);
+        for (int i = threadIdx.x; i < (geo.S >> 2); i += blockDim.x) dst[i] = src[i];
+    }
+    if (threadIdx.x == 0) {
+        kenv[e] = k;
+        dvenv[e] = dvl;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// One Jacobi sweep (sweep index k, 1-based) of every grid, V double-buffered in HBM.
+// check_prev: skip the whole launch when the previous sweep's global max|dV| was already < tol
+// (lets the host enqueue sweeps speculatively without a sync per sweep).
+// POLICY: evaluate only, write pi (used once after convergence on V_{k-1}).
+// ------------------------------------------------------------------------------------------------
+template <typename T, int MODEL, bool SLIP, int MAP, bool POLICY>
+__global__ void __launch_bounds__(256)
+vi_sweep_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, const T *__restrict__ Vin,
+                T *__restrict__ Vout, int8_t *__restrict__ pi, unsigned long long *__restrict__ shards,
+                int k, int check_prev) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    if (check_prev && k > 1) {
+        const unsigned long long *prev = shards + (long long)(k - 2) * 8;
+        double m = 0.0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) m = fmax(m, __longlong_as_double((long long)prev[i]));
+        if (m < geo.tol) return;
+    }
+    const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T));
+    T *Vi = reinterpret_cast<T *>(smem);
+    T *Vo = reinterpret_cast<T *>(smem + L.v_bytes);
+    int8_t *pis = reinterpret_cast<int8_t *>(smem + 2 * L.v_bytes);
+    uint8_t *cl = reinterpret_cast<uint8_t *>(smem + 2 * L.v_bytes + L.pi_bytes);
+    T *slots = reinterpret_cast<T *>(smem + 2 * L.v_bytes + L.pi_bytes + L.cells_bytes);
+
+    T acc = (T)0;
+    for (int e = blockIdx.x; e < geo.B; e += gridDim.x) {
+        const long long vb = (long long)e * geo.S;
+        __syncthreads();
+        copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
+        copy16(Vi, Vin + vb, L.v_bytes);
+        __syncthreads();
+        acc = tmax(acc, sweep_lds<T, MODEL, SLIP, MAP, !POLICY>(geo, cf, cl, Vi, Vo, pis));
+        __syncthreads();
+        if (!POLICY) {
+            copy16(Vout + vb, Vo, L.v_bytes);
+        } else {
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(pis);
+            uint32_t *dst = reinterpret_cast<uint32_t *>(pi + vb);
+            for (int i = threadIdx.x; i < (geo.S >> 2); i += blockDim.x) dst[i] = src[i];
+        }
+    }
+    if (!POLICY) {
+        const T bdv = block_max(acc, slots, 0);
+        if (threadIdx.x == 0 && shards)
+            atomicMax(shards + (long long)(k - 1) * 8 + (blockIdx.x & 7),
+                      (unsigned long long)__double_as_longlong((double)bdv));
+    }
+}
+
+__global__ void __launch_bounds__(1024)
+vi_reduce_kernel(const int32_t *__restrict__ kenv, const double *__restrict__ dvenv, int B,
+                 unsigned long long *__restrict__ out) {
+    __shared__ int ks[16], kn[16];
+    __shared__ double ds[16];
+    int km = 0, kmin = 0x7fffffff;
+    double dm = 0.0;
+    for (int i = threadIdx.x; i < B; i += blockDim.x) {
+        km = max(km, kenv[i]);
+        kmin = min(kmin, kenv[i]);
+        dm = fmax(dm, dvenv[i]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        km = max(km, __shfl_xor(km, o));
+        kmin = min(kmin, __shfl_xor(kmin, o));
+        dm = fmax(dm, __shfl_xor(dm, o));
+    }
+    if ((threadIdx.x & 63) == 0) { ks[threadIdx.x >> 6] = km; kn[threadIdx.x >> 6] = kmin; ds[threadIdx.x >> 6] = dm; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) { km = max(km, ks[i]); kmin = min(kmin, kn[i]); dm = fmax(dm, ds[i]); }
+        out[0] = (unsigned long long)km;
+        out[1] = (unsigned long long)__double_as_longlong(dm);
+        out[2] = (unsigned long long)kmin;
+    }
+}
+
+}  // namespace mgdp
+
+// ================================================================================================
+// Host side
+// ================================================================================================
+using namespace mgdp;
+
+struct mgdp_vi {
+    mgdp_vi_desc d;
+    int S = 0, HW = 0, HWp = 0, A = 0, tsize = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    uint8_t *d_cells = nullptr;
+    void *d_V[2] = {nullptr, nullptr};
+    int8_t *d_pi = nullptr;
+    int32_t *d_kenv = nullptr;
+    double *d_dvenv = nullptr;
+    unsigned long long *d_shards = nullptr;
+    unsigned long long *d_red = nullptr;
+    unsigned long long *h_red = nullptr;  // pinned
+    int cur = 0;        // V buffer holding the current V (sweep method)
+    int k_min = 0;      // min sweeps over grids after the last reduce (fused method)
+    bool k_done_valid = false;  // k_min / dv_red describe the current device state
+    double dv_red = 0.0;
+    int k_done = 0;     // sweeps completed by every grid (uniform after run_to / sweep)
+    int32_t sweeps = 0, converged = 0;
+    bool cells_loaded = false;
+    // timing of the dominant kernel
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+    std::vector<int> ev_sweep;  // sweep index of each timed sweep launch (-1 = fused launch)
+    double total_ms = 0.0;
+    int64_t launches = 0;
+    int fused_block = 256;
+    int sweep_grid = 2048;
+};
+
+namespace {
+
+Geo make_geo(const mgdp_vi *vi) {
+    Geo g;
+    g.B = vi->d.B;
+    g.W = vi->d.W;
+    g.H = vi->d.H;
+    g.HW = vi->HW;
+    g.HWp = vi->HWp;
+    g.S = vi->S;
+    g.off[0] = 1;
+    g.off[1] = vi->d.W;
+    g.off[2] = -1;
+    g.off[3] = -vi->d.W;
+    g.max_sweeps = vi->d.max_sweeps;
+    g.tol = vi->d.tol;
+    return g;
+}
+
+template <typename T>
+Coef<T> make_coef(const mgdp_vi *vi) {
+    Coef<T> c;
+    c.g = (T)vi->d.gamma;
+    const double p = vi->d.slip_p;
+    c.p = (T)p;
+    c.c = (T)((1.0 - p) / 6.0);
+    return c;
+}
+
+int timed_begin(mgdp_vi *vi, int sweep_idx) {
+    if (!vi->timing) return 0;
+    hipEvent_t a, b;
+    MGDP_HIP(hipEventCreate(&a));
+    MGDP_HIP(hipEventCreate(&b));
+    MGDP_HIP(hipEventRecord(a, vi->stream));
+    vi->ev.push_back({a, b});
+    vi->ev_sweep.push_back(sweep_idx);
+    return 0;
+}
+int timed_end(mgdp_vi *vi) {
+    if (!vi->timing) return 0;
+    MGDP_HIP(hipEventRecord(vi->ev.back().second, vi->stream));
+    return 0;
+}
+// Called after a stream sync: fold recorded events into total_ms (sweep launches beyond the
+// last useful sweep no-op and are not counted).
+int timed_collect(mgdp_vi *vi, int last_sweep) {
+    for (size_t i = 0; i < vi->ev.size(); ++i) {
+        const int si = vi->ev_sweep[i];
+        if (si < 0 || si <= last_sweep) {
+            float ms = 0.f;
+            MGDP_HIP(hipEventElapsedTime(&ms, vi->ev[i].first, vi->ev[i].second));
+            vi->total_ms += ms;
+            vi->launches += 1;
+        }
+        (void)hipEventDestroy(vi->ev[i].first);
+        (void)hipEventDestroy(vi->ev[i].second);
+    }
+    vi->ev.clear();
+    vi->ev_sweep.clear();
+    return 0;
+}
+
+template <typename T, int MODEL, bool SLIP, int MAP>
+int launch_fused_t(mgdp_vi *vi, int k_target) {
+    const Geo g = make_geo(vi);
+    const Smem L = smem_layout(vi->S, vi->HWp, sizeof(T));
+    auto kern = vi_fused_kernel<T, MODEL, SLIP, MAP>;
+    if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
+    if (int rc = timed_begin(vi, -1)) return rc;
+    hipLaunchKernelGGL(kern, dim3(vi->d.B), dim3(vi->fused_block), L.total(), vi->stream, g,
+                       make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv,
+                       vi->d_dvenv, k_target);
+    MGDP_HIP(hipGetLastError());
+    return timed_end(vi);
+}
+
+template <typename T, int MODEL, bool SLIP, int MAP>
+int launch_sweep_t(mgdp_vi *vi, int k, int check_prev, bool policy) {
+    const Geo g = make_geo(vi);
+    const Smem L = smem_layout(vi->S, vi->HWp, sizeof(T));
+    const int grid = std::min(vi->d.B, vi->sweep_grid);
+    const T *Vin = (const T *)vi->d_V[(k - 1) & 1];
+    T *Vout = (T *)vi->d_V[k & 1];
+    if (policy) {
+        auto kern = vi_sweep_kernel<T, MODEL, SLIP, MAP, true>;
+        if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), L.total(), vi->stream, g, make_coef<T>(vi),
+                           vi->d_cells, Vin, Vout, vi->d_pi, (unsigned long long *)nullptr, k, 0);
+        MGDP_HIP(hipGetLastError());
+        return 0;
+    }
+    auto kern = vi_sweep_kernel<T, MODEL, SLIP, MAP, false>;
+    if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
+    if (int rc = timed_begin(vi, k)) return rc;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), L.total(), vi->stream, g, make_coef<T>(vi),
+                       vi->d_cells, Vin, Vout, vi->d_pi, vi->d_shards, k, check_prev);
+    MGDP_HIP(hipGetLastError());
+    return timed_end(vi);
+}
+
+// Dispatch on (dtype, model, slip, mapping).
+template <template <typename, int, bool, int> class F, typename... Args>
+int dispatch(mgdp_vi *vi, Args... args) {
+    const bool slip = vi->d.slip_p >= 0.0;
+    const bool sa = vi->d.mapping == MGDP_MAP_SA;
+    if (vi->d.dtype == MGDP_F32) {
+        if (vi->d.model == MGDP_MODEL_XYD) {
+            if (slip) return sa ? F<float, 0, true, 1>::run(vi, args...) : F<float, 0, true, 0>::run(vi, args...);
+            return sa ? F<float, 0, false, 1>::run(vi, args...) : F<float, 0, false, 0>::run(vi, args...);
+        }
+        return sa ? F<float, 1, false, 1>::run(vi, args...) : F<float, 1, false, 0>::run(vi, args...);
+    }
+    if (vi->d.model == MGDP_MODEL_XYD) {
+        if (slip) return sa ? F<double, 0, true, 1>::run(vi, args...) : F<double, 0, true, 0>::run(vi, args...);
+        return sa ? F<double, 0, false, 1>::run(vi, args...) : F<double, 0, false, 0>::run(vi, args...);
+    }
+    return sa ? F<double, 1, false, 1>::run(vi, args...) : F<double, 1, false, 0>::run(vi, args...);
+}
+
+template <typename T, int MODEL, bool SLIP, int MAP>
+struct FusedF {
+    static int run(mgdp_vi *vi, int k_target) { return launch_fused_t<T, MODEL, SLIP, MAP>(vi, k_target); }
+};
+template <typename T, int MODEL, bool SLIP, int MAP>
+struct SweepF {
+    static int run(mgdp_vi *vi, int k, int check_prev, bool policy) {
+        return launch_sweep_t<T, MODEL, SLIP, MAP>(vi, k, check_prev, policy);
+    }
+};
+
+int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
+    hipLaunchKernelGGL(vi_reduce_kernel, dim3(1), dim3(1024), 0, vi->stream, vi->d_kenv, vi->d_dvenv,
+                       vi->d.B, vi->d_red);
+    MGDP_HIP(hipGetLastError());
+    MGDP_HIP(hipMemcpyAsync(vi->h_red, vi->d_red, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, vi->stream));
+    MGDP_HIP(hipStreamSynchronize(vi->stream));
+    if (int rc = timed_collect(vi, 1 << 30)) return rc;
+    long long bits = (long long)vi->h_red[1];
+    std::memcpy(&vi->dv_red, &bits, sizeof(double));
+    vi->k_min = (int)vi->h_red[2];
+    vi->k_done_valid = true;
+    if (kmax) *kmax = (int32_t)vi->h_red[0];
+    if (dvmax) *dvmax = vi->dv_red;
+    return 0;
+}
+
+double shard_max(const unsigned long long *sh) {
+    double m = 0.0;
+    for (int i = 0; i < 8; ++i) {
+        double v;
+        std::memcpy(&v, &sh[i], sizeof(double));
+        m = v > m ? v : m;
+    }
+    return m;
+}
+
+// Sweep method: run sweeps k_done+1.. with the device-global rule; force = run exactly to k_stop.
+int sweep_run(mgdp_vi *vi, int k_stop, bool force, double *dv_out) {
+    const int chunk = 8;
+    std::vector<unsigned long long> host(8 * chunk);
+    double dv = 0.0;
+    while (vi->k_done < k_stop) {
+        const int n = std::min(chunk, k_stop - vi->k_done);
+        for (int i = 1; i <= n; ++i)
+            if (int rc = dispatch<SweepF>(vi, vi->k_done + i, force ? 0 : 1, false)) return rc;
+        MGDP_HIP(hipMemcpyAsync(host.data(), vi->d_shards + (long long)vi->k_done * 8, 8 * n * sizeof(unsigned long long), hipMemcpyDeviceToHost, vi->stream));
+        MGDP_HIP(hipStreamSynchronize(vi->stream));
+        int last = vi->k_done + n;
+        bool stop = false;
+        for (int i = 0; i < n; ++i) {
+            dv = shard_max(&host[8 * i]);
+            if (!force && dv < vi->d.tol) {
+                last = vi->k_done + i + 1;
+                stop = true;
+                break;
+            }
+        }
+        if (int rc = timed_collect(vi, last)) return rc;
+        vi->k_done = last;
+        vi->cur = last & 1;
+        if (stop) break;
+    }
+    if (dv_out) *dv_out = dv;
+    return 0;
+}
+
+int validate_cells(const mgdp_vi_desc &d, const uint8_t *cells) {
+    const int HW = d.W * d.H;
+    for (int b = 0; b < d.B; ++b) {
+        const uint8_t *c = cells + (int64_t)b * HW;
+        int doors = 0, keys = 0;
+        for (int y = 0; y < d.H; ++y)
+            for (int x = 0; x < d.W; ++x) {
+                const int t = c[y * d.W + x];
+                const bool border = x == 0 || y == 0 || x == d.W - 1 || y == d.H - 1;
+                bool ok = t == T_EMPTY || t == T_WALL || t == T_FLOOR || t == T_GOAL || t == T_LAVA;
+                if (d.model == MGDP_MODEL_DOORKEY) {
+                    if (t == T_DOOR) { ++doors; ok = !border; }
+                    if (t == T_KEY) { ++keys; ok = !border; }
+                }
+                MGDP_CHECK(ok, MGDP_E_UNSUPPORTED, "grid %d cell (%d,%d): type %d is outside the %s model", b, x, y, t,
+                           d.model == MGDP_MODEL_XYD ? "XYD" : "DoorKey");
+                MGDP_CHECK(!(border && (t == T_EMPTY || t == T_FLOOR)), MGDP_E_UNSUPPORTED,
+                           "grid %d border cell (%d,%d) is walkable; the model needs a closed border", b, x, y);
+            }
+        if (d.model == MGDP_MODEL_DOORKEY)
+            MGDP_CHECK(doors == 1 && keys == 1, MGDP_E_UNSUPPORTED,
+                       "grid %d: DoorKey model needs exactly one door and one key (found %d, %d)", b, doors, keys);
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mgdp_vi_num_states(const mgdp_vi_desc *d, int64_t *S) {
+    MGDP_CHECK(d && S, MGDP_E_INVALID, "null argument");
+    *S = (int64_t)d->W * d->H * (d->model == MGDP_MODEL_XYD ? 4 : 16);
+    return 0;
+}
+
+int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
+    MGDP_CHECK(desc && out, MGDP_E_INVALID, "null argument");
+    const mgdp_vi_desc &d = *desc;
+    MGDP_CHECK(d.model == MGDP_MODEL_XYD || d.model == MGDP_MODEL_DOORKEY, MGDP_E_INVALID, "unknown model %d", d.model);
+    MGDP_CHECK(d.dtype == MGDP_F32 || d.dtype == MGDP_F64, MGDP_E_INVALID, "unknown dtype %d", d.dtype);
+    MGDP_CHECK(d.method == MGDP_METHOD_FUSED || d.method == MGDP_METHOD_SWEEP, MGDP_E_INVALID, "unknown method %d", d.method);
+    MGDP_CHECK(d.mapping == MGDP_MAP_CELL || d.mapping == MGDP_MAP_SA, MGDP_E_INVALID, "unknown mapping %d", d.mapping);
+    MGDP_CHECK(d.B > 0 && d.W >= 3 && d.H >= 3, MGDP_E_INVALID, "bad shape B=%d W=%d H=%d", d.B, d.W, d.H);
+    MGDP_CHECK(d.max_sweeps > 0, MGDP_E_INVALID, "max_sweeps must be > 0");
+    MGDP_CHECK(d.gamma >= 0.0 && d.gamma < 1.0, MGDP_E_INVALID, "gamma must be in [0, 1)");
+    MGDP_CHECK(d.tol > 0.0, MGDP_E_INVALID, "tol must be > 0");
+    MGDP_CHECK(!(d.slip_p >= 0.0 && d.model != MGDP_MODEL_XYD), MGDP_E_UNSUPPORTED,
+               "slip transitions are defined for the XYD model only");
+    MGDP_CHECK(d.slip_p <= 1.0, MGDP_E_INVALID, "slip_p must be <= 1");
+    int ndev = 0;
+    MGDP_HIP(hipGetDeviceCount(&ndev));
+    MGDP_CHECK(d.device >= 0 && d.device < ndev, MGDP_E_HIP, "device %d not available (%d visible)", d.device, ndev);
+    DeviceGuard guard(d.device);
+    MGDP_CHECK(guard.ok, MGDP_E_HIP, "hipSetDevice(%d) failed", d.device);
+
+    mgdp_vi *vi = new mgdp_vi();
+    vi->d = d;
+    vi->HW = d.W * d.H;
+    vi->HWp = (int)round_up(vi->HW, 16);
+    vi->S = vi->HW * (d.model == MGDP_MODEL_XYD ? 4 : 16);
+    vi->A = d.model == MGDP_MODEL_XYD ? 7 : 5;
+    vi->tsize = d.dtype == MGDP_F32 ? 4 : 8;
+    const Smem L = smem_layout(vi->S, vi->HWp, vi->tsize);
+    if (L.total() > 160 * 1024) {
+        delete vi;
+        set_error("grid too large for the LDS-resident kernels (%d B > 160 KiB)", L.total());
+        return MGDP_E_UNSUPPORTED;
+    }
+    // fused: one workgroup per grid; a lone grid gets a wider workgroup (single-CU solve)
+    const int items = d.mapping == MGDP_MAP_SA ? vi->S * 8 : vi->HW;
+    int blk = d.B == 1 ? 1024 : 256;
+    while (blk > 64 && blk / 2 >= items) blk /= 2;
+    vi->fused_block = blk;
+
+    const size_t BS = (size_t)d.B * vi->S;
+    hipError_t e = hipSuccess;
+    auto al = [&](void **p, size_t n) { if (e == hipSuccess) e = hipMalloc(p, n); };
+    al((void **)&vi->d_cells, (size_t)d.B * vi->HWp);
+    al(&vi->d_V[0], BS * vi->tsize);
+    if (d.method == MGDP_METHOD_SWEEP) al(&vi->d_V[1], BS * vi->tsize);
+    al((void **)&vi->d_pi, BS);
+    al((void **)&vi->d_kenv, sizeof(int32_t) * d.B);
+    al((void **)&vi->d_dvenv, sizeof(double) * d.B);
+    al((void **)&vi->d_shards, sizeof(unsigned long long) * 8 * (size_t)(d.max_sweeps + 1));
+    al((void **)&vi->d_red, sizeof(unsigned long long) * 4);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&vi->h_red, 4 * sizeof(unsigned long long), hipHostMallocDefault);
+    if (e == hipSuccess) {
+        e = hipStreamCreateWithFlags(&vi->stream, hipStreamNonBlocking);
+        vi->own_stream = e == hipSuccess;
+    }
+    if (e == hipSuccess) e = hipMemset(vi->d_cells, 0, (size_t)d.B * vi->HWp);
+    if (e != hipSuccess) {
+        mgdp_vi_destroy(vi);
+        return hip_fail(e, "mgdp_vi_create allocation", __FILE__, __LINE__);
+    }
+    *out = vi;
+    return mgdp_vi_reset(vi);
+}
+
+int mgdp_vi_destroy(mgdp_vi *vi) {
+    if (!vi) return 0;
+    DeviceGuard guard(vi->d.device);
+    if (vi->stream) (void)hipStreamSynchronize(vi->stream);
+    for (auto &p : vi->ev) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
+    (void)hipFree(vi->d_cells);
+    (void)hipFree(vi->d_V[0]);
+    (void)hipFree(vi->d_V[1]);
+    (void)hipFree(vi->d_pi);
+    (void)hipFree(vi->d_kenv);
+    (void)hipFree(vi->d_dvenv);
+    (void)hipFree(vi->d_shards);
+    (void)hipFree(vi->d_red);
+    if (vi->h_red) (void)hipHostFree(vi->h_red);
+    if (vi->own_stream) (void)hipStreamDestroy(vi->stream);
+    delete vi;
+    return 0;
+}
+
+int mgdp_vi_set_stream(mgdp_vi *vi, void *s) {
+    MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
+    DeviceGuard guard(vi->d.device);
+    MGDP_HIP(hipStreamSynchronize(vi->stream));
+    if (vi->own_stream) { (void)hipStreamDestroy(vi->stream); vi->own_stream = false; vi->stream = nullptr; }
+    if (s) {
+        vi->stream = (hipStream_t)s;
+    } else {
+        MGDP_HIP(hipStreamCreateWithFlags(&vi->stream, hipStreamNonBlocking));
+        vi->own_stream = true;
+    }
+    return 0;
+}
+
+int mgdp_vi_load_cells(mgdp_vi *vi, const uint8_t *cells) {
+    MGDP_CHECK(vi && cells, MGDP_E_INVALID, "null argument");
+    if (int rc = validate_cells(vi->d, cells)) return rc;
+    DeviceGuard guard(vi->d.device);
+    std::vector<uint8_t> pad((size_t)vi->d.B * vi->HWp, 0);
+    for (int b = 0; b < vi->d.B; ++b) std::memcpy(&pad[(size_t)b * vi->HWp], cells + (size_t)b * vi->HW, vi->HW);
+    MGDP_HIP(hipMemcpyAsync(vi->d_cells, pad.data(), pad.size(), hipMemcpyHostToDevice, vi->stream));
+    MGDP_HIP(hipStreamSynchronize(vi->stream));
+    vi->cells_loaded = true;
+    vi->k_done_valid = false;
+    return 0;
+}
+
+int mgdp_vi_load_cells_device(mgdp_vi *vi, const uint8_t *d_cells) {
+    MGDP_CHECK(vi && d_cells, MGDP_E_INVALID, "null argument");
+    DeviceGuard guard(vi->d.device);
+    MGDP_HIP(hipMemcpy2DAsync(vi->d_cells, vi->HWp, d_cells, vi->HW, vi->HW, vi->d.B, hipMemcpyDeviceToDevice, vi->stream));
+    vi->cells_loaded = true;
+    vi->k_done_valid = false;
+    return 0;
+}
+
+int mgdp_vi_reset(mgdp_vi *vi) {
+    MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
+    DeviceGuard guard(vi->d.device);
+    const size_t BS = (size_t)vi->d.B * vi->S;
+    MGDP_HIP(hipMemsetAsync(vi->d_V[0], 0, BS * vi->tsize, vi->stream));
+    if (vi->d_V[1]) MGDP_HIP(hipMemsetAsync(vi->d_V[1], 0, BS * vi->tsize, vi->stream));
+    MGDP_HIP(hipMemsetAsync(vi->d_kenv, 0, sizeof(int32_t) * vi->d.B, vi->stream));
+    MGDP_HIP(hipMemsetAsync(vi->d_dvenv, 0, sizeof(double) * vi->d.B, vi->stream));
+    MGDP_HIP(hipMemsetAsync(vi->d_shards, 0, sizeof(unsigned long long) * 8 * (size_t)(vi->d.max_sweeps + 1), vi->stream));
+    vi->cur = 0;
+    vi->k_done = 0;
+    vi->k_min = 0;
+    vi->k_done_valid = false;
+    vi->sweeps = 0;
+    vi->converged = 0;
+    return 0;
+}
+
+int mgdp_vi_run_local(mgdp_vi *vi, int32_t *k_local_max) {
+    MGDP_CHECK(vi && k_local_max, MGDP_E_INVALID, "null argument");
+    MGDP_CHECK(vi->cells_loaded, MGDP_E_INVALID, "no cells loaded");
+    DeviceGuard guard(vi->d.device);
+    if (vi->d.method == MGDP_METHOD_FUSED) {
+        if (int rc = dispatch<FusedF>(vi, -1)) return rc;
+        int32_t km;
+        if (int rc = reduce_env(vi, &km, nullptr)) return rc;
+        *k_local_max = km;
+        return 0;
+    }
+    if (int rc = sweep_run(vi, vi->d.max_sweeps, false, nullptr)) return rc;
+    *k_local_max = vi->k_done;
+    return 0;
+}
+
+int mgdp_vi_run_to(mgdp_vi *vi, int32_t k_target, double *dv_out) {
+    MGDP_CHECK(vi && dv_out, MGDP_E_INVALID, "null argument");
+    MGDP_CHECK(k_target >= 0 && k_target <= vi->d.max_sweeps, MGDP_E_INVALID, "k_target %d out of range", k_target);
+    DeviceGuard guard(vi->d.device);
+    if (vi->d.method == MGDP_METHOD_FUSED) {
+        if (vi->k_min == k_target && vi->k_done_valid) {  // every grid is already there
+            vi->k_done = k_target;
+            *dv_out = vi->dv_red;
+            return 0;
+        }
+        if (int rc = dispatch<FusedF>(vi, k_target)) return rc;
+        int32_t km;
+        if (int rc = reduce_env(vi, &km, dv_out)) return rc;
+        MGDP_CHECK(km == k_target, MGDP_E_INVALID, "run_to(%d): a grid is already at sweep %d", k_target, km);
+        vi->k_done = k_target;
+        return 0;
+    }
+    MGDP_CHECK(k_target >= vi->k_done, MGDP_E_INVALID, "run_to(%d) behind sweep %d", k_target, vi->k_done);
+    if (k_target == vi->k_done) {
+        std::vector<unsigned long long> sh(8);
+        if (k_target == 0) { *dv_out = 0.0; return 0; }
+        MGDP_HIP(hipMemcpy(sh.data(), vi->d_shards + (long long)(k_target - 1) * 8, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        *dv_out = shard_max(sh.data());
+        return 0;
+    }
+    return sweep_run(vi, k_target, true, dv_out);
+}
+
+int mgdp_vi_sweep(mgdp_vi *vi, double *dv_out) {
+    MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
+    if (vi->d.method == MGDP_METHOD_FUSED) {
+        int32_t km = 0;
+        DeviceGuard guard(vi->d.device);
+        if (int rc = reduce_env(vi, &km, nullptr)) return rc;
+        return mgdp_vi_run_to(vi, km + 1, dv_out);
+    }
+    return mgdp_vi_run_to(vi, vi->k_done + 1, dv_out);
+}
+
+int mgdp_vi_finish(mgdp_vi *vi, int32_t sweeps) {
+    MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
+    DeviceGuard guard(vi->d.device);
+    vi->sweeps = sweeps;
+    if (vi->d.method == MGDP_METHOD_SWEEP && sweeps > 0) {
+        MGDP_CHECK(sweeps == vi->k_done, MGDP_E_INVALID, "finish(%d) but %d sweeps were run", sweeps, vi->k_done);
+        // pi of sweep k = argmax evaluated on V_{k-1} (bit-identical to what sweep k computed)
+        if (int rc = dispatch<SweepF>(vi, sweeps, 0, true)) return rc;
+        vi->cur = sweeps & 1;
+    }
+    MGDP_HIP(hipStreamSynchronize(vi->stream));
+    return 0;
+}
+
+int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *converged_out) {
+    MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
+    if (int rc = mgdp_vi_reset(vi)) return rc;
+    int32_t k = 0;
+    if (int rc = mgdp_vi_run_local(vi, &k)) return rc;
+    double dv = 0.0;
+    if (int rc = mgdp_vi_run_to(vi, k, &dv)) return rc;
+    while (!(dv < vi->d.tol) && k < vi->d.max_sweeps) {  // contraction broken by rounding: global rule
+        if (int rc = mgdp_vi_sweep(vi, &dv)) return rc;
+        ++k;
+    }
+    if (int rc = mgdp_vi_finish(vi, k)) return rc;
+    vi->converged = dv < vi->d.tol;
+    if (sweeps_out) *sweeps_out = k;
+    if (dv_out) *dv_out = dv;
+    if (converged_out) *converged_out = vi->converged;
+    return 0;
+}
+
+int mgdp_vi_get_values(mgdp_vi *vi, void *V) {
+    MGDP_CHECK(vi && V, MGDP_E_INVALID, "null argument");
+    DeviceGuard guard(vi->d.device);
+    const void *src = vi->d.method == MGDP_METHOD_SWEEP ? vi->d_V[vi->cur] : vi->d_V[0];
+    MGDP_HIP(hipMemcpyAsync(V, src, (size_t)vi->d.B * vi->S * vi->tsize, hipMemcpyDeviceToHost, vi->stream));
+    MGDP_HIP(hipStreamSynchronize(vi->stream));
+    return 0;
+}
+
+int mgdp_vi_get_policy(mgdp_vi *vi, int8_t *pi) {
+    MGDP_CHECK(vi && pi, MGDP_E_INVALID, "null argument");
+    DeviceGuard guard(vi->d.device);
+    MGDP_HIP(hipMemcpyAsync(pi, vi->d_pi, (size_t)vi->d.B * vi->S, hipMemcpyDeviceToHost, vi->stream));
+    MGDP_HIP(hipStreamSynchronize(vi->stream));
+    return 0;
+}
+
+int mgdp_vi_get_dv_trace(mgdp_vi *vi, double *trace, int32_t n) {
+    MGDP_CHECK(vi && trace && n >= 0 && n <= vi->d.max_sweeps, MGDP_E_INVALID, "bad argument");
+    DeviceGuard guard(vi->d.device);
+    std::vector<unsigned long long> sh((size_t)8 * n);
+    if (n) MGDP_HIP(hipMemcpy(sh.data(), vi->d_shards, sh.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; ++i) trace[i] = shard_max(&sh[8 * (size_t)i]);
+    return 0;
+}
+
+int mgdp_vi_device_buffers(mgdp_vi *vi, void **d_V, void **d_pi) {
+    MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
+    if (d_V) *d_V = vi->d.method == MGDP_METHOD_SWEEP ? vi->d_V[vi->cur] : vi->d_V[0];
+    if (d_pi) *d_pi = vi->d_pi;
+    return 0;
+}
+
+int mgdp_vi_enable_timing(mgdp_vi *vi, int32_t on) {
+    MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
+    vi->timing = on != 0;
+    vi->total_ms = 0.0;
+    vi->launches = 0;
+    return 0;
+}
+
+int mgdp_vi_kernel_time(mgdp_vi *vi, double *total_ms, int64_t *launches) {
+    MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
+    if (total_ms) *total_ms = vi->total_ms;
+    if (launches) *launches = vi->launches;
+    return 0;
+}
+
+}  // extern "C"

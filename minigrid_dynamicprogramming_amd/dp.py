@@ -1,0 +1,249 @@
+"""Tabular value iteration over Minigrid grids on MI355X (front end of csrc/vi.hip).
+
+The reference has no DP code; this module implements the build-defined
+value iteration of DESIGN.md "A9", whose transition is the reference MiniGridEnv.step
+(minigrid/minigrid_env.py:520-583).  Models:
+  "xyd"      s = (y*W + x)*4 + dir, 7 actions (Empty, FourRooms, LavaCrossing, SimpleCrossing)
+  "doorkey"  s = (((y*W + x)*4 + dir)*2 + has_key)*2 + door_open, 5 action lanes
+             (left, right, forward, pickup, toggle)
+Optional slip transitions follow StochasticActionWrapper (minigrid/wrappers.py:775-796).
+All arithmetic runs in libmgdp.so on the GPU; results are bit-identical to the CPU oracle.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .core import COLOR_TO_IDX, OBJECT_TO_IDX
+
+MODELS = {"xyd": _lib.MODEL_XYD, "doorkey": _lib.MODEL_DOORKEY}
+DTYPES = {"f32": _lib.F32, "f64": _lib.F64}
+METHODS = {"fused": _lib.METHOD_FUSED, "sweep": _lib.METHOD_SWEEP}
+MAPPINGS = {"cell": _lib.MAP_CELL, "sa": _lib.MAP_SA}
+DOORKEY_ACTIONS = (0, 1, 2, 3, 5)  # DP action lane -> env action (doorkey.py:25-33)
+
+
+def n_states(model: str, W: int, H: int) -> int:
+    return W * H * (4 if model == "xyd" else 16)
+
+
+def n_actions(model: str) -> int:
+    return 7 if model == "xyd" else 5
+
+
+def state_index(model: str, W: int, x: int, y: int, d: int, has_key: int = 0, door_open: int = 0) -> int:
+    s = (y * W + x) * 4 + d
+    if model == "doorkey":
+        s = (s * 2 + has_key) * 2 + door_open
+    return s
+
+
+def to_cells(grids) -> tuple[np.ndarray, np.ndarray | None]:
+    """Normalise grids to (B, H, W) OBJECT_TO_IDX cell codes (+ the (B, W, H, 3) encodings when known).
+
+    Accepts: env objects with .grid, Grid objects (or lists of either), (B, W, H, 3) encodings in
+    the reference's x-major Grid.encode() layout, or cell codes (H, W) / (B, H, W)."""
+    if isinstance(grids, np.ndarray):
+        a = grids
+        if a.ndim == 4:  # (B, W, H, 3) encodings
+            enc = np.ascontiguousarray(a, dtype=np.uint8)
+            return np.ascontiguousarray(enc[..., 0].transpose(0, 2, 1)), enc
+        if a.ndim == 2:  # (H, W) cells
+            a = a[None]
+        if a.ndim != 3:
+            raise ValueError("expected (B, W, H, 3) encodings or (B, H, W) / (H, W) cell codes")
+        return np.ascontiguousarray(a, dtype=np.uint8), None
+    if hasattr(grids, "grid") or hasattr(grids, "encode"):
+        grids = [grids]
+    encs = []
+    for g in grids:
+        grid = g.grid if hasattr(g, "grid") else g
+        encs.append(grid.encode())
+    enc = np.ascontiguousarray(np.stack(encs), dtype=np.uint8)
+    return np.ascontiguousarray(enc[..., 0].transpose(0, 2, 1)), enc
+
+
+def infer_model(cells: np.ndarray) -> str:
+    has_door = (cells == OBJECT_TO_IDX["door"]).any()
+    has_key = (cells == OBJECT_TO_IDX["key"]).any()
+    return "doorkey" if (has_door or has_key) else "xyd"
+
+
+def check_doorkey_encoding(enc: np.ndarray):
+    """DoorKey model preconditions that need colours/states: one LOCKED door, key of its colour."""
+    for b in range(enc.shape[0]):
+        t = enc[b, :, :, 0]
+        door = np.argwhere(t == OBJECT_TO_IDX["door"])
+        key = np.argwhere(t == OBJECT_TO_IDX["key"])
+        if len(door) != 1 or len(key) != 1:
+            raise ValueError(f"grid {b}: the DoorKey model needs exactly one door and one key")
+        dx, dy = door[0]
+        kx, ky = key[0]
+        if enc[b, dx, dy, 2] != 2:
+            raise ValueError(f"grid {b}: the DoorKey model starts from a locked door")
+        if enc[b, dx, dy, 1] != enc[b, kx, ky, 1]:
+            raise ValueError(f"grid {b}: key colour does not match the door")
+
+
+@dataclass
+class VIResult:
+    V: np.ndarray        # (B, S) float32 / float64
+    pi: np.ndarray       # (B, S) int8 action lane (-1 = absorbing)
+    sweeps: int
+    converged: bool
+    dv: float            # max |V_k - V_{k-1}| at the last sweep
+    model: str
+    W: int
+    H: int
+
+    def value(self, b: int, x: int, y: int, d: int, has_key: int = 0, door_open: int = 0):
+        return self.V[b, state_index(self.model, self.W, x, y, d, has_key, door_open)]
+
+    def action(self, b: int, x: int, y: int, d: int, has_key: int = 0, door_open: int = 0) -> int:
+        """Greedy env action (Actions id) at a state."""
+        lane = int(self.pi[b, state_index(self.model, self.W, x, y, d, has_key, door_open)])
+        if lane < 0:
+            return -1
+        return DOORKEY_ACTIONS[lane] if self.model == "doorkey" else lane
+
+
+class ValueIteration:
+    """A batch of B grids resident on one GPU (an mgdp_vi handle); solve() may be called repeatedly.
+
+    method "fused": one workgroup per grid, V in LDS for the whole solve (default; fastest).
+    method "sweep": one launch per Jacobi sweep, V double-buffered in HBM.
+    mapping "cell": one thread per cell; "sa": one thread per (state, action) + wave max-reduce.
+    """
+
+    def __init__(self, grids, model: str = "auto", gamma: float = 0.99, tol: float = 1e-6,
+                 slip_p: float | None = None, max_sweeps: int = 10000, dtype: str = "f32",
+                 method: str = "fused", mapping: str = "cell", device: int = 0, stream=None):
+        cells, enc = to_cells(grids)
+        if model == "auto":
+            model = infer_model(cells)
+        if model not in MODELS:
+            raise ValueError(f"unknown model {model!r}")
+        if model == "doorkey" and enc is not None:
+            check_doorkey_encoding(enc)
+        self.L = _lib.load()
+        _lib.require_gpu()
+        B, H, W = cells.shape
+        self.model, self.B, self.W, self.H = model, B, W, H
+        self.S = n_states(model, W, H)
+        self.dtype = dtype
+        self.np_dtype = np.float32 if dtype == "f32" else np.float64
+        self.tol = float(tol)
+        self.max_sweeps = int(max_sweeps)
+        d = _lib.ViDesc()
+        d.model = MODELS[model]
+        d.dtype = DTYPES[dtype]
+        d.method = METHODS[method]
+        d.mapping = MAPPINGS[mapping]
+        d.B, d.W, d.H = B, W, H
+        d.max_sweeps = self.max_sweeps
+        d.device = device
+        d.gamma = float(gamma)
+        d.tol = float(tol)
+        d.slip_p = -1.0 if slip_p is None else float(slip_p)
+        self.desc = d
+        h = ctypes.c_void_p()
+        _lib.check(self.L.mgdp_vi_create(ctypes.byref(d), ctypes.byref(h)), "mgdp_vi_create")
+        self.h = h
+        if stream is not None:
+            _lib.check(self.L.mgdp_vi_set_stream(h, ctypes.c_void_p(int(stream))), "mgdp_vi_set_stream")
+        cells = np.ascontiguousarray(cells, np.uint8)
+        _lib.check(self.L.mgdp_vi_load_cells(h, _lib.ptr(cells)), "mgdp_vi_load_cells")
+        self.sweeps = 0
+        self.converged = False
+        self.dv = float("nan")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.mgdp_vi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- single-device solve
+    def solve(self) -> int:
+        k = ctypes.c_int32(0)
+        dv = ctypes.c_double(0)
+        conv = ctypes.c_int32(0)
+        _lib.check(self.L.mgdp_vi_solve(self.h, ctypes.byref(k), ctypes.byref(dv), ctypes.byref(conv)),
+                   "mgdp_vi_solve")
+        self.sweeps, self.dv, self.converged = k.value, dv.value, bool(conv.value)
+        return self.sweeps
+
+    # -- multi-device protocol pieces (see distributed.py)
+    def reset(self):
+        _lib.check(self.L.mgdp_vi_reset(self.h), "mgdp_vi_reset")
+
+    def run_local(self) -> int:
+        k = ctypes.c_int32(0)
+        _lib.check(self.L.mgdp_vi_run_local(self.h, ctypes.byref(k)), "mgdp_vi_run_local")
+        return k.value
+
+    def run_to(self, k: int) -> float:
+        dv = ctypes.c_double(0)
+        _lib.check(self.L.mgdp_vi_run_to(self.h, int(k), ctypes.byref(dv)), "mgdp_vi_run_to")
+        return dv.value
+
+    def sweep(self) -> float:
+        dv = ctypes.c_double(0)
+        _lib.check(self.L.mgdp_vi_sweep(self.h, ctypes.byref(dv)), "mgdp_vi_sweep")
+        return dv.value
+
+    def finish(self, sweeps: int, dv: float):
+        _lib.check(self.L.mgdp_vi_finish(self.h, int(sweeps)), "mgdp_vi_finish")
+        self.sweeps, self.dv = int(sweeps), float(dv)
+        self.converged = dv < self.tol
+
+    # -- results
+    def values(self) -> np.ndarray:
+        V = np.empty((self.B, self.S), self.np_dtype)
+        _lib.check(self.L.mgdp_vi_get_values(self.h, _lib.ptr(V)), "mgdp_vi_get_values")
+        return V
+
+    def policy(self) -> np.ndarray:
+        pi = np.empty((self.B, self.S), np.int8)
+        _lib.check(self.L.mgdp_vi_get_policy(self.h, _lib.ptr(pi)), "mgdp_vi_get_policy")
+        return pi
+
+    def dv_trace(self) -> np.ndarray:
+        t = np.zeros(self.sweeps, np.float64)
+        _lib.check(self.L.mgdp_vi_get_dv_trace(self.h, _lib.ptr(t), self.sweeps), "mgdp_vi_get_dv_trace")
+        return t
+
+    def result(self) -> VIResult:
+        return VIResult(self.values(), self.policy(), self.sweeps, self.converged, self.dv, self.model,
+                        self.W, self.H)
+
+    def enable_timing(self, on: bool = True):
+        _lib.check(self.L.mgdp_vi_enable_timing(self.h, int(on)), "mgdp_vi_enable_timing")
+
+    def kernel_time(self) -> tuple[float, int]:
+        ms = ctypes.c_double(0)
+        n = ctypes.c_int64(0)
+        _lib.check(self.L.mgdp_vi_kernel_time(self.h, ctypes.byref(ms), ctypes.byref(n)), "mgdp_vi_kernel_time")
+        return ms.value, n.value
+
+    @property
+    def updates_per_sweep(self) -> int:
+        return self.B * self.S * n_actions(self.model)
+
+
+def value_iteration(grids, **kwargs) -> VIResult:
+    """Solve value iteration for one grid or a batch (one global stopping rule) on one GPU."""
+    vi = ValueIteration(grids, **kwargs)
+    try:
+        vi.solve()
+        return vi.result()
+    finally:
+        vi.close()

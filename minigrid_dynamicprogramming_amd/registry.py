@@ -1,0 +1,67 @@
+"""Env registry: the reference's registered ids for the target families (minigrid/__init__.py:23-1130).
+
+make(id, **kwargs) constructs the env class with the registered kwargs, like gymnasium.make's
+EnvSpec.make (without gymnasium's checker wrappers).  When gymnasium is importable the same ids are
+also registered with it under this package's entry points.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+from ._gym import HAVE_GYMNASIUM
+from .core import Wall
+
+
+@dataclass
+class EnvSpec:
+    id: str
+    entry_point: str
+    kwargs: dict = field(default_factory=dict)
+    nondeterministic: bool = False
+
+    def make(self, **kwargs):
+        from . import envs
+
+        cls = getattr(envs, self.entry_point.split(":")[1])
+        return cls(**{**self.kwargs, **kwargs})
+
+
+registry: dict[str, EnvSpec] = {}
+
+
+def register(id: str, entry_point: str, kwargs: dict | None = None):
+    registry[id] = EnvSpec(id, entry_point, dict(kwargs or {}))
+    if HAVE_GYMNASIUM:  # pragma: no cover
+        import gymnasium
+
+        gymnasium.register(id=id, entry_point=entry_point, kwargs=dict(kwargs or {}))
+
+
+def make(id: str, **kwargs):
+    if id not in registry:
+        raise KeyError(f"unknown env id {id!r}; registered: {sorted(registry)}")
+    return registry[id].make(**kwargs)
+
+
+def register_minigrid_envs():
+    ep = "minigrid_dynamicprogramming_amd.envs:"
+    # LavaCrossing / SimpleCrossing, minigrid/__init__.py:34-83
+    for s, n in ((9, 1), (9, 2), (9, 3), (11, 5)):
+        register(f"MiniGrid-LavaCrossingS{s}N{n}-v0", ep + "CrossingEnv", {"size": s, "num_crossings": n})
+        register(f"MiniGrid-SimpleCrossingS{s}N{n}-v0", ep + "CrossingEnv",
+                 {"size": s, "num_crossings": n, "obstacle_type": Wall})
+    # DoorKey, :103-125
+    for s in (5, 6, 8, 16):
+        register(f"MiniGrid-DoorKey-{s}x{s}-v0", ep + "DoorKeyEnv", {"size": s})
+    # Empty, :168-201
+    register("MiniGrid-Empty-5x5-v0", ep + "EmptyEnv", {"size": 5})
+    register("MiniGrid-Empty-Random-5x5-v0", ep + "EmptyEnv", {"size": 5, "agent_start_pos": None})
+    register("MiniGrid-Empty-6x6-v0", ep + "EmptyEnv", {"size": 6})
+    register("MiniGrid-Empty-Random-6x6-v0", ep + "EmptyEnv", {"size": 6, "agent_start_pos": None})
+    register("MiniGrid-Empty-8x8-v0", ep + "EmptyEnv")
+    register("MiniGrid-Empty-16x16-v0", ep + "EmptyEnv", {"size": 16})
+    # FourRooms, :223-226
+    register("MiniGrid-FourRooms-v0", ep + "FourRoomsEnv")
+
+
+register_minigrid_envs()

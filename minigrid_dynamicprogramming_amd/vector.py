@@ -1,0 +1,154 @@
+"""Batched MiniGrid stepping on one GPU: B envs resident in HBM, one HIP launch per step.
+
+The reference vectorises with gymnasium's in-process SyncVectorEnv (tests/test_envs.py:310-330),
+which loops MiniGridEnv.step (minigrid_env.py:520-590) serially.  Here every env's grid planes and
+agent state live in HBM and one envs_step_kernel launch advances all of them (csrc/envs.hip).
+Grids are generated on the host by the reference-exact generators (envs.py) and uploaded on reset.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .registry import make
+
+
+class MiniGridVecEnv:
+    """B independent envs of one registered id (same W, H), stepped together on one GPU.
+
+    step(actions) -> (obs, reward, terminated, truncated, info) with obs = {"image": (B,V,V,3) uint8,
+    "direction": (B,) int32, "mission": [str]*B}.  autoreset=True resets finished envs right after
+    the step with their next seed (the returned obs is then the reset observation and the final
+    observation is in info["final_obs_image"]).
+    """
+
+    def __init__(self, env_id: str, num_envs: int, device: int = 0, autoreset: bool = False, **kwargs):
+        self.env_id = env_id
+        self.num_envs = int(num_envs)
+        self.autoreset = autoreset
+        self._gen = make(env_id, **kwargs)  # host-side generator (one instance reused per seed)
+        self.W, self.H = self._gen.width, self._gen.height
+        self.view = self._gen.agent_view_size
+        self.max_steps = self._gen.max_steps
+        self.see_through = self._gen.see_through_walls
+        self.mission = self._gen.mission
+        self.L = _lib.load()
+        _lib.require_gpu()
+        h = ctypes.c_void_p()
+        _lib.check(self.L.mgdp_envs_create(device, self.num_envs, self.W, self.H, self.view, ctypes.byref(h)),
+                   "mgdp_envs_create")
+        self.h = h
+        B, V = self.num_envs, self.view
+        self._obs = np.zeros((B, V, V, 3), np.uint8)
+        self._dir = np.zeros(B, np.int32)
+        self._rew = np.zeros(B, np.float64)
+        self._term = np.zeros(B, np.uint8)
+        self._trunc = np.zeros(B, np.uint8)
+        self._status = np.zeros(B, np.int32)
+        self._seeds = np.zeros(B, np.int64)
+        self._next_seed = 0
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.mgdp_envs_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- raw state upload
+    def load(self, enc: np.ndarray, agent: np.ndarray, max_steps=None, see_through=None, mask=None):
+        """Upload grids (B, W, H, 3) x-major encodings and agents (B, 3) = (x, y, dir)."""
+        B = self.num_envs
+        enc = np.ascontiguousarray(enc, np.uint8)
+        agent = np.ascontiguousarray(agent, np.int32)
+        assert enc.shape == (B, self.W, self.H, 3) and agent.shape == (B, 3)
+        ms = np.full(B, self.max_steps if max_steps is None else 0, np.int32)
+        if max_steps is not None:
+            ms[:] = np.asarray(max_steps, np.int32)
+        see = np.full(B, 1 if self.see_through else 0, np.uint8)
+        if see_through is not None:
+            see[:] = np.asarray(see_through, np.uint8)
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        _lib.check(self.L.mgdp_envs_load(self.h, _lib.ptr(enc), _lib.ptr(agent), _lib.ptr(ms), _lib.ptr(see),
+                                         _lib.ptr(m)), "mgdp_envs_load")
+
+    def _generate(self, seeds):
+        encs, agents = [], []
+        for s in seeds:
+            e, a = self._gen.generate(seed=int(s))
+            encs.append(e)
+            agents.append(a)
+        return np.stack(encs), np.array(agents, np.int32)
+
+    def observe(self):
+        _lib.check(self.L.mgdp_envs_observe(self.h, _lib.ptr(self._obs), _lib.ptr(self._dir)), "mgdp_envs_observe")
+        return self._obs_dict()
+
+    def _obs_dict(self):
+        return {"image": self._obs.copy(), "direction": self._dir.copy(), "mission": [self.mission] * self.num_envs}
+
+    # ---------------------------------------------------------------- gym-style API
+    def reset(self, seed: int | None = None):
+        if seed is None:
+            seed = int(np.random.SeedSequence().generate_state(1)[0])
+        self._seeds = np.arange(self.num_envs, dtype=np.int64) + int(seed)
+        self._next_seed = int(seed) + self.num_envs
+        enc, agent = self._generate(self._seeds)
+        self.load(enc, agent)
+        return self.observe(), {"seeds": self._seeds.copy()}
+
+    def step(self, actions):
+        a = np.ascontiguousarray(np.asarray(actions).reshape(self.num_envs), np.int32)
+        rc = self.L.mgdp_envs_step(self.h, _lib.ptr(a), _lib.ptr(self._obs), _lib.ptr(self._dir),
+                                   _lib.ptr(self._rew), _lib.ptr(self._term), _lib.ptr(self._trunc),
+                                   _lib.ptr(self._status))
+        if rc == _lib.MGDP_E_ACTION:
+            bad = np.flatnonzero(self._status == _lib.MGDP_E_ACTION)
+            raise ValueError(f"Unknown action: {actions[bad[0]] if len(bad) else actions} (env {bad.tolist()})")
+        _lib.check(rc, "mgdp_envs_step")
+        obs = self._obs_dict()
+        term = self._term.astype(bool)
+        trunc = self._trunc.astype(bool)
+        info = {}
+        if self.autoreset:
+            done = term | trunc
+            if done.any():
+                info["final_obs_image"] = obs["image"].copy()
+                idx = np.flatnonzero(done)
+                seeds = self._next_seed + np.arange(len(idx))
+                self._next_seed += len(idx)
+                self._seeds[idx] = seeds
+                enc = np.zeros((self.num_envs, self.W, self.H, 3), np.uint8)
+                agent = np.zeros((self.num_envs, 3), np.int32)
+                e, ag = self._generate(seeds)
+                enc[idx], agent[idx] = e, ag
+                mask = done.astype(np.uint8)
+                self.load(enc, agent, mask=mask)
+                obs = self.observe()
+        return obs, self._rew.copy(), term, trunc, info
+
+    def step_device(self, actions, obs, direction, reward, terminated, truncated, status):
+        """Zero-copy step on device buffers (torch CUDA tensors or raw pointers), asynchronous."""
+        _lib.check(self.L.mgdp_envs_step_device(self.h, _lib.ptr(actions), _lib.ptr(obs), _lib.ptr(direction),
+                                                _lib.ptr(reward), _lib.ptr(terminated), _lib.ptr(truncated),
+                                                _lib.ptr(status)), "mgdp_envs_step_device")
+
+    def set_stream(self, stream):
+        _lib.check(self.L.mgdp_envs_set_stream(self.h, ctypes.c_void_p(int(stream) if stream else 0)),
+                   "mgdp_envs_set_stream")
+
+    def get_state(self):
+        B = self.num_envs
+        enc = np.zeros((B, self.W, self.H, 3), np.uint8)
+        agent = np.zeros((B, 3), np.int32)
+        carry = np.zeros((B, 2), np.int32)
+        sc = np.zeros(B, np.int32)
+        _lib.check(self.L.mgdp_envs_get_state(self.h, _lib.ptr(enc), _lib.ptr(agent), _lib.ptr(carry), _lib.ptr(sc)),
+                   "mgdp_envs_get_state")
+        return {"enc": enc, "agent": agent, "carry": carry, "step_count": sc}

@@ -365,9 +365,9 @@ int orc_step(int W, int H, uint8_t *ty, uint8_t *co, uint8_t *st, int32_t *state
     *reward = 0.0;
     *terminated = 0;
     *truncated = 0;
-    if (action < 0 || action > 6) return -1;
     int fx = ax + DX[d], fy = ay + DY[d];
-    if (fx < 0 || fy < 0 || fx >= W || fy >= H) return -2;
+    if (fx < 0 || fy < 0 || fx >= W || fy >= H) return -2; /* Grid.get assertion, :533 */
+    if (action < 0 || action > 6) return -1;              /* ValueError, :579-580 */
     int fi = fy * W + fx;
     int ft = ty[fi];
     int fnone = ft == T_EMPTY;
