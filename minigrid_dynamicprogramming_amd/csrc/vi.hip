@@ -20,7 +20,7 @@
 //                     whole solve; many sweeps per launch, one __syncthreads per sweep.
 //   vi_sweep_kernel   one Jacobi sweep of every grid: per grid, V'[grid] is staged HBM->LDS with
 //                     16-B coalesced loads, updated from LDS, written back LDS->HBM.
-//   vi_reduce_kernel  max over grids of (kenv, dvenv).
+//   vi_stream_kernel  one Jacobi sweep of every grid without LDS staging (MAP_CELL, sweep method).
 // Thread mappings (template MAP): MGDP_MAP_CELL = one thread per cell updating its 4 (XYD) or
 // 16 (DoorKey) states from 16-B LDS vectors; MGDP_MAP_SA = one thread per (state, action),
 // 8 lanes per state, wave shuffle max-reduce with the lowest action index winning ties.
@@ -82,19 +82,49 @@ __device__ __forceinline__ T block_max(T v, T *slots, int parity) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Per-cell topology.  Cell types never change during a solve, so a thread that owns a cell can
+// resolve its transition structure once (from LDS or HBM) and keep it in registers for every sweep.
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+struct XydTopo {
+    int valid;       // agent may stand here (empty / floor)
+    uint32_t term;   // bit d: forward from dir d enters a terminal cell (goal / lava)
+    int nbi[4];      // V index read by forward from dir d (own state when blocked or terminal)
+    T tq[4];         // terminal forward value: 1 (goal, R = 1) or 0 (lava)
+};
+
+template <typename T>
+__device__ __forceinline__ XydTopo<T> xyd_topo(const uint8_t *cl, const Geo &geo, int c) {
+    XydTopo<T> tp;
+    tp.valid = xyd_free(cl[c]);
+    tp.term = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const int cfr = c + geo.off[d];
+        const int tf = tp.valid ? cl[cfr] : T_WALL;  // valid cells are interior (closed border)
+        tp.tq[d] = (T)0;
+        tp.nbi[d] = c * 4 + d;
+        if (tf == T_GOAL) { tp.term |= 1u << d; tp.tq[d] = (T)1; }
+        else if (tf == T_LAVA) { tp.term |= 1u << d; }
+        else if (xyd_free(tf)) tp.nbi[d] = cfr * 4 + d;
+    }
+    return tp;
+}
+
 // One cell of the XYD model (4 states, actions 0..6).  Returns max |dV| over the cell's states.
 // Q_det: left/right/self (= pickup/drop/toggle/done) = g*V, forward per minigrid_env.py:546-553.
-// ------------------------------------------------------------------------------------------------
-template <typename T, bool SLIP, bool WRITE_V>
-__device__ __forceinline__ T xyd_cell(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
-                                      const T *Vin, T *Vout, int8_t *pis, int c) {
-    const int t = cl[c];
-    if (!xyd_free(t)) {
+template <typename T, bool SLIP, bool WRITE_V, bool WRITE_PI>
+__device__ __forceinline__ T xyd_update(const XydTopo<T> &tp, const Coef<T> &cf, const T *Vin, T *Vout,
+                                        int8_t *pis, int c) {
+    if (!tp.valid) {
         if (WRITE_V) *reinterpret_cast<V4<T> *>(Vout + c * 4) = V4<T>{{(T)0, (T)0, (T)0, (T)0}};
-        *reinterpret_cast<int32_t *>(pis + c * 4) = -1;
+        if (WRITE_PI) *reinterpret_cast<int32_t *>(pis + c * 4) = -1;
         return (T)0;
     }
     const V4<T> own = *reinterpret_cast<const V4<T> *>(Vin + c * 4);
+    T nbv[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) nbv[d] = Vin[tp.nbi[d]];
     T gv[4];
 #pragma unroll
     for (int d = 0; d < 4; ++d) gv[d] = cf.g * own.v[d];
@@ -103,13 +133,7 @@ __device__ __forceinline__ T xyd_cell(const Geo &geo, const Coef<T> &cf, const u
     T dv = (T)0;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-        const int cfr = c + geo.off[d];
-        const int tf = cl[cfr];
-        T qF;
-        if (tf == T_GOAL) qF = (T)1;
-        else if (tf == T_LAVA) qF = (T)0;
-        else if (xyd_free(tf)) qF = cf.g * Vin[cfr * 4 + d];
-        else qF = gv[d];
+        const T qF = ((tp.term >> d) & 1u) ? tp.tq[d] : cf.g * nbv[d];
         const T qL = gv[(d + 3) & 3], qR = gv[(d + 1) & 3], qS = gv[d];
         T best;
         int arg;
@@ -137,18 +161,45 @@ __device__ __forceinline__ T xyd_cell(const Geo &geo, const Coef<T> &cf, const u
         dv = tmax(dv, tabs_diff(best, own.v[d]));
     }
     if (WRITE_V) *reinterpret_cast<V4<T> *>(Vout + c * 4) = out;
-    *reinterpret_cast<uint32_t *>(pis + c * 4) = pk;
+    if (WRITE_PI) *reinterpret_cast<uint32_t *>(pis + c * 4) = pk;
     return dv;
 }
 
-// ------------------------------------------------------------------------------------------------
+// DoorKey cell topology: own type, the 4 front-cell types and neighbour V offsets.
+struct DkTopo {
+    int t;
+    int tf[4];
+    int nb[4];  // V index of (front cell, dir d, has_key 0, door_open 0)
+};
+
+__device__ __forceinline__ DkTopo dk_topo(const uint8_t *cl, const Geo &geo, int c) {
+    DkTopo tp;
+    tp.t = cl[c];
+    const bool inner = tp.t != T_WALL && tp.t != T_GOAL && tp.t != T_LAVA;  // walkable for some (hk, door)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const int cfr = inner ? c + geo.off[d] : c;
+        tp.tf[d] = inner ? cl[cfr] : T_WALL;
+        tp.nb[d] = cfr * 16 + d * 4;
+    }
+    return tp;
+}
+
 // One cell of the DoorKey product model: 16 states l = (dir*2 + has_key)*2 + door_open,
 // action lanes left, right, forward, pickup, toggle (world_object.py:185-195, 244).
-// ------------------------------------------------------------------------------------------------
-template <typename T, bool WRITE_V>
-__device__ __forceinline__ T dk_cell(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
-                                     const T *Vin, T *Vout, int8_t *pis, int c) {
-    const int t = cl[c];
+template <typename T, bool WRITE_V, bool WRITE_PI>
+__device__ __forceinline__ T dk_update(const DkTopo &tp, const Coef<T> &cf, const T *Vin, T *Vout,
+                                       int8_t *pis, int c) {
+    const int t = tp.t;
+    if (t == T_WALL || t == T_GOAL || t == T_LAVA) {  // no (has_key, door_open) makes it walkable
+        if (WRITE_V) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                *reinterpret_cast<V4<T> *>(Vout + c * 16 + 4 * q) = V4<T>{{(T)0, (T)0, (T)0, (T)0}};
+        }
+        if (WRITE_PI) *reinterpret_cast<uint4 *>(pis + c * 16) = make_uint4(~0u, ~0u, ~0u, ~0u);
+        return (T)0;
+    }
     const T *vc = Vin + c * 16;
     T own[16];
 #pragma unroll
@@ -165,9 +216,8 @@ __device__ __forceinline__ T dk_cell(const Geo &geo, const Coef<T> &cf, const ui
     T dv = (T)0;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-        const int cfr = c + geo.off[d];
-        const int tf = cl[cfr];
-        const V4<T> nb = *reinterpret_cast<const V4<T> *>(Vin + cfr * 16 + d * 4);
+        const int tf = tp.tf[d];
+        const V4<T> nb = *reinterpret_cast<const V4<T> *>(Vin + tp.nb[d]);
 #pragma unroll
         for (int hk = 0; hk < 2; ++hk) {
 #pragma unroll
@@ -206,12 +256,14 @@ __device__ __forceinline__ T dk_cell(const Geo &geo, const Coef<T> &cf, const ui
             *reinterpret_cast<V4<T> *>(Vout + c * 16 + 4 * q) =
                 V4<T>{{outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]}};
     }
-    uint32_t w[4];
+    if (WRITE_PI) {
+        uint32_t w[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-        w[q] = (uint32_t)(uint8_t)outp[4 * q] | ((uint32_t)(uint8_t)outp[4 * q + 1] << 8) |
-               ((uint32_t)(uint8_t)outp[4 * q + 2] << 16) | ((uint32_t)(uint8_t)outp[4 * q + 3] << 24);
-    *reinterpret_cast<uint4 *>(pis + c * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+        for (int q = 0; q < 4; ++q)
+            w[q] = (uint32_t)(uint8_t)outp[4 * q] | ((uint32_t)(uint8_t)outp[4 * q + 1] << 8) |
+                   ((uint32_t)(uint8_t)outp[4 * q + 2] << 16) | ((uint32_t)(uint8_t)outp[4 * q + 3] << 24);
+        *reinterpret_cast<uint4 *>(pis + c * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
     return dv;
 }
 
@@ -314,8 +366,10 @@ __device__ __forceinline__ T sweep_lds(const Geo &geo, const Coef<T> &cf, const 
     if (MAP == MGDP_MAP_SA) return sa_sweep<T, MODEL, SLIP, WRITE_V>(geo, cf, cl, Vin, Vout, pis);
     T dv = (T)0;
     for (int c = threadIdx.x; c < geo.HW; c += blockDim.x) {
-        if (MODEL == MGDP_MODEL_XYD) dv = tmax(dv, xyd_cell<T, SLIP, WRITE_V>(geo, cf, cl, Vin, Vout, pis, c));
-        else dv = tmax(dv, dk_cell<T, WRITE_V>(geo, cf, cl, Vin, Vout, pis, c));
+        if (MODEL == MGDP_MODEL_XYD)
+            dv = tmax(dv, xyd_update<T, SLIP, WRITE_V, true>(xyd_topo<T>(cl, geo, c), cf, Vin, Vout, pis, c));
+        else
+            dv = tmax(dv, dk_update<T, WRITE_V, true>(dk_topo(cl, geo, c), cf, Vin, Vout, pis, c));
     }
     return dv;
 }
@@ -331,6 +385,16 @@ __device__ __forceinline__ void zero16(void *dst, int bytes) {
     for (int i = threadIdx.x; i < (bytes >> 4); i += blockDim.x) d[i] = make_uint4(0, 0, 0, 0);
 }
 
+// Block-wide OR of a predicate with ONE barrier: one byte flag per wave, two parities so that a
+// flag set is rewritten only after every thread has passed the following barrier.
+__device__ __forceinline__ bool block_any(bool p, uint8_t *flags, int parity) {
+    const unsigned long long b = __ballot(p);
+    if ((threadIdx.x & 63) == 0) flags[parity * 16 + (threadIdx.x >> 6)] = b != 0ull;
+    __syncthreads();
+    const uint4 f = *reinterpret_cast<const uint4 *>(flags + parity * 16);
+    return (f.x | f.y | f.z | f.w) != 0u;
+}
+
 struct Smem {
     int v_bytes, pi_bytes, cells_bytes, slot_bytes;
     __host__ __device__ int total() const { return 2 * v_bytes + pi_bytes + cells_bytes + slot_bytes; }
@@ -341,19 +405,27 @@ __host__ __device__ inline Smem smem_layout(int S, int HWp, int tsize) {
     m.v_bytes = S * tsize;  // S is a multiple of 4 -> 16-B multiple for f32, f64
     m.pi_bytes = (S + 15) / 16 * 16;
     m.cells_bytes = HWp;
-    m.slot_bytes = 2 * 16 * 8;
+    m.slot_bytes = 2 * 16 * 8 + 32;  // block_max slots [2][16] + block_any flags [2][16]
     return m;
 }
 
+constexpr int kRedShards = 64;  // fused-kernel reduction: [2 slots][64 shards][kmax, dv bits, kmin, -]
+
 // ------------------------------------------------------------------------------------------------
-// Fused solve: blockIdx.x = grid index.  k_target < 0: sweep until this grid's own max|dV| < tol
-// (or max_sweeps).  k_target >= 0: sweep until exactly k_target sweeps have been done.
+// Fused solve: blockIdx.x = grid index; the grid's cells, both V buffers and pi stay in LDS for
+// every sweep of the launch.  k_target < 0: sweep until this grid's own max|dV| < tol (or
+// max_sweeps); k_target >= 0: sweep until exactly k_target sweeps are done.  fresh: start from
+// V_0 = 0 regardless of kenv/dvenv.  MAP_CELL with HW <= blockDim keeps each thread's cell
+// topology in registers for the whole launch (no LDS cell reads inside the sweep loop).
+// Per-sweep convergence test = block OR of (|dV| >= tol) (ballot + one byte per wave); the exact
+// max |dV| is reduced once, after the last sweep.  Every block folds (k, dV) into reduction slot
+// `slot` with sharded atomics; block 0 re-arms the other slot for the next launch.
 // ------------------------------------------------------------------------------------------------
 template <typename T, int MODEL, bool SLIP, int MAP>
 __global__ void __launch_bounds__(1024)
 vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
-                int k_target) {
+                unsigned long long *__restrict__ red, int slot, int k_target, int fresh) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int e = blockIdx.x;
     const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T));
@@ -362,51 +434,91 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
     int8_t *pis = reinterpret_cast<int8_t *>(smem + 2 * L.v_bytes);
     uint8_t *cl = reinterpret_cast<uint8_t *>(smem + 2 * L.v_bytes + L.pi_bytes);
     T *slots = reinterpret_cast<T *>(smem + 2 * L.v_bytes + L.pi_bytes + L.cells_bytes);
+    uint8_t *flags = reinterpret_cast<uint8_t *>(smem + 2 * L.v_bytes + L.pi_bytes + L.cells_bytes + 256);
 
-    int k = kenv[e];
-    double dvl = dvenv[e];
+    if (blockIdx.x == 0) {
+        unsigned long long *o = red + (slot ^ 1) * kRedShards * 4;
+        for (int i = threadIdx.x; i < kRedShards * 4; i += blockDim.x) o[i] = (i & 3) == 2 ? 0x7fffffffull : 0ull;
+    }
+    int k = fresh ? 0 : kenv[e];
+    double dvl = fresh ? 0.0 : dvenv[e];
     const bool work = k_target < 0 ? (!(k > 0 && dvl < geo.tol) && k < geo.max_sweeps) : (k < k_target);
-    if (!work) return;
+    if (work) {
+        const long long vb = (long long)e * geo.S;
+        copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
+        if (k == 0) zero16(V0, L.v_bytes);
+        else copy16(V0, V + vb, L.v_bytes);
+        if (threadIdx.x < 32) flags[threadIdx.x] = 0;
+        __syncthreads();
 
-    const long long vb = (long long)e * geo.S;
-    copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
-    if (k == 0) zero16(V0, L.v_bytes);
-    else copy16(V0, V + vb, L.v_bytes);
-    __syncthreads();
-
-    int cur = 0, parity = 0;
-    while (true) {
-        const T *Vin = cur ? V1 : V0;
-        T *Vout = cur ? V0 : V1;
-        const T dv = sweep_lds<T, MODEL, SLIP, MAP, true>(geo, cf, cl, Vin, Vout, pis);
-        const T bdv = block_max(dv, slots, parity);
-        parity ^= 1;
-        cur ^= 1;
-        ++k;
-        dvl = (double)bdv;
-        if (k_target < 0) {
-            if (dvl < geo.tol || k >= geo.max_sweeps) break;
-        } else if (k >= k_target) {
-            break;
+        const bool fast = MAP == MGDP_MAP_CELL && geo.HW <= (int)blockDim.x;
+        const int c = threadIdx.x;
+        const bool own = c < geo.HW;
+        XydTopo<T> xt;
+        DkTopo dt;
+        if (fast && own) {
+            if (MODEL == MGDP_MODEL_XYD) xt = xyd_topo<T>(cl, geo, c);
+            else dt = dk_topo(cl, geo, c);
+        }
+        int cur = 0, parity = 0;
+        T diff = (T)0;
+        while (true) {
+            const T *Vin = cur ? V1 : V0;
+            T *Vout = cur ? V0 : V1;
+            if (fast) {
+                if (own) {
+                    if (MODEL == MGDP_MODEL_XYD) diff = xyd_update<T, SLIP, true, true>(xt, cf, Vin, Vout, pis, c);
+                    else diff = dk_update<T, true, true>(dt, cf, Vin, Vout, pis, c);
+                }
+            } else {
+                diff = sweep_lds<T, MODEL, SLIP, MAP, true>(geo, cf, cl, Vin, Vout, pis);
+            }
+            cur ^= 1;
+            ++k;
+            if (k_target < 0) {
+                const bool more = block_any((double)diff >= geo.tol, flags, parity);
+                parity ^= 1;
+                if (!more || k >= geo.max_sweeps) break;
+            } else {
+                __syncthreads();
+                if (k >= k_target) break;
+            }
+        }
+        dvl = (double)block_max(diff, slots, 0);
+        copy16(V + vb, cur ? V1 : V0, L.v_bytes);
+        {   // S is a multiple of 4, so pi rows are 4-byte aligned
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(pis);
+            uint32_t *dst = reinterpret_cast<uint32_t *>(pi + vb);
+            for (int i = threadIdx.x; i < (geo.S >> 2); i += blockDim.x) dst[i] = src[i];
+        }
+        if (threadIdx.x == 0) {
+            kenv[e] = k;
+            dvenv[e] = dvl;
         }
     }
-    copy16(V + vb, cur ? V1 : V0, L.v_bytes);
-    {   // S is a multiple of 4, so pi rows are 4-byte aligned
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(pis);
-        uint32_t *dst = reinterpret_cast<uint32_t *>(pi + vb);
-        for (int i = threadIdx.x; i < (geo.S >> 2); i += blockDim.x) dst[i] = src[i];
-    }
     if (threadIdx.x == 0) {
-        kenv[e] = k;
-        dvenv[e] = dvl;
+        unsigned long long *r = red + (slot * kRedShards + (e & (kRedShards - 1))) * 4;
+        atomicMax(r + 0, (unsigned long long)k);
+        atomicMax(r + 1, (unsigned long long)__double_as_longlong(dvl));
+        atomicMin(r + 2, (unsigned long long)k);
     }
 }
 
+// Early exit of a speculatively enqueued sweep: the previous sweep already met the rule.
+__device__ __forceinline__ bool prev_sweep_converged(const unsigned long long *shards, int k, double tol) {
+    if (k <= 1) return false;
+    const unsigned long long *prev = shards + (long long)(k - 2) * 8;
+    double m = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m = fmax(m, __longlong_as_double((long long)prev[i]));
+    return m < tol;
+}
+
 // ------------------------------------------------------------------------------------------------
-// One Jacobi sweep (sweep index k, 1-based) of every grid, V double-buffered in HBM.
-// check_prev: skip the whole launch when the previous sweep's global max|dV| was already < tol
-// (lets the host enqueue sweeps speculatively without a sync per sweep).
-// POLICY: evaluate only, write pi (used once after convergence on V_{k-1}).
+// One Jacobi sweep (index k, 1-based) of every grid, V double-buffered in HBM, MAP_SA mapping:
+// per grid, V'[grid] is staged HBM -> LDS with 16-B loads (the LDS tile of the neighbourhood),
+// updated by (state, action) lanes, written back LDS -> HBM.  check_prev: skip when the previous
+// sweep's global max|dV| was already < tol.  POLICY: evaluate only, write pi.
 // ------------------------------------------------------------------------------------------------
 template <typename T, int MODEL, bool SLIP, int MAP, bool POLICY>
 __global__ void __launch_bounds__(256)
@@ -414,13 +526,7 @@ vi_sweep_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, const T 
                 T *__restrict__ Vout, int8_t *__restrict__ pi, unsigned long long *__restrict__ shards,
                 int k, int check_prev) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    if (check_prev && k > 1) {
-        const unsigned long long *prev = shards + (long long)(k - 2) * 8;
-        double m = 0.0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) m = fmax(m, __longlong_as_double((long long)prev[i]));
-        if (m < geo.tol) return;
-    }
+    if (check_prev && prev_sweep_converged(shards, k, geo.tol)) return;
     const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T));
     T *Vi = reinterpret_cast<T *>(smem);
     T *Vo = reinterpret_cast<T *>(smem + L.v_bytes);
@@ -453,31 +559,39 @@ vi_sweep_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, const T 
     }
 }
 
-__global__ void __launch_bounds__(1024)
-vi_reduce_kernel(const int32_t *__restrict__ kenv, const double *__restrict__ dvenv, int B,
-                 unsigned long long *__restrict__ out) {
-    __shared__ int ks[16], kn[16];
-    __shared__ double ds[16];
-    int km = 0, kmin = 0x7fffffff;
-    double dm = 0.0;
-    for (int i = threadIdx.x; i < B; i += blockDim.x) {
-        km = max(km, kenv[i]);
-        kmin = min(kmin, kenv[i]);
-        dm = fmax(dm, dvenv[i]);
+// ------------------------------------------------------------------------------------------------
+// One Jacobi sweep, MAP_CELL mapping, streaming: one thread per cell, no LDS staging.  The wave's
+// own V rows are read with 16-B loads (coalesced), front-cell values and types are gathered from
+// L1/L2 (they are the neighbouring rows of the same or adjacent waves), new V leaves with 16-B
+// stores.  Chunks of `blk` cells of one grid are distributed grid-stride over the launch.
+// ------------------------------------------------------------------------------------------------
+template <typename T, int MODEL, bool SLIP, bool POLICY>
+__global__ void __launch_bounds__(256)
+vi_stream_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, const T *__restrict__ Vin,
+                 T *__restrict__ Vout, int8_t *__restrict__ pi, unsigned long long *__restrict__ shards,
+                 int k, int check_prev, int bpe, int nchunks) {
+    __shared__ T slots[32];
+    if (check_prev && prev_sweep_converged(shards, k, geo.tol)) return;
+    T acc = (T)0;
+    for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+        const int e = ch / bpe;
+        const int c = (ch - e * bpe) * (int)blockDim.x + (int)threadIdx.x;
+        if (c < geo.HW) {
+            const uint8_t *ce = cells + (long long)e * geo.HWp;
+            const long long vb = (long long)e * geo.S;
+            if (MODEL == MGDP_MODEL_XYD)
+                acc = tmax(acc, xyd_update<T, SLIP, !POLICY, POLICY>(xyd_topo<T>(ce, geo, c), cf, Vin + vb,
+                                                                     Vout + vb, pi + vb, c));
+            else
+                acc = tmax(acc, dk_update<T, !POLICY, POLICY>(dk_topo(ce, geo, c), cf, Vin + vb, Vout + vb,
+                                                              pi + vb, c));
+        }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        km = max(km, __shfl_xor(km, o));
-        kmin = min(kmin, __shfl_xor(kmin, o));
-        dm = fmax(dm, __shfl_xor(dm, o));
-    }
-    if ((threadIdx.x & 63) == 0) { ks[threadIdx.x >> 6] = km; kn[threadIdx.x >> 6] = kmin; ds[threadIdx.x >> 6] = dm; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) { km = max(km, ks[i]); kmin = min(kmin, kn[i]); dm = fmax(dm, ds[i]); }
-        out[0] = (unsigned long long)km;
-        out[1] = (unsigned long long)__double_as_longlong(dm);
-        out[2] = (unsigned long long)kmin;
+    if (!POLICY) {
+        const T bdv = block_max(acc, slots, 0);
+        if (threadIdx.x == 0 && shards)
+            atomicMax(shards + (long long)(k - 1) * 8 + (blockIdx.x & 7),
+                      (unsigned long long)__double_as_longlong((double)bdv));
     }
 }
 
@@ -502,7 +616,8 @@ struct mgdp_vi {
     unsigned long long *d_red = nullptr;
     unsigned long long *h_red = nullptr;  // pinned
     int cur = 0;        // V buffer holding the current V (sweep method)
-    int k_min = 0;      // min sweeps over grids after the last reduce (fused method)
+    int k_min = 0;      // min / max sweeps over grids after the last reduce (fused method)
+    int k_max = 0;
     bool k_done_valid = false;  // k_min / dv_red describe the current device state
     double dv_red = 0.0;
     int k_done = 0;     // sweeps completed by every grid (uniform after run_to / sweep)
@@ -516,6 +631,9 @@ struct mgdp_vi {
     int64_t launches = 0;
     int fused_block = 256;
     int sweep_grid = 2048;
+    int stream_blk = 256;   // threads per cell chunk of vi_stream_kernel
+    int red_slot = 0;       // fused reduction slot written by the next launch
+    int fresh = 1;          // next fused launch starts from V_0 = 0
 };
 
 namespace {
@@ -590,33 +708,48 @@ int launch_fused_t(mgdp_vi *vi, int k_target) {
     if (int rc = timed_begin(vi, -1)) return rc;
     hipLaunchKernelGGL(kern, dim3(vi->d.B), dim3(vi->fused_block), L.total(), vi->stream, g,
                        make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv,
-                       vi->d_dvenv, k_target);
+                       vi->d_dvenv, vi->d_red, vi->red_slot, k_target, vi->fresh);
     MGDP_HIP(hipGetLastError());
+    vi->fresh = 0;
     return timed_end(vi);
 }
 
 template <typename T, int MODEL, bool SLIP, int MAP>
 int launch_sweep_t(mgdp_vi *vi, int k, int check_prev, bool policy) {
     const Geo g = make_geo(vi);
-    const Smem L = smem_layout(vi->S, vi->HWp, sizeof(T));
-    const int grid = std::min(vi->d.B, vi->sweep_grid);
     const T *Vin = (const T *)vi->d_V[(k - 1) & 1];
     T *Vout = (T *)vi->d_V[k & 1];
-    if (policy) {
-        auto kern = vi_sweep_kernel<T, MODEL, SLIP, MAP, true>;
-        if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), L.total(), vi->stream, g, make_coef<T>(vi),
-                           vi->d_cells, Vin, Vout, vi->d_pi, (unsigned long long *)nullptr, k, 0);
-        MGDP_HIP(hipGetLastError());
-        return 0;
+    unsigned long long *sh = policy ? nullptr : vi->d_shards;
+    if (!policy)
+        if (int rc = timed_begin(vi, k)) return rc;
+    if (MAP == MGDP_MAP_CELL) {
+        const int blk = vi->stream_blk;
+        const int bpe = (vi->HW + blk - 1) / blk;
+        const int nchunks = vi->d.B * bpe;
+        const int grid = std::min(nchunks, 256 * (2048 / blk));
+        if (policy)
+            hipLaunchKernelGGL((vi_stream_kernel<T, MODEL, SLIP, true>), dim3(grid), dim3(blk), 0, vi->stream, g,
+                               make_coef<T>(vi), vi->d_cells, Vin, Vout, vi->d_pi, sh, k, 0, bpe, nchunks);
+        else
+            hipLaunchKernelGGL((vi_stream_kernel<T, MODEL, SLIP, false>), dim3(grid), dim3(blk), 0, vi->stream, g,
+                               make_coef<T>(vi), vi->d_cells, Vin, Vout, vi->d_pi, sh, k, check_prev, bpe, nchunks);
+    } else {
+        const Smem L = smem_layout(vi->S, vi->HWp, sizeof(T));
+        const int grid = std::min(vi->d.B, vi->sweep_grid);
+        if (policy) {
+            auto kern = vi_sweep_kernel<T, MODEL, SLIP, MAP, true>;
+            if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(256), L.total(), vi->stream, g, make_coef<T>(vi),
+                               vi->d_cells, Vin, Vout, vi->d_pi, sh, k, 0);
+        } else {
+            auto kern = vi_sweep_kernel<T, MODEL, SLIP, MAP, false>;
+            if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(256), L.total(), vi->stream, g, make_coef<T>(vi),
+                               vi->d_cells, Vin, Vout, vi->d_pi, sh, k, check_prev);
+        }
     }
-    auto kern = vi_sweep_kernel<T, MODEL, SLIP, MAP, false>;
-    if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
-    if (int rc = timed_begin(vi, k)) return rc;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), L.total(), vi->stream, g, make_coef<T>(vi),
-                       vi->d_cells, Vin, Vout, vi->d_pi, vi->d_shards, k, check_prev);
     MGDP_HIP(hipGetLastError());
-    return timed_end(vi);
+    return policy ? 0 : timed_end(vi);
 }
 
 // Dispatch on (dtype, model, slip, mapping).
@@ -649,18 +782,25 @@ struct SweepF {
     }
 };
 
+// Read back the reduction slot written by the last fused launch: max k, max dV, min k over grids.
 int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
-    hipLaunchKernelGGL(vi_reduce_kernel, dim3(1), dim3(1024), 0, vi->stream, vi->d_kenv, vi->d_dvenv,
-                       vi->d.B, vi->d_red);
-    MGDP_HIP(hipGetLastError());
-    MGDP_HIP(hipMemcpyAsync(vi->h_red, vi->d_red, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, vi->stream));
+    const size_t n = (size_t)kRedShards * 4;
+    MGDP_HIP(hipMemcpyAsync(vi->h_red, vi->d_red + (size_t)vi->red_slot * n, n * sizeof(unsigned long long),
+                            hipMemcpyDeviceToHost, vi->stream));
     MGDP_HIP(hipStreamSynchronize(vi->stream));
+    vi->red_slot ^= 1;
     if (int rc = timed_collect(vi, 1 << 30)) return rc;
-    long long bits = (long long)vi->h_red[1];
-    std::memcpy(&vi->dv_red, &bits, sizeof(double));
-    vi->k_min = (int)vi->h_red[2];
+    unsigned long long km = 0, dvb = 0, kmin = 0x7fffffffull;
+    for (int i = 0; i < kRedShards; ++i) {
+        km = std::max(km, vi->h_red[4 * i]);
+        dvb = std::max(dvb, vi->h_red[4 * i + 1]);
+        kmin = std::min(kmin, vi->h_red[4 * i + 2]);
+    }
+    std::memcpy(&vi->dv_red, &dvb, sizeof(double));  // non-negative doubles order like their bits
+    vi->k_min = (int)kmin;
+    vi->k_max = (int)km;
     vi->k_done_valid = true;
-    if (kmax) *kmax = (int32_t)vi->h_red[0];
+    if (kmax) *kmax = (int32_t)km;
     if (dvmax) *dvmax = vi->dv_red;
     return 0;
 }
@@ -774,11 +914,15 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
         set_error("grid too large for the LDS-resident kernels (%d B > 160 KiB)", L.total());
         return MGDP_E_UNSUPPORTED;
     }
-    // fused: one workgroup per grid; a lone grid gets a wider workgroup (single-CU solve)
-    const int items = d.mapping == MGDP_MAP_SA ? vi->S * 8 : vi->HW;
-    int blk = d.B == 1 ? 1024 : 256;
-    while (blk > 64 && blk / 2 >= items) blk /= 2;
-    vi->fused_block = blk;
+    // fused: one workgroup per grid.  MAP_CELL: one thread per cell (register topology) when the
+    // grid has <= 1024 cells; MAP_SA: 8 lanes per state, a lone grid gets the widest workgroup.
+    if (d.mapping == MGDP_MAP_CELL) {
+        vi->fused_block = (int)std::min<int64_t>(1024, round_up(vi->HW, 64));
+    } else {
+        int blk = d.B == 1 ? 1024 : 256;
+        while (blk > 64 && blk / 2 >= vi->S * 8) blk /= 2;
+        vi->fused_block = blk;
+    }
 
     const size_t BS = (size_t)d.B * vi->S;
     hipError_t e = hipSuccess;
@@ -790,13 +934,19 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     al((void **)&vi->d_kenv, sizeof(int32_t) * d.B);
     al((void **)&vi->d_dvenv, sizeof(double) * d.B);
     al((void **)&vi->d_shards, sizeof(unsigned long long) * 8 * (size_t)(d.max_sweeps + 1));
-    al((void **)&vi->d_red, sizeof(unsigned long long) * 4);
-    if (e == hipSuccess) e = hipHostMalloc((void **)&vi->h_red, 4 * sizeof(unsigned long long), hipHostMallocDefault);
+    al((void **)&vi->d_red, sizeof(unsigned long long) * 2 * kRedShards * 4);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&vi->h_red, kRedShards * 4 * sizeof(unsigned long long), hipHostMallocDefault);
     if (e == hipSuccess) {
         e = hipStreamCreateWithFlags(&vi->stream, hipStreamNonBlocking);
         vi->own_stream = e == hipSuccess;
     }
     if (e == hipSuccess) e = hipMemset(vi->d_cells, 0, (size_t)d.B * vi->HWp);
+    if (e == hipSuccess) {  // arm both fused reduction slots
+        std::vector<unsigned long long> init((size_t)2 * kRedShards * 4, 0ull);
+        for (size_t i = 2; i < init.size(); i += 4) init[i] = 0x7fffffffull;
+        e = hipMemcpy(vi->d_red, init.data(), init.size() * sizeof(unsigned long long), hipMemcpyHostToDevice);
+    }
+    vi->stream_blk = (int)std::min<int64_t>(256, round_up(vi->HW, 64));
     if (e != hipSuccess) {
         mgdp_vi_destroy(vi);
         return hip_fail(e, "mgdp_vi_create allocation", __FILE__, __LINE__);
@@ -863,12 +1013,12 @@ int mgdp_vi_load_cells_device(mgdp_vi *vi, const uint8_t *d_cells) {
 int mgdp_vi_reset(mgdp_vi *vi) {
     MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
     DeviceGuard guard(vi->d.device);
-    const size_t BS = (size_t)vi->d.B * vi->S;
-    MGDP_HIP(hipMemsetAsync(vi->d_V[0], 0, BS * vi->tsize, vi->stream));
-    if (vi->d_V[1]) MGDP_HIP(hipMemsetAsync(vi->d_V[1], 0, BS * vi->tsize, vi->stream));
-    MGDP_HIP(hipMemsetAsync(vi->d_kenv, 0, sizeof(int32_t) * vi->d.B, vi->stream));
-    MGDP_HIP(hipMemsetAsync(vi->d_dvenv, 0, sizeof(double) * vi->d.B, vi->stream));
-    MGDP_HIP(hipMemsetAsync(vi->d_shards, 0, sizeof(unsigned long long) * 8 * (size_t)(vi->d.max_sweeps + 1), vi->stream));
+    if (vi->d.method == MGDP_METHOD_SWEEP) {  // V_0 = 0 and an empty dV trace
+        const size_t BS = (size_t)vi->d.B * vi->S;
+        MGDP_HIP(hipMemsetAsync(vi->d_V[0], 0, BS * vi->tsize, vi->stream));
+        MGDP_HIP(hipMemsetAsync(vi->d_shards, 0, sizeof(unsigned long long) * 8 * (size_t)(vi->d.max_sweeps + 1), vi->stream));
+    }
+    vi->fresh = 1;  // the next fused launch ignores kenv/dvenv and starts from V_0 = 0
     vi->cur = 0;
     vi->k_done = 0;
     vi->k_min = 0;
@@ -925,10 +1075,9 @@ int mgdp_vi_run_to(mgdp_vi *vi, int32_t k_target, double *dv_out) {
 int mgdp_vi_sweep(mgdp_vi *vi, double *dv_out) {
     MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
     if (vi->d.method == MGDP_METHOD_FUSED) {
-        int32_t km = 0;
-        DeviceGuard guard(vi->d.device);
-        if (int rc = reduce_env(vi, &km, nullptr)) return rc;
-        return mgdp_vi_run_to(vi, km + 1, dv_out);
+        MGDP_CHECK(vi->k_done_valid && vi->k_min == vi->k_max, MGDP_E_INVALID,
+                   "mgdp_vi_sweep: grids are not at a common sweep index (call mgdp_vi_run_to first)");
+        return mgdp_vi_run_to(vi, vi->k_max + 1, dv_out);
     }
     return mgdp_vi_run_to(vi, vi->k_done + 1, dv_out);
 }
