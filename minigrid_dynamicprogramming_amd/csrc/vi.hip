@@ -12,15 +12,16 @@
 //   V      T      [2][B][S]     value double-buffer (fused method uses buffer 0 in place)
 //   pi     int8   [B][S]        greedy action of the last sweep (-1 = absorbing state)
 //   kenv   int32  [B], dvenv f64 [B]   sweeps done / last max|dV| per grid (fused method)
+//   red    u64    [64][4] + u32 ticket fused-launch reduction (kmax, dV bits, kmin) -> host-mapped
 //   shards u64    [max_sweeps][8]      per-sweep global max|dV| as f64 bits (sweep method),
 //                                      8 atomic shards (blockIdx & 7) to spread contention
 //
 // Kernels
 //   vi_fused_kernel   one workgroup per grid: cells + both V buffers + pi live in LDS for the
 //                     whole solve; many sweeps per launch, one __syncthreads per sweep.
-//   vi_sweep_kernel   one Jacobi sweep of every grid: per grid, V'[grid] is staged HBM->LDS with
-//                     16-B coalesced loads, updated from LDS, written back LDS->HBM.
-//   vi_stream_kernel  one Jacobi sweep of every grid without LDS staging (MAP_CELL, sweep method).
+//   vi_sweep_kernel   one Jacobi sweep of every grid: per grid, V'[grid] is staged HBM->LDS (the
+//                     LDS tile of the neighbourhood; the next grid's tile is prefetched into
+//                     registers while the current one is computed), updated from LDS, written back.
 // Thread mappings (template MAP): MGDP_MAP_CELL = one thread per cell updating its 4 (XYD) or
 // 16 (DoorKey) states from 16-B LDS vectors; MGDP_MAP_SA = one thread per (state, action),
 // 8 lanes per state, wave shuffle max-reduce with the lowest action index winning ties.
@@ -55,10 +56,15 @@ __device__ __forceinline__ bool dk_walk(int t, int hk, int dop) {
     return t == T_EMPTY || t == T_FLOOR || (t == T_DOOR && dop) || (t == T_KEY && hk);
 }
 
+// All values handled here are finite and >= +0 (V in [0, 1], rewards in {0, 1}), so max() is
+// order-independent and equal to the oracle's "strictly greater replaces" scan, and
+// |a - b| equals the oracle's (a > b ? a - b : b - a) bit for bit.
 template <typename T>
 __device__ __forceinline__ T tmax(T a, T b) { return a > b ? a : b; }
-template <typename T>
-__device__ __forceinline__ T tabs_diff(T a, T b) { return a > b ? a - b : b - a; }
+__device__ __forceinline__ float vmax(float a, float b) { return fmaxf(a, b); }
+__device__ __forceinline__ double vmax(double a, double b) { return fmax(a, b); }
+__device__ __forceinline__ float vabs(float a) { return fabsf(a); }
+__device__ __forceinline__ double vabs(double a) { return fabs(a); }
 
 template <typename T>
 __device__ __forceinline__ T wave_max(T v) {
@@ -79,6 +85,15 @@ __device__ __forceinline__ T block_max(T v, T *slots, int parity) {
     T m = slots[parity * 16];
     for (int i = 1; i < nw; ++i) m = tmax(m, slots[parity * 16 + i]);
     return m;
+}
+
+// Block-wide OR of a predicate with ONE barrier: one byte flag per wave, two parities.
+__device__ __forceinline__ bool block_any(bool p, uint8_t *flags, int parity) {
+    const unsigned long long b = __ballot(p);
+    if ((threadIdx.x & 63) == 0) flags[parity * 16 + (threadIdx.x >> 6)] = b != 0ull;
+    __syncthreads();
+    const uint4 f = *reinterpret_cast<const uint4 *>(flags + parity * 16);
+    return (f.x | f.y | f.z | f.w) != 0u;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -113,6 +128,7 @@ __device__ __forceinline__ XydTopo<T> xyd_topo(const uint8_t *cl, const Geo &geo
 
 // One cell of the XYD model (4 states, actions 0..6).  Returns max |dV| over the cell's states.
 // Q_det: left/right/self (= pickup/drop/toggle/done) = g*V, forward per minigrid_env.py:546-553.
+// WRITE_PI = false is the value-only sweep (max without argmax); pi is extracted once at the end.
 template <typename T, bool SLIP, bool WRITE_V, bool WRITE_PI>
 __device__ __forceinline__ T xyd_update(const XydTopo<T> &tp, const Coef<T> &cf, const T *Vin, T *Vout,
                                         int8_t *pis, int c) {
@@ -135,30 +151,32 @@ __device__ __forceinline__ T xyd_update(const XydTopo<T> &tp, const Coef<T> &cf,
     for (int d = 0; d < 4; ++d) {
         const T qF = ((tp.term >> d) & 1u) ? tp.tq[d] : cf.g * nbv[d];
         const T qL = gv[(d + 3) & 3], qR = gv[(d + 1) & 3], qS = gv[d];
-        T best;
-        int arg;
-        if (!SLIP) {
-            best = qL; arg = 0;
-            if (qR > best) { best = qR; arg = 1; }
-            if (qF > best) { best = qF; arg = 2; }
-            if (qS > best) { best = qS; arg = 3; }
-        } else {
+        T a0 = qL, a1 = qR, a2 = qF, a3 = qS;  // Q of actions 0..3 (4..6 equal action 3)
+        if (SLIP) {
             T s6 = qL + qR;
             s6 = s6 + qF;
             s6 = s6 + qS;
             s6 = s6 + qS;
             s6 = s6 + qS;
             const T tail = cf.c * s6;
-            const T Q0 = cf.p * qL + tail, Q1 = cf.p * qR + tail, Q2 = cf.p * qF + tail,
-                    Q3 = cf.p * qS + tail;
-            best = Q0; arg = 0;
-            if (Q1 > best) { best = Q1; arg = 1; }
-            if (Q2 > best) { best = Q2; arg = 2; }
-            if (Q3 > best) { best = Q3; arg = 3; }
+            a0 = cf.p * qL + tail;
+            a1 = cf.p * qR + tail;
+            a2 = cf.p * qF + tail;
+            a3 = cf.p * qS + tail;
+        }
+        T best;
+        if (WRITE_PI) {
+            int arg = 0;
+            best = a0;
+            if (a1 > best) { best = a1; arg = 1; }
+            if (a2 > best) { best = a2; arg = 2; }
+            if (a3 > best) { best = a3; arg = 3; }
+            pk |= (uint32_t)(uint8_t)arg << (8 * d);
+        } else {
+            best = vmax(vmax(a0, a1), vmax(a2, a3));
         }
         out.v[d] = best;
-        pk |= (uint32_t)(uint8_t)arg << (8 * d);
-        dv = tmax(dv, tabs_diff(best, own.v[d]));
+        dv = vmax(dv, vabs(best - own.v[d]));
     }
     if (WRITE_V) *reinterpret_cast<V4<T> *>(Vout + c * 4) = out;
     if (WRITE_PI) *reinterpret_cast<uint32_t *>(pis + c * 4) = pk;
@@ -238,15 +256,20 @@ __device__ __forceinline__ T dk_update(const DkTopo &tp, const Coef<T> &cf, cons
                     if (dop) qT = gv[(d * 2 + hk) * 2 + 0];
                     else if (hk) qT = gv[(d * 2 + hk) * 2 + 1];
                 }
-                T best = qL;
-                int arg = 0;
-                if (qR > best) { best = qR; arg = 1; }
-                if (qF > best) { best = qF; arg = 2; }
-                if (qP > best) { best = qP; arg = 3; }
-                if (qT > best) { best = qT; arg = 4; }
+                T best;
+                if (WRITE_PI) {
+                    best = qL;
+                    int arg = 0;
+                    if (qR > best) { best = qR; arg = 1; }
+                    if (qF > best) { best = qF; arg = 2; }
+                    if (qP > best) { best = qP; arg = 3; }
+                    if (qT > best) { best = qT; arg = 4; }
+                    outp[l] = (int8_t)arg;
+                } else {
+                    best = vmax(vmax(vmax(qL, qR), vmax(qF, qP)), qT);
+                }
                 outv[l] = best;
-                outp[l] = (int8_t)arg;
-                dv = tmax(dv, tabs_diff(best, own[l]));
+                dv = vmax(dv, vabs(best - own[l]));
             }
         }
     }
@@ -354,22 +377,23 @@ __device__ __forceinline__ T sa_sweep(const Geo &geo, const Coef<T> &cf, const u
             const T nv = valid ? q : (T)0;
             if (WRITE_V) Vout[ss] = nv;
             pis[ss] = valid ? (int8_t)arg : (int8_t)-1;
-            dv = tmax(dv, tabs_diff(nv, old));
+            dv = vmax(dv, vabs(nv - old));
         }
     }
     return dv;
 }
 
-template <typename T, int MODEL, bool SLIP, int MAP, bool WRITE_V>
+// Generic LDS sweep over all cells of one grid (topology re-read from LDS each time).
+template <typename T, int MODEL, bool SLIP, int MAP, bool WRITE_V, bool WRITE_PI>
 __device__ __forceinline__ T sweep_lds(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
                                        const T *Vin, T *Vout, int8_t *pis) {
     if (MAP == MGDP_MAP_SA) return sa_sweep<T, MODEL, SLIP, WRITE_V>(geo, cf, cl, Vin, Vout, pis);
     T dv = (T)0;
     for (int c = threadIdx.x; c < geo.HW; c += blockDim.x) {
         if (MODEL == MGDP_MODEL_XYD)
-            dv = tmax(dv, xyd_update<T, SLIP, WRITE_V, true>(xyd_topo<T>(cl, geo, c), cf, Vin, Vout, pis, c));
+            dv = vmax(dv, xyd_update<T, SLIP, WRITE_V, WRITE_PI>(xyd_topo<T>(cl, geo, c), cf, Vin, Vout, pis, c));
         else
-            dv = tmax(dv, dk_update<T, WRITE_V, true>(dk_topo(cl, geo, c), cf, Vin, Vout, pis, c));
+            dv = vmax(dv, dk_update<T, WRITE_V, WRITE_PI>(dk_topo(cl, geo, c), cf, Vin, Vout, pis, c));
     }
     return dv;
 }
@@ -384,15 +408,11 @@ __device__ __forceinline__ void zero16(void *dst, int bytes) {
     uint4 *d = reinterpret_cast<uint4 *>(dst);
     for (int i = threadIdx.x; i < (bytes >> 4); i += blockDim.x) d[i] = make_uint4(0, 0, 0, 0);
 }
-
-// Block-wide OR of a predicate with ONE barrier: one byte flag per wave, two parities so that a
-// flag set is rewritten only after every thread has passed the following barrier.
-__device__ __forceinline__ bool block_any(bool p, uint8_t *flags, int parity) {
-    const unsigned long long b = __ballot(p);
-    if ((threadIdx.x & 63) == 0) flags[parity * 16 + (threadIdx.x >> 6)] = b != 0ull;
-    __syncthreads();
-    const uint4 f = *reinterpret_cast<const uint4 *>(flags + parity * 16);
-    return (f.x | f.y | f.z | f.w) != 0u;
+__device__ __forceinline__ void copy_pi(int8_t *dst, const int8_t *src, int S) {
+    // S is a multiple of 4, so pi rows are 4-byte aligned
+    const uint32_t *s = reinterpret_cast<const uint32_t *>(src);
+    uint32_t *d = reinterpret_cast<uint32_t *>(dst);
+    for (int i = threadIdx.x; i < (S >> 2); i += blockDim.x) d[i] = s[i];
 }
 
 struct Smem {
@@ -409,7 +429,48 @@ __host__ __device__ inline Smem smem_layout(int S, int HWp, int tsize) {
     return m;
 }
 
-constexpr int kRedShards = 64;  // fused-kernel reduction: [2 slots][64 shards][kmax, dv bits, kmin, -]
+constexpr int kRedShards = 64;  // fused-launch reduction shards: [64][kmax, dV bits, kmin, -]
+
+// Fold this block's (k, dV) into the launch reduction; the last block to arrive (arrival ticket,
+// agent-scope release/acquire per cdna_hip_programming.md Guideline 16) combines the shards,
+// publishes {kmax, dV, kmin} to host-mapped memory and re-arms shards + ticket for the next launch.
+__device__ __forceinline__ void fused_reduce(unsigned long long *red, unsigned int *ticket,
+                                             unsigned long long *host_out, int k, double dvl,
+                                             unsigned int *lds_flag) {
+    if (threadIdx.x == 0) {
+        unsigned long long *r = red + (blockIdx.x & (kRedShards - 1)) * 4;
+        atomicMax(r + 0, (unsigned long long)k);
+        atomicMax(r + 1, (unsigned long long)__double_as_longlong(dvl));
+        atomicMin(r + 2, (unsigned long long)k);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned int t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *lds_flag = t == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (*lds_flag && threadIdx.x < 64) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        unsigned long long *r = red + threadIdx.x * 4;
+        unsigned long long km = __hip_atomic_load(r + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long dv = __hip_atomic_load(r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long kn = __hip_atomic_load(r + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(r + 0, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(r + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(r + 2, 0x7fffffffull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            km = max(km, (unsigned long long)__shfl_xor(km, o));
+            dv = max(dv, (unsigned long long)__shfl_xor(dv, o));
+            kn = min(kn, (unsigned long long)__shfl_xor(kn, o));
+        }
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(host_out + 0, km, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_out + 1, dv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_out + 2, kn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
 
 // ------------------------------------------------------------------------------------------------
 // Fused solve: blockIdx.x = grid index; the grid's cells, both V buffers and pi stay in LDS for
@@ -417,15 +478,16 @@ constexpr int kRedShards = 64;  // fused-kernel reduction: [2 slots][64 shards][
 // max_sweeps); k_target >= 0: sweep until exactly k_target sweeps are done.  fresh: start from
 // V_0 = 0 regardless of kenv/dvenv.  MAP_CELL with HW <= blockDim keeps each thread's cell
 // topology in registers for the whole launch (no LDS cell reads inside the sweep loop).
-// Per-sweep convergence test = block OR of (|dV| >= tol) (ballot + one byte per wave); the exact
-// max |dV| is reduced once, after the last sweep.  Every block folds (k, dV) into reduction slot
-// `slot` with sharded atomics; block 0 re-arms the other slot for the next launch.
+// Sweeps are value-only (max, no argmax); the per-sweep convergence test is a block OR of
+// (|dV| >= tol) (ballot + one byte per wave, one barrier); after the loop the exact max |dV| is
+// reduced once and pi is extracted once from V_{k-1} (exactly what sweep k's argmax would give).
 // ------------------------------------------------------------------------------------------------
 template <typename T, int MODEL, bool SLIP, int MAP>
 __global__ void __launch_bounds__(1024)
 vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
-                unsigned long long *__restrict__ red, int slot, int k_target, int fresh) {
+                unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
+                unsigned long long *__restrict__ host_out, int k_target, int fresh) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int e = blockIdx.x;
     const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T));
@@ -436,10 +498,6 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
     T *slots = reinterpret_cast<T *>(smem + 2 * L.v_bytes + L.pi_bytes + L.cells_bytes);
     uint8_t *flags = reinterpret_cast<uint8_t *>(smem + 2 * L.v_bytes + L.pi_bytes + L.cells_bytes + 256);
 
-    if (blockIdx.x == 0) {
-        unsigned long long *o = red + (slot ^ 1) * kRedShards * 4;
-        for (int i = threadIdx.x; i < kRedShards * 4; i += blockDim.x) o[i] = (i & 3) == 2 ? 0x7fffffffull : 0ull;
-    }
     int k = fresh ? 0 : kenv[e];
     double dvl = fresh ? 0.0 : dvenv[e];
     const bool work = k_target < 0 ? (!(k > 0 && dvl < geo.tol) && k < geo.max_sweeps) : (k < k_target);
@@ -467,11 +525,11 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
             T *Vout = cur ? V0 : V1;
             if (fast) {
                 if (own) {
-                    if (MODEL == MGDP_MODEL_XYD) diff = xyd_update<T, SLIP, true, true>(xt, cf, Vin, Vout, pis, c);
-                    else diff = dk_update<T, true, true>(dt, cf, Vin, Vout, pis, c);
+                    if (MODEL == MGDP_MODEL_XYD) diff = xyd_update<T, SLIP, true, false>(xt, cf, Vin, Vout, pis, c);
+                    else diff = dk_update<T, true, false>(dt, cf, Vin, Vout, pis, c);
                 }
             } else {
-                diff = sweep_lds<T, MODEL, SLIP, MAP, true>(geo, cf, cl, Vin, Vout, pis);
+                diff = sweep_lds<T, MODEL, SLIP, MAP, true, MAP == MGDP_MAP_SA>(geo, cf, cl, Vin, Vout, pis);
             }
             cur ^= 1;
             ++k;
@@ -485,23 +543,26 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
             }
         }
         dvl = (double)block_max(diff, slots, 0);
-        copy16(V + vb, cur ? V1 : V0, L.v_bytes);
-        {   // S is a multiple of 4, so pi rows are 4-byte aligned
-            const uint32_t *src = reinterpret_cast<const uint32_t *>(pis);
-            uint32_t *dst = reinterpret_cast<uint32_t *>(pi + vb);
-            for (int i = threadIdx.x; i < (geo.S >> 2); i += blockDim.x) dst[i] = src[i];
+        if (MAP == MGDP_MAP_CELL) {  // pi of the last sweep = argmax on V_{k-1} (buffer cur ^ 1)
+            const T *Vprev = cur ? V0 : V1;
+            if (fast) {
+                if (own) {
+                    if (MODEL == MGDP_MODEL_XYD) xyd_update<T, SLIP, false, true>(xt, cf, Vprev, nullptr, pis, c);
+                    else dk_update<T, false, true>(dt, cf, Vprev, nullptr, pis, c);
+                }
+            } else {
+                sweep_lds<T, MODEL, SLIP, MAP, false, true>(geo, cf, cl, Vprev, nullptr, pis);
+            }
+            __syncthreads();
         }
+        copy16(V + vb, cur ? V1 : V0, L.v_bytes);
+        copy_pi(pi + vb, pis, geo.S);
         if (threadIdx.x == 0) {
             kenv[e] = k;
             dvenv[e] = dvl;
         }
     }
-    if (threadIdx.x == 0) {
-        unsigned long long *r = red + (slot * kRedShards + (e & (kRedShards - 1))) * 4;
-        atomicMax(r + 0, (unsigned long long)k);
-        atomicMax(r + 1, (unsigned long long)__double_as_longlong(dvl));
-        atomicMin(r + 2, (unsigned long long)k);
-    }
+    fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16));
 }
 
 // Early exit of a speculatively enqueued sweep: the previous sweep already met the rule.
@@ -515,13 +576,17 @@ __device__ __forceinline__ bool prev_sweep_converged(const unsigned long long *s
 }
 
 // ------------------------------------------------------------------------------------------------
-// One Jacobi sweep (index k, 1-based) of every grid, V double-buffered in HBM, MAP_SA mapping:
-// per grid, V'[grid] is staged HBM -> LDS with 16-B loads (the LDS tile of the neighbourhood),
-// updated by (state, action) lanes, written back LDS -> HBM.  check_prev: skip when the previous
-// sweep's global max|dV| was already < tol.  POLICY: evaluate only, write pi.
+// One Jacobi sweep (index k, 1-based) of every grid, V double-buffered in HBM.  Per grid the V
+// tile and cells are staged HBM -> LDS, updated from LDS, written back with 16-B stores.  While a
+// grid is computed, the next grid's tile is already in flight into registers (PREFETCH), so the
+// HBM stream overlaps the LDS compute.  check_prev: skip when the previous sweep's global
+// max|dV| was already < tol.  POLICY: evaluate only, write pi.
 // ------------------------------------------------------------------------------------------------
-template <typename T, int MODEL, bool SLIP, int MAP, bool POLICY>
-__global__ void __launch_bounds__(256)
+constexpr int kSweepBlock = 256;
+constexpr int kPrefetchRegs = 8;  // 16-B registers per thread: tiles up to 32 KiB
+
+template <typename T, int MODEL, bool SLIP, int MAP, bool POLICY, bool PREFETCH>
+__global__ void __launch_bounds__(kSweepBlock)
 vi_sweep_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, const T *__restrict__ Vin,
                 T *__restrict__ Vout, int8_t *__restrict__ pi, unsigned long long *__restrict__ shards,
                 int k, int check_prev) {
@@ -533,59 +598,43 @@ vi_sweep_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, const T 
     int8_t *pis = reinterpret_cast<int8_t *>(smem + 2 * L.v_bytes);
     uint8_t *cl = reinterpret_cast<uint8_t *>(smem + 2 * L.v_bytes + L.pi_bytes);
     T *slots = reinterpret_cast<T *>(smem + 2 * L.v_bytes + L.pi_bytes + L.cells_bytes);
+    const int nv16 = L.v_bytes >> 4, nc16 = geo.HWp >> 4;
+    const uint4 *Vin16 = reinterpret_cast<const uint4 *>(Vin);
+    const uint4 *C16 = reinterpret_cast<const uint4 *>(cells);
+
+    uint4 rv[PREFETCH ? kPrefetchRegs : 1];
+    uint4 rc = make_uint4(0, 0, 0, 0);
+    auto fetch = [&](int e) {
+#pragma unroll
+        for (int r = 0; r < (PREFETCH ? kPrefetchRegs : 1); ++r) {
+            const int i = threadIdx.x + r * kSweepBlock;
+            if (i < nv16) rv[r] = Vin16[(long long)e * nv16 + i];
+        }
+        if ((int)threadIdx.x < nc16) rc = C16[(long long)e * nc16 + threadIdx.x];
+    };
+    if (PREFETCH && (int)blockIdx.x < geo.B) fetch(blockIdx.x);
 
     T acc = (T)0;
     for (int e = blockIdx.x; e < geo.B; e += gridDim.x) {
         const long long vb = (long long)e * geo.S;
-        __syncthreads();
-        copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
-        copy16(Vi, Vin + vb, L.v_bytes);
-        __syncthreads();
-        acc = tmax(acc, sweep_lds<T, MODEL, SLIP, MAP, !POLICY>(geo, cf, cl, Vi, Vo, pis));
-        __syncthreads();
-        if (!POLICY) {
-            copy16(Vout + vb, Vo, L.v_bytes);
+        __syncthreads();  // the previous grid's LDS tile is no longer read
+        if (PREFETCH) {
+#pragma unroll
+            for (int r = 0; r < kPrefetchRegs; ++r) {
+                const int i = threadIdx.x + r * kSweepBlock;
+                if (i < nv16) reinterpret_cast<uint4 *>(Vi)[i] = rv[r];
+            }
+            if ((int)threadIdx.x < nc16) reinterpret_cast<uint4 *>(cl)[threadIdx.x] = rc;
+            if (e + (int)gridDim.x < geo.B) fetch(e + gridDim.x);  // in flight during the compute
         } else {
-            const uint32_t *src = reinterpret_cast<const uint32_t *>(pis);
-            uint32_t *dst = reinterpret_cast<uint32_t *>(pi + vb);
-            for (int i = threadIdx.x; i < (geo.S >> 2); i += blockDim.x) dst[i] = src[i];
+            copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
+            copy16(Vi, Vin + vb, L.v_bytes);
         }
-    }
-    if (!POLICY) {
-        const T bdv = block_max(acc, slots, 0);
-        if (threadIdx.x == 0 && shards)
-            atomicMax(shards + (long long)(k - 1) * 8 + (blockIdx.x & 7),
-                      (unsigned long long)__double_as_longlong((double)bdv));
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
-// One Jacobi sweep, MAP_CELL mapping, streaming: one thread per cell, no LDS staging.  The wave's
-// own V rows are read with 16-B loads (coalesced), front-cell values and types are gathered from
-// L1/L2 (they are the neighbouring rows of the same or adjacent waves), new V leaves with 16-B
-// stores.  Chunks of `blk` cells of one grid are distributed grid-stride over the launch.
-// ------------------------------------------------------------------------------------------------
-template <typename T, int MODEL, bool SLIP, bool POLICY>
-__global__ void __launch_bounds__(256)
-vi_stream_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, const T *__restrict__ Vin,
-                 T *__restrict__ Vout, int8_t *__restrict__ pi, unsigned long long *__restrict__ shards,
-                 int k, int check_prev, int bpe, int nchunks) {
-    __shared__ T slots[32];
-    if (check_prev && prev_sweep_converged(shards, k, geo.tol)) return;
-    T acc = (T)0;
-    for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-        const int e = ch / bpe;
-        const int c = (ch - e * bpe) * (int)blockDim.x + (int)threadIdx.x;
-        if (c < geo.HW) {
-            const uint8_t *ce = cells + (long long)e * geo.HWp;
-            const long long vb = (long long)e * geo.S;
-            if (MODEL == MGDP_MODEL_XYD)
-                acc = tmax(acc, xyd_update<T, SLIP, !POLICY, POLICY>(xyd_topo<T>(ce, geo, c), cf, Vin + vb,
-                                                                     Vout + vb, pi + vb, c));
-            else
-                acc = tmax(acc, dk_update<T, !POLICY, POLICY>(dk_topo(ce, geo, c), cf, Vin + vb, Vout + vb,
-                                                              pi + vb, c));
-        }
+        __syncthreads();
+        acc = vmax(acc, sweep_lds<T, MODEL, SLIP, MAP, !POLICY, POLICY || MAP == MGDP_MAP_SA>(geo, cf, cl, Vi, Vo, pis));
+        __syncthreads();
+        if (!POLICY) copy16(Vout + vb, Vo, L.v_bytes);
+        else copy_pi(pi + vb, pis, geo.S);
     }
     if (!POLICY) {
         const T bdv = block_max(acc, slots, 0);
@@ -613,8 +662,10 @@ struct mgdp_vi {
     int32_t *d_kenv = nullptr;
     double *d_dvenv = nullptr;
     unsigned long long *d_shards = nullptr;
-    unsigned long long *d_red = nullptr;
-    unsigned long long *h_red = nullptr;  // pinned
+    unsigned long long *d_red = nullptr;    // fused reduction shards [64][4]
+    unsigned int *d_ticket = nullptr;       // arrival ticket of the fused reduction
+    unsigned long long *h_out = nullptr;    // host-mapped {kmax, dV bits, kmin}
+    unsigned long long *d_hout = nullptr;   // device alias of h_out
     int cur = 0;        // V buffer holding the current V (sweep method)
     int k_min = 0;      // min / max sweeps over grids after the last reduce (fused method)
     int k_max = 0;
@@ -631,8 +682,6 @@ struct mgdp_vi {
     int64_t launches = 0;
     int fused_block = 256;
     int sweep_grid = 2048;
-    int stream_blk = 256;   // threads per cell chunk of vi_stream_kernel
-    int red_slot = 0;       // fused reduction slot written by the next launch
     int fresh = 1;          // next fused launch starts from V_0 = 0
 };
 
@@ -708,48 +757,35 @@ int launch_fused_t(mgdp_vi *vi, int k_target) {
     if (int rc = timed_begin(vi, -1)) return rc;
     hipLaunchKernelGGL(kern, dim3(vi->d.B), dim3(vi->fused_block), L.total(), vi->stream, g,
                        make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv,
-                       vi->d_dvenv, vi->d_red, vi->red_slot, k_target, vi->fresh);
+                       vi->d_dvenv, vi->d_red, vi->d_ticket, vi->d_hout, k_target, vi->fresh);
     MGDP_HIP(hipGetLastError());
     vi->fresh = 0;
     return timed_end(vi);
 }
 
+template <typename T, int MODEL, bool SLIP, int MAP, bool POLICY, bool PREFETCH>
+int launch_sweep_kernel(mgdp_vi *vi, const T *Vin, T *Vout, int k, int check_prev) {
+    const Smem L = smem_layout(vi->S, vi->HWp, sizeof(T));
+    auto kern = vi_sweep_kernel<T, MODEL, SLIP, MAP, POLICY, PREFETCH>;
+    if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
+    const int grid = std::min(vi->d.B, vi->sweep_grid);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kSweepBlock), L.total(), vi->stream, make_geo(vi), make_coef<T>(vi),
+                       vi->d_cells, Vin, Vout, vi->d_pi, POLICY ? nullptr : vi->d_shards, k, check_prev);
+    MGDP_HIP(hipGetLastError());
+    return 0;
+}
+
 template <typename T, int MODEL, bool SLIP, int MAP>
 int launch_sweep_t(mgdp_vi *vi, int k, int check_prev, bool policy) {
-    const Geo g = make_geo(vi);
     const T *Vin = (const T *)vi->d_V[(k - 1) & 1];
     T *Vout = (T *)vi->d_V[k & 1];
-    unsigned long long *sh = policy ? nullptr : vi->d_shards;
-    if (!policy)
-        if (int rc = timed_begin(vi, k)) return rc;
-    if (MAP == MGDP_MAP_CELL) {
-        const int blk = vi->stream_blk;
-        const int bpe = (vi->HW + blk - 1) / blk;
-        const int nchunks = vi->d.B * bpe;
-        const int grid = std::min(nchunks, 256 * (2048 / blk));
-        if (policy)
-            hipLaunchKernelGGL((vi_stream_kernel<T, MODEL, SLIP, true>), dim3(grid), dim3(blk), 0, vi->stream, g,
-                               make_coef<T>(vi), vi->d_cells, Vin, Vout, vi->d_pi, sh, k, 0, bpe, nchunks);
-        else
-            hipLaunchKernelGGL((vi_stream_kernel<T, MODEL, SLIP, false>), dim3(grid), dim3(blk), 0, vi->stream, g,
-                               make_coef<T>(vi), vi->d_cells, Vin, Vout, vi->d_pi, sh, k, check_prev, bpe, nchunks);
-    } else {
-        const Smem L = smem_layout(vi->S, vi->HWp, sizeof(T));
-        const int grid = std::min(vi->d.B, vi->sweep_grid);
-        if (policy) {
-            auto kern = vi_sweep_kernel<T, MODEL, SLIP, MAP, true>;
-            if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(256), L.total(), vi->stream, g, make_coef<T>(vi),
-                               vi->d_cells, Vin, Vout, vi->d_pi, sh, k, 0);
-        } else {
-            auto kern = vi_sweep_kernel<T, MODEL, SLIP, MAP, false>;
-            if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(256), L.total(), vi->stream, g, make_coef<T>(vi),
-                               vi->d_cells, Vin, Vout, vi->d_pi, sh, k, check_prev);
-        }
-    }
-    MGDP_HIP(hipGetLastError());
-    return policy ? 0 : timed_end(vi);
+    if (policy) return launch_sweep_kernel<T, MODEL, SLIP, MAP, true, false>(vi, Vin, Vout, k, 0);
+    if (int rc = timed_begin(vi, k)) return rc;
+    const bool pf = (int64_t)vi->S * sizeof(T) <= (int64_t)kSweepBlock * kPrefetchRegs * 16;
+    const int rc = pf ? launch_sweep_kernel<T, MODEL, SLIP, MAP, false, true>(vi, Vin, Vout, k, check_prev)
+                      : launch_sweep_kernel<T, MODEL, SLIP, MAP, false, false>(vi, Vin, Vout, k, check_prev);
+    if (rc) return rc;
+    return timed_end(vi);
 }
 
 // Dispatch on (dtype, model, slip, mapping).
@@ -782,21 +818,13 @@ struct SweepF {
     }
 };
 
-// Read back the reduction slot written by the last fused launch: max k, max dV, min k over grids.
+// Read the reduction the last fused launch published to host-mapped memory: max k, max dV, min k.
 int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
-    const size_t n = (size_t)kRedShards * 4;
-    MGDP_HIP(hipMemcpyAsync(vi->h_red, vi->d_red + (size_t)vi->red_slot * n, n * sizeof(unsigned long long),
-                            hipMemcpyDeviceToHost, vi->stream));
     MGDP_HIP(hipStreamSynchronize(vi->stream));
-    vi->red_slot ^= 1;
     if (int rc = timed_collect(vi, 1 << 30)) return rc;
-    unsigned long long km = 0, dvb = 0, kmin = 0x7fffffffull;
-    for (int i = 0; i < kRedShards; ++i) {
-        km = std::max(km, vi->h_red[4 * i]);
-        dvb = std::max(dvb, vi->h_red[4 * i + 1]);
-        kmin = std::min(kmin, vi->h_red[4 * i + 2]);
-    }
-    std::memcpy(&vi->dv_red, &dvb, sizeof(double));  // non-negative doubles order like their bits
+    const volatile unsigned long long *h = vi->h_out;
+    const unsigned long long km = h[0], dvb = h[1], kmin = h[2];
+    std::memcpy(&vi->dv_red, (const void *)&dvb, sizeof(double));  // non-negative doubles order like their bits
     vi->k_min = (int)kmin;
     vi->k_max = (int)km;
     vi->k_done_valid = true;
@@ -934,19 +962,21 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     al((void **)&vi->d_kenv, sizeof(int32_t) * d.B);
     al((void **)&vi->d_dvenv, sizeof(double) * d.B);
     al((void **)&vi->d_shards, sizeof(unsigned long long) * 8 * (size_t)(d.max_sweeps + 1));
-    al((void **)&vi->d_red, sizeof(unsigned long long) * 2 * kRedShards * 4);
-    if (e == hipSuccess) e = hipHostMalloc((void **)&vi->h_red, kRedShards * 4 * sizeof(unsigned long long), hipHostMallocDefault);
+    al((void **)&vi->d_red, sizeof(unsigned long long) * (kRedShards * 4 + 2));
+    if (e == hipSuccess) e = hipHostMalloc((void **)&vi->h_out, 4 * sizeof(unsigned long long),
+                                           hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&vi->d_hout, vi->h_out, 0);
     if (e == hipSuccess) {
         e = hipStreamCreateWithFlags(&vi->stream, hipStreamNonBlocking);
         vi->own_stream = e == hipSuccess;
     }
     if (e == hipSuccess) e = hipMemset(vi->d_cells, 0, (size_t)d.B * vi->HWp);
-    if (e == hipSuccess) {  // arm both fused reduction slots
-        std::vector<unsigned long long> init((size_t)2 * kRedShards * 4, 0ull);
-        for (size_t i = 2; i < init.size(); i += 4) init[i] = 0x7fffffffull;
+    if (e == hipSuccess) {  // arm the fused reduction (every launch re-arms it for the next)
+        std::vector<unsigned long long> init((size_t)kRedShards * 4 + 2, 0ull);
+        for (size_t i = 2; i < (size_t)kRedShards * 4; i += 4) init[i] = 0x7fffffffull;
         e = hipMemcpy(vi->d_red, init.data(), init.size() * sizeof(unsigned long long), hipMemcpyHostToDevice);
+        vi->d_ticket = reinterpret_cast<unsigned int *>(vi->d_red + kRedShards * 4);
     }
-    vi->stream_blk = (int)std::min<int64_t>(256, round_up(vi->HW, 64));
     if (e != hipSuccess) {
         mgdp_vi_destroy(vi);
         return hip_fail(e, "mgdp_vi_create allocation", __FILE__, __LINE__);
@@ -968,7 +998,7 @@ int mgdp_vi_destroy(mgdp_vi *vi) {
     (void)hipFree(vi->d_dvenv);
     (void)hipFree(vi->d_shards);
     (void)hipFree(vi->d_red);
-    if (vi->h_red) (void)hipHostFree(vi->h_red);
+    if (vi->h_out) (void)hipHostFree(vi->h_out);
     if (vi->own_stream) (void)hipStreamDestroy(vi->stream);
     delete vi;
     return 0;
