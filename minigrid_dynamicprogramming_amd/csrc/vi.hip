@@ -431,32 +431,30 @@ __host__ __device__ inline Smem smem_layout(int S, int HWp, int tsize) {
 
 constexpr int kRedShards = 64;  // fused-launch reduction shards: [64][kmax, dV bits, kmin, -]
 
-// Fold this block's (k, dV) into the launch reduction; the last block to arrive (arrival ticket,
-// agent-scope release/acquire per cdna_hip_programming.md Guideline 16) combines the shards,
-// publishes {kmax, dV, kmin} to host-mapped memory and re-arms shards + ticket for the next launch.
+// Fold this block's (k, dV) into the launch reduction.  Every access to the shards and the ticket
+// is an atomic read-modify-write (performed at the device coherence point, never served from a
+// possibly stale per-XCD L2 line), so no cache fences are needed: each block's shard updates
+// return before its ticket add is issued, hence the block that draws the last ticket observes all
+// of them; it combines the shards with exchanges that also re-arm them for the next launch, and
+// publishes {kmax, dV bits, kmin} to host-mapped memory.
 __device__ __forceinline__ void fused_reduce(unsigned long long *red, unsigned int *ticket,
                                              unsigned long long *host_out, int k, double dvl,
                                              unsigned int *lds_flag) {
     if (threadIdx.x == 0) {
         unsigned long long *r = red + (blockIdx.x & (kRedShards - 1)) * 4;
-        atomicMax(r + 0, (unsigned long long)k);
-        atomicMax(r + 1, (unsigned long long)__double_as_longlong(dvl));
-        atomicMin(r + 2, (unsigned long long)k);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long a = __hip_atomic_fetch_max(r + 0, (unsigned long long)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long b = __hip_atomic_fetch_max(r + 1, (unsigned long long)__double_as_longlong(dvl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long c = __hip_atomic_fetch_min(r + 2, (unsigned long long)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" :: "v"(a), "v"(b), "v"(c) : "memory");
         const unsigned int t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *lds_flag = t == gridDim.x - 1;
     }
     __syncthreads();
     if (*lds_flag && threadIdx.x < 64) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         unsigned long long *r = red + threadIdx.x * 4;
-        unsigned long long km = __hip_atomic_load(r + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        unsigned long long dv = __hip_atomic_load(r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        unsigned long long kn = __hip_atomic_load(r + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(r + 0, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(r + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(r + 2, 0x7fffffffull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long km = __hip_atomic_exchange(r + 0, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long dv = __hip_atomic_exchange(r + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long kn = __hip_atomic_exchange(r + 2, 0x7fffffffull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
             km = max(km, (unsigned long long)__shfl_xor(km, o));
@@ -464,7 +462,7 @@ __device__ __forceinline__ void fused_reduce(unsigned long long *red, unsigned i
             kn = min(kn, (unsigned long long)__shfl_xor(kn, o));
         }
         if (threadIdx.x == 0) {
-            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_exchange(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(host_out + 0, km, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_out + 1, dv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_out + 2, kn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -683,6 +681,7 @@ struct mgdp_vi {
     int fused_block = 256;
     int sweep_grid = 2048;
     int fresh = 1;          // next fused launch starts from V_0 = 0
+    bool sweep_prefetch = true;
 };
 
 namespace {
@@ -781,7 +780,7 @@ int launch_sweep_t(mgdp_vi *vi, int k, int check_prev, bool policy) {
     T *Vout = (T *)vi->d_V[k & 1];
     if (policy) return launch_sweep_kernel<T, MODEL, SLIP, MAP, true, false>(vi, Vin, Vout, k, 0);
     if (int rc = timed_begin(vi, k)) return rc;
-    const bool pf = (int64_t)vi->S * sizeof(T) <= (int64_t)kSweepBlock * kPrefetchRegs * 16;
+    const bool pf = vi->sweep_prefetch && (int64_t)vi->S * sizeof(T) <= (int64_t)kSweepBlock * kPrefetchRegs * 16;
     const int rc = pf ? launch_sweep_kernel<T, MODEL, SLIP, MAP, false, true>(vi, Vin, Vout, k, check_prev)
                       : launch_sweep_kernel<T, MODEL, SLIP, MAP, false, false>(vi, Vin, Vout, k, check_prev);
     if (rc) return rc;
@@ -971,6 +970,8 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
         vi->own_stream = e == hipSuccess;
     }
     if (e == hipSuccess) e = hipMemset(vi->d_cells, 0, (size_t)d.B * vi->HWp);
+    if (const char *ev = std::getenv("MGDP_SWEEP_PREFETCH")) vi->sweep_prefetch = std::atoi(ev) != 0;
+    if (const char *ev = std::getenv("MGDP_SWEEP_GRID")) vi->sweep_grid = std::max(1, std::atoi(ev));
     if (e == hipSuccess) {  // arm the fused reduction (every launch re-arms it for the next)
         std::vector<unsigned long long> init((size_t)kRedShards * 4 + 2, 0ull);
         for (size_t i = 2; i < (size_t)kRedShards * 4; i += 4) init[i] = 0x7fffffffull;
