@@ -430,6 +430,7 @@ __host__ __device__ inline Smem smem_layout(int S, int HWp, int tsize) {
 }
 
 constexpr int kRedShards = 64;  // fused-launch reduction shards: [64][kmax, dV bits, kmin, -]
+constexpr int kInKernelReduceMaxB = 512;  // above this, a separate one-workgroup reduce kernel
 
 // Fold this block's (k, dV) into the launch reduction.  Every access to the shards and the ticket
 // is an atomic read-modify-write (performed at the device coherence point, never served from a
@@ -485,7 +486,7 @@ __global__ void __launch_bounds__(1024)
 vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
-                unsigned long long *__restrict__ host_out, int k_target, int fresh) {
+                unsigned long long *__restrict__ host_out, int k_target, int fresh, int in_kernel_reduce) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int e = blockIdx.x;
     const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T));
@@ -560,7 +561,36 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
             dvenv[e] = dvl;
         }
     }
-    fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16));
+    if (in_kernel_reduce) fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16));
+}
+
+// Large batches: one workgroup reduces the per-grid (kenv, dvenv) into host-mapped memory (a
+// single arrival ticket shared by tens of thousands of workgroups would serialise on one address).
+__global__ void __launch_bounds__(1024)
+vi_reduce_kernel(const int32_t *__restrict__ kenv, const double *__restrict__ dvenv, int B,
+                 unsigned long long *__restrict__ host_out) {
+    __shared__ unsigned long long sk[16], sd[16], sn[16];
+    unsigned long long km = 0, dm = 0, kn = 0x7fffffffull;
+    for (int i = threadIdx.x; i < B; i += blockDim.x) {
+        const unsigned long long k = (unsigned long long)kenv[i];
+        km = max(km, k);
+        kn = min(kn, k);
+        dm = max(dm, (unsigned long long)__double_as_longlong(dvenv[i]));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        km = max(km, (unsigned long long)__shfl_xor(km, o));
+        dm = max(dm, (unsigned long long)__shfl_xor(dm, o));
+        kn = min(kn, (unsigned long long)__shfl_xor(kn, o));
+    }
+    if ((threadIdx.x & 63) == 0) { sk[threadIdx.x >> 6] = km; sd[threadIdx.x >> 6] = dm; sn[threadIdx.x >> 6] = kn; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < (int)(blockDim.x >> 6); ++i) { km = max(km, sk[i]); dm = max(dm, sd[i]); kn = min(kn, sn[i]); }
+        __hip_atomic_store(host_out + 0, km, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host_out + 1, dm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host_out + 2, kn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // Early exit of a speculatively enqueued sweep: the previous sweep already met the rule.
@@ -605,7 +635,7 @@ vi_sweep_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, const T 
     auto fetch = [&](int e) {
 #pragma unroll
         for (int r = 0; r < (PREFETCH ? kPrefetchRegs : 1); ++r) {
-            const int i = threadIdx.x + r * kSweepBlock;
+            const int i = threadIdx.x + r * blockDim.x;
             if (i < nv16) rv[r] = Vin16[(long long)e * nv16 + i];
         }
         if ((int)threadIdx.x < nc16) rc = C16[(long long)e * nc16 + threadIdx.x];
@@ -619,7 +649,7 @@ vi_sweep_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, const T 
         if (PREFETCH) {
 #pragma unroll
             for (int r = 0; r < kPrefetchRegs; ++r) {
-                const int i = threadIdx.x + r * kSweepBlock;
+                const int i = threadIdx.x + r * blockDim.x;
                 if (i < nv16) reinterpret_cast<uint4 *>(Vi)[i] = rv[r];
             }
             if ((int)threadIdx.x < nc16) reinterpret_cast<uint4 *>(cl)[threadIdx.x] = rc;
@@ -681,7 +711,8 @@ struct mgdp_vi {
     int fused_block = 256;
     int sweep_grid = 2048;
     int fresh = 1;          // next fused launch starts from V_0 = 0
-    bool sweep_prefetch = true;
+    bool sweep_prefetch = false;  // measured: register prefetch loses to plain staging (vmcnt drains)
+    int sweep_block = 256;
 };
 
 namespace {
@@ -756,10 +787,17 @@ int launch_fused_t(mgdp_vi *vi, int k_target) {
     if (int rc = timed_begin(vi, -1)) return rc;
     hipLaunchKernelGGL(kern, dim3(vi->d.B), dim3(vi->fused_block), L.total(), vi->stream, g,
                        make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv,
-                       vi->d_dvenv, vi->d_red, vi->d_ticket, vi->d_hout, k_target, vi->fresh);
+                       vi->d_dvenv, vi->d_red, vi->d_ticket, vi->d_hout, k_target, vi->fresh,
+                       vi->d.B <= kInKernelReduceMaxB ? 1 : 0);
     MGDP_HIP(hipGetLastError());
     vi->fresh = 0;
-    return timed_end(vi);
+    if (int rc = timed_end(vi)) return rc;
+    if (vi->d.B > kInKernelReduceMaxB) {
+        hipLaunchKernelGGL(vi_reduce_kernel, dim3(1), dim3(1024), 0, vi->stream, vi->d_kenv, vi->d_dvenv, vi->d.B,
+                           vi->d_hout);
+        MGDP_HIP(hipGetLastError());
+    }
+    return 0;
 }
 
 template <typename T, int MODEL, bool SLIP, int MAP, bool POLICY, bool PREFETCH>
@@ -768,7 +806,7 @@ int launch_sweep_kernel(mgdp_vi *vi, const T *Vin, T *Vout, int k, int check_pre
     auto kern = vi_sweep_kernel<T, MODEL, SLIP, MAP, POLICY, PREFETCH>;
     if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
     const int grid = std::min(vi->d.B, vi->sweep_grid);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kSweepBlock), L.total(), vi->stream, make_geo(vi), make_coef<T>(vi),
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(vi->sweep_block), L.total(), vi->stream, make_geo(vi), make_coef<T>(vi),
                        vi->d_cells, Vin, Vout, vi->d_pi, POLICY ? nullptr : vi->d_shards, k, check_prev);
     MGDP_HIP(hipGetLastError());
     return 0;
@@ -780,7 +818,7 @@ int launch_sweep_t(mgdp_vi *vi, int k, int check_prev, bool policy) {
     T *Vout = (T *)vi->d_V[k & 1];
     if (policy) return launch_sweep_kernel<T, MODEL, SLIP, MAP, true, false>(vi, Vin, Vout, k, 0);
     if (int rc = timed_begin(vi, k)) return rc;
-    const bool pf = vi->sweep_prefetch && (int64_t)vi->S * sizeof(T) <= (int64_t)kSweepBlock * kPrefetchRegs * 16;
+    const bool pf = vi->sweep_prefetch && (int64_t)vi->S * sizeof(T) <= (int64_t)vi->sweep_block * kPrefetchRegs * 16;
     const int rc = pf ? launch_sweep_kernel<T, MODEL, SLIP, MAP, false, true>(vi, Vin, Vout, k, check_prev)
                       : launch_sweep_kernel<T, MODEL, SLIP, MAP, false, false>(vi, Vin, Vout, k, check_prev);
     if (rc) return rc;
@@ -972,6 +1010,7 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     if (e == hipSuccess) e = hipMemset(vi->d_cells, 0, (size_t)d.B * vi->HWp);
     if (const char *ev = std::getenv("MGDP_SWEEP_PREFETCH")) vi->sweep_prefetch = std::atoi(ev) != 0;
     if (const char *ev = std::getenv("MGDP_SWEEP_GRID")) vi->sweep_grid = std::max(1, std::atoi(ev));
+    if (const char *ev = std::getenv("MGDP_SWEEP_BLOCK")) vi->sweep_block = std::min(256, std::max(64, std::atoi(ev) / 64 * 64));
     if (e == hipSuccess) {  // arm the fused reduction (every launch re-arms it for the next)
         std::vector<unsigned long long> init((size_t)kRedShards * 4 + 2, 0ull);
         for (size_t i = 2; i < (size_t)kRedShards * 4; i += 4) init[i] = 0x7fffffffull;
