@@ -98,13 +98,14 @@ __device__ __forceinline__ bool block_any(bool p, uint8_t *flags, int parity) {
 
 // ------------------------------------------------------------------------------------------------
 // Per-cell topology.  Cell types never change during a solve, so a thread that owns a cell can
-// resolve its transition structure once (from LDS or HBM) and keep it in registers for every sweep.
+// resolve its transition structure once (from LDS or HBM) and keep it in registers for every
+// sweep.  The update code below is branch-free: every case is a select on these registers.
 // ------------------------------------------------------------------------------------------------
 template <typename T>
 struct XydTopo {
     int valid;       // agent may stand here (empty / floor)
     uint32_t term;   // bit d: forward from dir d enters a terminal cell (goal / lava)
-    int nbi[4];      // V index read by forward from dir d (own state when blocked or terminal)
+    int nbi[4];      // V index read by forward from dir d (own state when blocked / terminal / invalid)
     T tq[4];         // terminal forward value: 1 (goal, R = 1) or 0 (lava)
 };
 
@@ -126,27 +127,21 @@ __device__ __forceinline__ XydTopo<T> xyd_topo(const uint8_t *cl, const Geo &geo
     return tp;
 }
 
-// One cell of the XYD model (4 states, actions 0..6).  Returns max |dV| over the cell's states.
-// Q_det: left/right/self (= pickup/drop/toggle/done) = g*V, forward per minigrid_env.py:546-553.
-// WRITE_PI = false is the value-only sweep (max without argmax); pi is extracted once at the end.
-template <typename T, bool SLIP, bool WRITE_V, bool WRITE_PI>
-__device__ __forceinline__ T xyd_update(const XydTopo<T> &tp, const Coef<T> &cf, const T *Vin, T *Vout,
-                                        int8_t *pis, int c) {
-    if (!tp.valid) {
-        if (WRITE_V) *reinterpret_cast<V4<T> *>(Vout + c * 4) = V4<T>{{(T)0, (T)0, (T)0, (T)0}};
-        if (WRITE_PI) *reinterpret_cast<int32_t *>(pis + c * 4) = -1;
-        return (T)0;
-    }
-    const V4<T> own = *reinterpret_cast<const V4<T> *>(Vin + c * 4);
+// One cell of the XYD model: own = V_{k-1} of the cell's 4 states (registers), front values read
+// from Vin.  Q_det: left/right/self (= pickup/drop/toggle/done) = g*V, forward per
+// minigrid_env.py:546-553.  Invalid cells have own = 0 and all reads pointing at themselves, so
+// they compute exactly 0.  Returns max |dV|; with WRITE_PI also packs the 4 argmax lanes.
+template <typename T, bool SLIP, bool WRITE_PI>
+__device__ __forceinline__ T xyd_step(const XydTopo<T> &tp, const Coef<T> &cf, const V4<T> &own,
+                                      const T *Vin, V4<T> &out, uint32_t &pk) {
     T nbv[4];
 #pragma unroll
     for (int d = 0; d < 4; ++d) nbv[d] = Vin[tp.nbi[d]];
     T gv[4];
 #pragma unroll
     for (int d = 0; d < 4; ++d) gv[d] = cf.g * own.v[d];
-    V4<T> out;
-    uint32_t pk = 0;
     T dv = (T)0;
+    pk = 0;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
         const T qF = ((tp.term >> d) & 1u) ? tp.tq[d] : cf.g * nbv[d];
@@ -171,91 +166,82 @@ __device__ __forceinline__ T xyd_update(const XydTopo<T> &tp, const Coef<T> &cf,
             if (a1 > best) { best = a1; arg = 1; }
             if (a2 > best) { best = a2; arg = 2; }
             if (a3 > best) { best = a3; arg = 3; }
-            pk |= (uint32_t)(uint8_t)arg << (8 * d);
+            pk |= (uint32_t)(uint8_t)(tp.valid ? arg : -1) << (8 * d);
         } else {
             best = vmax(vmax(a0, a1), vmax(a2, a3));
         }
+        best = tp.valid ? best : (T)0;  // slip mixes in constants; absorbing states stay 0
         out.v[d] = best;
         dv = vmax(dv, vabs(best - own.v[d]));
     }
-    if (WRITE_V) *reinterpret_cast<V4<T> *>(Vout + c * 4) = out;
-    if (WRITE_PI) *reinterpret_cast<uint32_t *>(pis + c * 4) = pk;
     return dv;
 }
 
-// DoorKey cell topology: own type, the 4 front-cell types and neighbour V offsets.
+// DoorKey cell topology: own walkability per (has_key, door_open) and, per direction, the front
+// cell's kind, packed in registers.
 struct DkTopo {
-    int t;
-    int tf[4];
-    int nb[4];  // V index of (front cell, dir d, has_key 0, door_open 0)
+    uint32_t walk;   // bit (hk*2+dop): the agent may stand in this cell
+    uint32_t f[4];   // per dir: bits 0-3 front walkable per (hk*2+dop), 4 goal, 5 lava, 6 key, 7 door
+    int nb[4];       // V index of (front cell, dir d, has_key 0, door_open 0)
 };
+
+__device__ __forceinline__ uint32_t dk_walk_mask(int t) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int hk = 0; hk < 2; ++hk)
+#pragma unroll
+        for (int dop = 0; dop < 2; ++dop)
+            if (dk_walk(t, hk, dop)) m |= 1u << (hk * 2 + dop);
+    return m;
+}
 
 __device__ __forceinline__ DkTopo dk_topo(const uint8_t *cl, const Geo &geo, int c) {
     DkTopo tp;
-    tp.t = cl[c];
-    const bool inner = tp.t != T_WALL && tp.t != T_GOAL && tp.t != T_LAVA;  // walkable for some (hk, door)
+    const int t = cl[c];
+    tp.walk = dk_walk_mask(t);
+    const bool inner = tp.walk != 0;  // walkable for some (hk, door): interior by validation
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
         const int cfr = inner ? c + geo.off[d] : c;
-        tp.tf[d] = inner ? cl[cfr] : T_WALL;
+        const int tf = inner ? cl[cfr] : T_WALL;
+        tp.f[d] = dk_walk_mask(tf) | (tf == T_GOAL ? 16u : 0u) | (tf == T_LAVA ? 32u : 0u) |
+                  (tf == T_KEY ? 64u : 0u) | (tf == T_DOOR ? 128u : 0u);
         tp.nb[d] = cfr * 16 + d * 4;
     }
     return tp;
 }
 
-// One cell of the DoorKey product model: 16 states l = (dir*2 + has_key)*2 + door_open,
-// action lanes left, right, forward, pickup, toggle (world_object.py:185-195, 244).
-template <typename T, bool WRITE_V, bool WRITE_PI>
-__device__ __forceinline__ T dk_update(const DkTopo &tp, const Coef<T> &cf, const T *Vin, T *Vout,
-                                       int8_t *pis, int c) {
-    const int t = tp.t;
-    if (t == T_WALL || t == T_GOAL || t == T_LAVA) {  // no (has_key, door_open) makes it walkable
-        if (WRITE_V) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                *reinterpret_cast<V4<T> *>(Vout + c * 16 + 4 * q) = V4<T>{{(T)0, (T)0, (T)0, (T)0}};
-        }
-        if (WRITE_PI) *reinterpret_cast<uint4 *>(pis + c * 16) = make_uint4(~0u, ~0u, ~0u, ~0u);
-        return (T)0;
-    }
-    const T *vc = Vin + c * 16;
-    T own[16];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const V4<T> x = *reinterpret_cast<const V4<T> *>(vc + 4 * q);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) own[4 * q + j] = x.v[j];
-    }
+// One cell of the DoorKey product model: 16 states l = (dir*2 + has_key)*2 + door_open, action
+// lanes left, right, forward, pickup, toggle (world_object.py:185-195, 244).  own = V_{k-1}.
+template <typename T, bool WRITE_PI>
+__device__ __forceinline__ T dk_step(const DkTopo &tp, const Coef<T> &cf, const T (&own)[16],
+                                     const T *Vin, T (&outv)[16], uint32_t (&pk)[4]) {
     T gv[16];
 #pragma unroll
     for (int l = 0; l < 16; ++l) gv[l] = cf.g * own[l];
-    T outv[16];
-    int8_t outp[16];
     T dv = (T)0;
 #pragma unroll
+    for (int q = 0; q < 4; ++q) pk[q] = 0;
+#pragma unroll
     for (int d = 0; d < 4; ++d) {
-        const int tf = tp.tf[d];
+        const uint32_t f = tp.f[d];
         const V4<T> nb = *reinterpret_cast<const V4<T> *>(Vin + tp.nb[d]);
+        const bool goal = f & 16u, lava = f & 32u, key = f & 64u, door = f & 128u;
 #pragma unroll
         for (int hk = 0; hk < 2; ++hk) {
 #pragma unroll
             for (int dop = 0; dop < 2; ++dop) {
                 const int l = (d * 2 + hk) * 2 + dop;
-                if (!dk_walk(t, hk, dop)) { outv[l] = (T)0; outp[l] = -1; continue; }
+                const int hd = hk * 2 + dop;
                 const T qS = gv[l];
                 const T qL = gv[(((d + 3) & 3) * 2 + hk) * 2 + dop];
                 const T qR = gv[(((d + 1) & 3) * 2 + hk) * 2 + dop];
-                T qF;
-                if (tf == T_GOAL) qF = (T)1;
-                else if (tf == T_LAVA) qF = (T)0;
-                else if (dk_walk(tf, hk, dop)) qF = cf.g * nb.v[hk * 2 + dop];
-                else qF = qS;
-                const T qP = (tf == T_KEY && !hk) ? gv[(d * 2 + 1) * 2 + dop] : qS;
-                T qT = qS;
-                if (tf == T_DOOR) {
-                    if (dop) qT = gv[(d * 2 + hk) * 2 + 0];
-                    else if (hk) qT = gv[(d * 2 + hk) * 2 + 1];
-                }
+                const T qM = ((f >> hd) & 1u) ? cf.g * nb.v[hd] : qS;
+                const T qF = goal ? (T)1 : (lava ? (T)0 : qM);
+                const T qP = (!hk && key) ? gv[(d * 2 + 1) * 2 + dop] : qS;
+                const T qD = dop ? gv[(d * 2 + hk) * 2 + 0] : (hk ? gv[(d * 2 + hk) * 2 + 1] : qS);
+                const T qT = door ? qD : qS;
+                const bool valid = (tp.walk >> hd) & 1u;
                 T best;
                 if (WRITE_PI) {
                     best = qL;
@@ -264,29 +250,51 @@ __device__ __forceinline__ T dk_update(const DkTopo &tp, const Coef<T> &cf, cons
                     if (qF > best) { best = qF; arg = 2; }
                     if (qP > best) { best = qP; arg = 3; }
                     if (qT > best) { best = qT; arg = 4; }
-                    outp[l] = (int8_t)arg;
+                    pk[l >> 2] |= (uint32_t)(uint8_t)(valid ? arg : -1) << (8 * (l & 3));
                 } else {
                     best = vmax(vmax(vmax(qL, qR), vmax(qF, qP)), qT);
                 }
+                best = valid ? best : (T)0;
                 outv[l] = best;
                 dv = vmax(dv, vabs(best - own[l]));
             }
         }
     }
+    return dv;
+}
+
+// LDS/HBM wrappers: read own values from Vin, update, write V and/or pi.
+template <typename T, bool SLIP, bool WRITE_V, bool WRITE_PI>
+__device__ __forceinline__ T xyd_update(const XydTopo<T> &tp, const Coef<T> &cf, const T *Vin, T *Vout,
+                                        int8_t *pis, int c) {
+    const V4<T> own = *reinterpret_cast<const V4<T> *>(Vin + c * 4);
+    V4<T> out;
+    uint32_t pk;
+    const T dv = xyd_step<T, SLIP, WRITE_PI>(tp, cf, own, Vin, out, pk);
+    if (WRITE_V) *reinterpret_cast<V4<T> *>(Vout + c * 4) = out;
+    if (WRITE_PI) *reinterpret_cast<uint32_t *>(pis + c * 4) = pk;
+    return dv;
+}
+
+template <typename T, bool WRITE_V, bool WRITE_PI>
+__device__ __forceinline__ T dk_update(const DkTopo &tp, const Coef<T> &cf, const T *Vin, T *Vout,
+                                       int8_t *pis, int c) {
+    T own[16], outv[16];
+    uint32_t pk[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const V4<T> x = *reinterpret_cast<const V4<T> *>(Vin + c * 16 + 4 * q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) own[4 * q + j] = x.v[j];
+    }
+    const T dv = dk_step<T, WRITE_PI>(tp, cf, own, Vin, outv, pk);
     if (WRITE_V) {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
             *reinterpret_cast<V4<T> *>(Vout + c * 16 + 4 * q) =
                 V4<T>{{outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]}};
     }
-    if (WRITE_PI) {
-        uint32_t w[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            w[q] = (uint32_t)(uint8_t)outp[4 * q] | ((uint32_t)(uint8_t)outp[4 * q + 1] << 8) |
-                   ((uint32_t)(uint8_t)outp[4 * q + 2] << 16) | ((uint32_t)(uint8_t)outp[4 * q + 3] << 24);
-        *reinterpret_cast<uint4 *>(pis + c * 16) = make_uint4(w[0], w[1], w[2], w[3]);
-    }
+    if (WRITE_PI) *reinterpret_cast<uint4 *>(pis + c * 16) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
     return dv;
 }
 
@@ -509,50 +517,106 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
         __syncthreads();
 
         const bool fast = MAP == MGDP_MAP_CELL && geo.HW <= (int)blockDim.x;
-        const int c = threadIdx.x;
-        const bool own = c < geo.HW;
-        XydTopo<T> xt;
-        DkTopo dt;
-        if (fast && own) {
-            if (MODEL == MGDP_MODEL_XYD) xt = xyd_topo<T>(cl, geo, c);
-            else dt = dk_topo(cl, geo, c);
-        }
         int cur = 0, parity = 0;
         T diff = (T)0;
-        while (true) {
-            const T *Vin = cur ? V1 : V0;
-            T *Vout = cur ? V0 : V1;
-            if (fast) {
-                if (own) {
-                    if (MODEL == MGDP_MODEL_XYD) diff = xyd_update<T, SLIP, true, false>(xt, cf, Vin, Vout, pis, c);
-                    else diff = dk_update<T, true, false>(dt, cf, Vin, Vout, pis, c);
+        if (fast) {
+            // One thread per cell: topology and the cell's own V live in registers; the only LDS
+            // traffic per sweep is the front-cell reads and the cell's own write.
+            const int c = threadIdx.x;
+            const int cc = c < geo.HW ? c : 0;  // idle threads shadow cell 0 and never write
+            const bool own_cell = c < geo.HW;
+            if (MODEL == MGDP_MODEL_XYD) {
+                const XydTopo<T> tp = xyd_topo<T>(cl, geo, cc);
+                V4<T> own = *reinterpret_cast<const V4<T> *>(V0 + cc * 4);
+                while (true) {
+                    const T *Vin = cur ? V1 : V0;
+                    T *Vout = cur ? V0 : V1;
+                    V4<T> out;
+                    uint32_t pk;
+                    diff = xyd_step<T, SLIP, false>(tp, cf, own, Vin, out, pk);
+                    if (own_cell) *reinterpret_cast<V4<T> *>(Vout + cc * 4) = out;
+                    else diff = (T)0;
+                    own = out;
+                    cur ^= 1;
+                    ++k;
+                    if (k_target < 0) {
+                        const bool more = block_any((double)diff >= geo.tol, flags, parity);
+                        parity ^= 1;
+                        if (!more || k >= geo.max_sweeps) break;
+                    } else {
+                        __syncthreads();
+                        if (k >= k_target) break;
+                    }
+                }
+                dvl = (double)block_max(diff, slots, 0);
+                if (own_cell) {  // pi of the last sweep = argmax on V_{k-1} (buffer cur ^ 1)
+                    const T *Vprev = cur ? V0 : V1;
+                    xyd_update<T, SLIP, false, true>(tp, cf, Vprev, nullptr, pis, cc);
                 }
             } else {
-                diff = sweep_lds<T, MODEL, SLIP, MAP, true, MAP == MGDP_MAP_SA>(geo, cf, cl, Vin, Vout, pis);
-            }
-            cur ^= 1;
-            ++k;
-            if (k_target < 0) {
-                const bool more = block_any((double)diff >= geo.tol, flags, parity);
-                parity ^= 1;
-                if (!more || k >= geo.max_sweeps) break;
-            } else {
-                __syncthreads();
-                if (k >= k_target) break;
-            }
-        }
-        dvl = (double)block_max(diff, slots, 0);
-        if (MAP == MGDP_MAP_CELL) {  // pi of the last sweep = argmax on V_{k-1} (buffer cur ^ 1)
-            const T *Vprev = cur ? V0 : V1;
-            if (fast) {
-                if (own) {
-                    if (MODEL == MGDP_MODEL_XYD) xyd_update<T, SLIP, false, true>(xt, cf, Vprev, nullptr, pis, c);
-                    else dk_update<T, false, true>(dt, cf, Vprev, nullptr, pis, c);
+                const DkTopo tp = dk_topo(cl, geo, cc);
+                T own[16];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const V4<T> x = *reinterpret_cast<const V4<T> *>(V0 + cc * 16 + 4 * q);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) own[4 * q + j] = x.v[j];
                 }
-            } else {
-                sweep_lds<T, MODEL, SLIP, MAP, false, true>(geo, cf, cl, Vprev, nullptr, pis);
+                while (true) {
+                    const T *Vin = cur ? V1 : V0;
+                    T *Vout = cur ? V0 : V1;
+                    T outv[16];
+                    uint32_t pk[4];
+                    diff = dk_step<T, false>(tp, cf, own, Vin, outv, pk);
+                    if (own_cell) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            *reinterpret_cast<V4<T> *>(Vout + cc * 16 + 4 * q) =
+                                V4<T>{{outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]}};
+                    } else {
+                        diff = (T)0;
+                    }
+#pragma unroll
+                    for (int l = 0; l < 16; ++l) own[l] = outv[l];
+                    cur ^= 1;
+                    ++k;
+                    if (k_target < 0) {
+                        const bool more = block_any((double)diff >= geo.tol, flags, parity);
+                        parity ^= 1;
+                        if (!more || k >= geo.max_sweeps) break;
+                    } else {
+                        __syncthreads();
+                        if (k >= k_target) break;
+                    }
+                }
+                dvl = (double)block_max(diff, slots, 0);
+                if (own_cell) {
+                    const T *Vprev = cur ? V0 : V1;
+                    dk_update<T, false, true>(tp, cf, Vprev, nullptr, pis, cc);
+                }
             }
             __syncthreads();
+        } else {
+            while (true) {
+                const T *Vin = cur ? V1 : V0;
+                T *Vout = cur ? V0 : V1;
+                diff = sweep_lds<T, MODEL, SLIP, MAP, true, MAP == MGDP_MAP_SA>(geo, cf, cl, Vin, Vout, pis);
+                cur ^= 1;
+                ++k;
+                if (k_target < 0) {
+                    const bool more = block_any((double)diff >= geo.tol, flags, parity);
+                    parity ^= 1;
+                    if (!more || k >= geo.max_sweeps) break;
+                } else {
+                    __syncthreads();
+                    if (k >= k_target) break;
+                }
+            }
+            dvl = (double)block_max(diff, slots, 0);
+            if (MAP == MGDP_MAP_CELL) {  // pi of the last sweep = argmax on V_{k-1}
+                sweep_lds<T, MODEL, SLIP, MAP, false, true>(geo, cf, cl, cur ? V0 : V1, nullptr, pis);
+                __syncthreads();
+            }
         }
         copy16(V + vb, cur ? V1 : V0, L.v_bytes);
         copy_pi(pi + vb, pis, geo.S);
