@@ -25,8 +25,10 @@
 // Thread mappings (template MAP): MGDP_MAP_CELL = one thread per cell updating its 4 (XYD) or
 // 16 (DoorKey) states from 16-B LDS vectors; MGDP_MAP_SA = one thread per (state, action),
 // 8 lanes per state, wave shuffle max-reduce with the lowest action index winning ties.
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
+#include <climits>
 #include <cstring>
 #include <vector>
 
@@ -446,9 +448,23 @@ constexpr int kInKernelReduceMaxB = 512;  // above this, a separate one-workgrou
 // return before its ticket add is issued, hence the block that draws the last ticket observes all
 // of them; it combines the shards with exchanges that also re-arm them for the next launch, and
 // publishes {kmax, dV bits, kmin} to host-mapped memory.
+__device__ __forceinline__ void publish(unsigned long long *host_out, unsigned long long km,
+                                        unsigned long long dv, unsigned long long kn, unsigned int epoch) {
+    __hip_atomic_store(host_out + 0, km, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host_out + 1, dv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host_out + 2, kn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host_out + 3, (unsigned long long)epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ __forceinline__ void fused_reduce(unsigned long long *red, unsigned int *ticket,
                                              unsigned long long *host_out, int k, double dvl,
-                                             unsigned int *lds_flag) {
+                                             unsigned int *lds_flag, unsigned int epoch) {
+    if (gridDim.x == 1) {  // a lone grid publishes directly
+        if (threadIdx.x == 0)
+            publish(host_out, (unsigned long long)k, (unsigned long long)__double_as_longlong(dvl),
+                    (unsigned long long)k, epoch);
+        return;
+    }
     if (threadIdx.x == 0) {
         unsigned long long *r = red + (blockIdx.x & (kRedShards - 1)) * 4;
         const unsigned long long a = __hip_atomic_fetch_max(r + 0, (unsigned long long)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -472,9 +488,7 @@ __device__ __forceinline__ void fused_reduce(unsigned long long *red, unsigned i
         }
         if (threadIdx.x == 0) {
             __hip_atomic_exchange(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(host_out + 0, km, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(host_out + 1, dv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(host_out + 2, kn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            publish(host_out, km, dv, kn, epoch);
         }
     }
 }
@@ -494,7 +508,8 @@ __global__ void __launch_bounds__(1024)
 vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
-                unsigned long long *__restrict__ host_out, int k_target, int fresh, int in_kernel_reduce) {
+                unsigned long long *__restrict__ host_out, int k_target, int fresh, int in_kernel_reduce,
+                unsigned int epoch) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int e = blockIdx.x;
     const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T));
@@ -625,14 +640,14 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
             dvenv[e] = dvl;
         }
     }
-    if (in_kernel_reduce) fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16));
+    if (in_kernel_reduce) fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16), epoch);
 }
 
 // Large batches: one workgroup reduces the per-grid (kenv, dvenv) into host-mapped memory (a
 // single arrival ticket shared by tens of thousands of workgroups would serialise on one address).
 __global__ void __launch_bounds__(1024)
 vi_reduce_kernel(const int32_t *__restrict__ kenv, const double *__restrict__ dvenv, int B,
-                 unsigned long long *__restrict__ host_out) {
+                 unsigned long long *__restrict__ host_out, unsigned int epoch) {
     __shared__ unsigned long long sk[16], sd[16], sn[16];
     unsigned long long km = 0, dm = 0, kn = 0x7fffffffull;
     for (int i = threadIdx.x; i < B; i += blockDim.x) {
@@ -651,9 +666,7 @@ vi_reduce_kernel(const int32_t *__restrict__ kenv, const double *__restrict__ dv
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int i = 1; i < (int)(blockDim.x >> 6); ++i) { km = max(km, sk[i]); dm = max(dm, sd[i]); kn = min(kn, sn[i]); }
-        __hip_atomic_store(host_out + 0, km, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(host_out + 1, dm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(host_out + 2, kn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        publish(host_out, km, dm, kn, epoch);
     }
 }
 
@@ -775,6 +788,7 @@ struct mgdp_vi {
     int fused_block = 256;
     int sweep_grid = 2048;
     int fresh = 1;          // next fused launch starts from V_0 = 0
+    unsigned int epoch = 0; // tag of the last fused launch; its result lands in h_out[3]
     bool sweep_prefetch = false;  // measured: register prefetch loses to plain staging (vmcnt drains)
     int sweep_block = 256;
 };
@@ -823,12 +837,11 @@ int timed_end(mgdp_vi *vi) {
     MGDP_HIP(hipEventRecord(vi->ev.back().second, vi->stream));
     return 0;
 }
-// Called after a stream sync: fold recorded events into total_ms (sweep launches beyond the
-// last useful sweep no-op and are not counted).
-int timed_collect(mgdp_vi *vi, int last_sweep) {
+// Fold completed events into total_ms (called after a stream sync).  Sweep launches past the
+// stopping sweep no-op and were marked uncounted (ev_sweep = INT_MAX) by sweep_run.
+int timed_collect(mgdp_vi *vi) {
     for (size_t i = 0; i < vi->ev.size(); ++i) {
-        const int si = vi->ev_sweep[i];
-        if (si < 0 || si <= last_sweep) {
+        if (vi->ev_sweep[i] != INT32_MAX) {
             float ms = 0.f;
             MGDP_HIP(hipEventElapsedTime(&ms, vi->ev[i].first, vi->ev[i].second));
             vi->total_ms += ms;
@@ -852,13 +865,13 @@ int launch_fused_t(mgdp_vi *vi, int k_target) {
     hipLaunchKernelGGL(kern, dim3(vi->d.B), dim3(vi->fused_block), L.total(), vi->stream, g,
                        make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv,
                        vi->d_dvenv, vi->d_red, vi->d_ticket, vi->d_hout, k_target, vi->fresh,
-                       vi->d.B <= kInKernelReduceMaxB ? 1 : 0);
+                       vi->d.B <= kInKernelReduceMaxB ? 1 : 0, ++vi->epoch);
     MGDP_HIP(hipGetLastError());
     vi->fresh = 0;
     if (int rc = timed_end(vi)) return rc;
     if (vi->d.B > kInKernelReduceMaxB) {
         hipLaunchKernelGGL(vi_reduce_kernel, dim3(1), dim3(1024), 0, vi->stream, vi->d_kenv, vi->d_dvenv, vi->d.B,
-                           vi->d_hout);
+                           vi->d_hout, vi->epoch);
         MGDP_HIP(hipGetLastError());
     }
     return 0;
@@ -921,9 +934,21 @@ struct SweepF {
 
 // Read the reduction the last fused launch published to host-mapped memory: max k, max dV, min k.
 int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
-    MGDP_HIP(hipStreamSynchronize(vi->stream));
-    if (int rc = timed_collect(vi, 1 << 30)) return rc;
+    // The last workgroup (or the reduce kernel) publishes {kmax, dV, kmin, epoch} to host-mapped
+    // memory; poll the epoch instead of a stream synchronisation (lower completion latency).
+    // Everything else stays stream-ordered.  Poll the stream now and then to surface faults.
     const volatile unsigned long long *h = vi->h_out;
+    for (uint64_t spin = 0; h[3] != (unsigned long long)vi->epoch; ++spin) {
+        if ((spin & 1023) == 1023) {
+            const hipError_t q = hipStreamQuery(vi->stream);
+            if (q == hipSuccess) {
+                if (h[3] == (unsigned long long)vi->epoch) break;
+                MGDP_CHECK(false, MGDP_E_HIP, "fused launch finished without publishing its result (epoch %u)", vi->epoch);
+            }
+            if (q != hipErrorNotReady) return hip_fail(q, "fused value-iteration launch", __FILE__, __LINE__);
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
     const unsigned long long km = h[0], dvb = h[1], kmin = h[2];
     std::memcpy(&vi->dv_red, (const void *)&dvb, sizeof(double));  // non-negative doubles order like their bits
     vi->k_min = (int)kmin;
@@ -950,6 +975,7 @@ int sweep_run(mgdp_vi *vi, int k_stop, bool force, double *dv_out) {
     std::vector<unsigned long long> host(8 * chunk);
     double dv = 0.0;
     while (vi->k_done < k_stop) {
+        const size_t ev0 = vi->ev_sweep.size();
         const int n = std::min(chunk, k_stop - vi->k_done);
         for (int i = 1; i <= n; ++i)
             if (int rc = dispatch<SweepF>(vi, vi->k_done + i, force ? 0 : 1, false)) return rc;
@@ -965,7 +991,8 @@ int sweep_run(mgdp_vi *vi, int k_stop, bool force, double *dv_out) {
                 break;
             }
         }
-        if (int rc = timed_collect(vi, last)) return rc;
+        for (size_t i = ev0; i < vi->ev_sweep.size(); ++i)
+            if (vi->ev_sweep[i] > last) vi->ev_sweep[i] = INT32_MAX;
         vi->k_done = last;
         vi->cur = last & 1;
         if (stop) break;
@@ -1225,8 +1252,10 @@ int mgdp_vi_finish(mgdp_vi *vi, int32_t sweeps) {
         // pi of sweep k = argmax evaluated on V_{k-1} (bit-identical to what sweep k computed)
         if (int rc = dispatch<SweepF>(vi, sweeps, 0, true)) return rc;
         vi->cur = sweeps & 1;
+        MGDP_HIP(hipStreamSynchronize(vi->stream));
     }
-    MGDP_HIP(hipStreamSynchronize(vi->stream));
+    // fused: V and pi were written by the launch whose result was already observed; later reads
+    // (mgdp_vi_get_*) are ordered on the stream
     return 0;
 }
 
@@ -1292,6 +1321,9 @@ int mgdp_vi_enable_timing(mgdp_vi *vi, int32_t on) {
 
 int mgdp_vi_kernel_time(mgdp_vi *vi, double *total_ms, int64_t *launches) {
     MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
+    DeviceGuard guard(vi->d.device);
+    MGDP_HIP(hipStreamSynchronize(vi->stream));
+    if (int rc = timed_collect(vi)) return rc;
     if (total_ms) *total_ms = vi->total_ms;
     if (launches) *launches = vi->launches;
     return 0;
