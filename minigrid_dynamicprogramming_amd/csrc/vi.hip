@@ -98,6 +98,18 @@ __device__ __forceinline__ bool block_any(bool p, uint8_t *flags, int parity) {
     return (f.x | f.y | f.z | f.w) != 0u;
 }
 
+// Split form of block_any for loops that test the PREVIOUS sweep's flags right after the
+// barrier, in parallel with the next sweep's LDS reads: flag_write before the barrier,
+// flags_any after it (same two-parity protocol).
+__device__ __forceinline__ void flag_write(bool p, uint8_t *flags, int parity) {
+    const unsigned long long b = __ballot(p);
+    if ((threadIdx.x & 63) == 0) flags[parity * 16 + (threadIdx.x >> 6)] = b != 0ull;
+}
+__device__ __forceinline__ bool flags_any(const uint8_t *flags, int parity) {
+    const uint4 f = *reinterpret_cast<const uint4 *>(flags + parity * 16);
+    return (f.x | f.y | f.z | f.w) != 0u;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Per-cell topology.  Cell types never change during a solve, so a thread that owns a cell can
 // resolve its transition structure once (from LDS or HBM) and keep it in registers for every
@@ -133,12 +145,15 @@ __device__ __forceinline__ XydTopo<T> xyd_topo(const uint8_t *cl, const Geo &geo
 // from Vin.  Q_det: left/right/self (= pickup/drop/toggle/done) = g*V, forward per
 // minigrid_env.py:546-553.  Invalid cells have own = 0 and all reads pointing at themselves, so
 // they compute exactly 0.  Returns max |dV|; with WRITE_PI also packs the 4 argmax lanes.
-template <typename T, bool SLIP, bool WRITE_PI>
-__device__ __forceinline__ T xyd_step(const XydTopo<T> &tp, const Coef<T> &cf, const V4<T> &own,
-                                      const T *Vin, V4<T> &out, uint32_t &pk) {
-    T nbv[4];
+template <typename T>
+__device__ __forceinline__ void xyd_load_nb(const XydTopo<T> &tp, const T *Vin, T (&nbv)[4]) {
 #pragma unroll
     for (int d = 0; d < 4; ++d) nbv[d] = Vin[tp.nbi[d]];
+}
+
+template <typename T, bool SLIP, bool WRITE_PI>
+__device__ __forceinline__ T xyd_step(const XydTopo<T> &tp, const Coef<T> &cf, const V4<T> &own,
+                                      const T (&nbv)[4], V4<T> &out, uint32_t &pk) {
     T gv[4];
 #pragma unroll
     for (int d = 0; d < 4; ++d) gv[d] = cf.g * own.v[d];
@@ -215,9 +230,15 @@ __device__ __forceinline__ DkTopo dk_topo(const uint8_t *cl, const Geo &geo, int
 
 // One cell of the DoorKey product model: 16 states l = (dir*2 + has_key)*2 + door_open, action
 // lanes left, right, forward, pickup, toggle (world_object.py:185-195, 244).  own = V_{k-1}.
+template <typename T>
+__device__ __forceinline__ void dk_load_nb(const DkTopo &tp, const T *Vin, V4<T> (&nb)[4]) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) nb[d] = *reinterpret_cast<const V4<T> *>(Vin + tp.nb[d]);
+}
+
 template <typename T, bool WRITE_PI>
 __device__ __forceinline__ T dk_step(const DkTopo &tp, const Coef<T> &cf, const T (&own)[16],
-                                     const T *Vin, T (&outv)[16], uint32_t (&pk)[4]) {
+                                     const V4<T> (&nbs)[4], T (&outv)[16], uint32_t (&pk)[4]) {
     T gv[16];
 #pragma unroll
     for (int l = 0; l < 16; ++l) gv[l] = cf.g * own[l];
@@ -227,7 +248,7 @@ __device__ __forceinline__ T dk_step(const DkTopo &tp, const Coef<T> &cf, const 
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
         const uint32_t f = tp.f[d];
-        const V4<T> nb = *reinterpret_cast<const V4<T> *>(Vin + tp.nb[d]);
+        const V4<T> &nb = nbs[d];
         const bool goal = f & 16u, lava = f & 32u, key = f & 64u, door = f & 128u;
 #pragma unroll
         for (int hk = 0; hk < 2; ++hk) {
@@ -270,9 +291,11 @@ template <typename T, bool SLIP, bool WRITE_V, bool WRITE_PI>
 __device__ __forceinline__ T xyd_update(const XydTopo<T> &tp, const Coef<T> &cf, const T *Vin, T *Vout,
                                         int8_t *pis, int c) {
     const V4<T> own = *reinterpret_cast<const V4<T> *>(Vin + c * 4);
+    T nbv[4];
+    xyd_load_nb(tp, Vin, nbv);
     V4<T> out;
     uint32_t pk;
-    const T dv = xyd_step<T, SLIP, WRITE_PI>(tp, cf, own, Vin, out, pk);
+    const T dv = xyd_step<T, SLIP, WRITE_PI>(tp, cf, own, nbv, out, pk);
     if (WRITE_V) *reinterpret_cast<V4<T> *>(Vout + c * 4) = out;
     if (WRITE_PI) *reinterpret_cast<uint32_t *>(pis + c * 4) = pk;
     return dv;
@@ -289,7 +312,9 @@ __device__ __forceinline__ T dk_update(const DkTopo &tp, const Coef<T> &cf, cons
 #pragma unroll
         for (int j = 0; j < 4; ++j) own[4 * q + j] = x.v[j];
     }
-    const T dv = dk_step<T, WRITE_PI>(tp, cf, own, Vin, outv, pk);
+    V4<T> nbs[4];
+    dk_load_nb(tp, Vin, nbs);
+    const T dv = dk_step<T, WRITE_PI>(tp, cf, own, nbs, outv, pk);
     if (WRITE_V) {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -450,10 +475,14 @@ constexpr int kInKernelReduceMaxB = 512;  // above this, a separate one-workgrou
 // publishes {kmax, dV bits, kmin} to host-mapped memory.
 __device__ __forceinline__ void publish(unsigned long long *host_out, unsigned long long km,
                                         unsigned long long dv, unsigned long long kn, unsigned int epoch) {
+    // The host polls host_out[3]; the three values are acknowledged (vmcnt drained) before the
+    // epoch word is stored, so the host sees them first.  No L2 write-back (release) is needed:
+    // V and pi are consumed only by later stream-ordered operations.
     __hip_atomic_store(host_out + 0, km, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(host_out + 1, dv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(host_out + 2, kn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(host_out + 3, (unsigned long long)epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(host_out + 3, (unsigned long long)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __device__ __forceinline__ void fused_reduce(unsigned long long *red, unsigned int *ticket,
@@ -540,28 +569,35 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
             const int c = threadIdx.x;
             const int cc = c < geo.HW ? c : 0;  // idle threads shadow cell 0 and never write
             const bool own_cell = c < geo.HW;
+            // Loop control: right after each barrier the previous sweep's convergence flags are
+            // read together with this sweep's front-cell values (independent LDS reads), so the
+            // stop test costs no extra LDS round trip.
+            const int k_start = k;
+            auto stop_now = [&]() -> bool {
+                if (k_target >= 0) return k >= k_target;
+                if (k >= geo.max_sweeps) return true;
+                return k > k_start && !flags_any(flags, parity ^ 1);
+            };
             if (MODEL == MGDP_MODEL_XYD) {
                 const XydTopo<T> tp = xyd_topo<T>(cl, geo, cc);
                 V4<T> own = *reinterpret_cast<const V4<T> *>(V0 + cc * 4);
                 while (true) {
                     const T *Vin = cur ? V1 : V0;
                     T *Vout = cur ? V0 : V1;
+                    T nbv[4];
+                    xyd_load_nb(tp, Vin, nbv);
+                    if (stop_now()) break;
                     V4<T> out;
                     uint32_t pk;
-                    diff = xyd_step<T, SLIP, false>(tp, cf, own, Vin, out, pk);
+                    const T d = xyd_step<T, SLIP, false>(tp, cf, own, nbv, out, pk);
+                    diff = own_cell ? d : (T)0;
                     if (own_cell) *reinterpret_cast<V4<T> *>(Vout + cc * 4) = out;
-                    else diff = (T)0;
                     own = out;
+                    if (k_target < 0) flag_write((double)diff >= geo.tol, flags, parity);
+                    __syncthreads();
+                    parity ^= 1;
                     cur ^= 1;
                     ++k;
-                    if (k_target < 0) {
-                        const bool more = block_any((double)diff >= geo.tol, flags, parity);
-                        parity ^= 1;
-                        if (!more || k >= geo.max_sweeps) break;
-                    } else {
-                        __syncthreads();
-                        if (k >= k_target) break;
-                    }
                 }
                 dvl = (double)block_max(diff, slots, 0);
                 if (own_cell) {  // pi of the last sweep = argmax on V_{k-1} (buffer cur ^ 1)
@@ -580,29 +616,26 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
                 while (true) {
                     const T *Vin = cur ? V1 : V0;
                     T *Vout = cur ? V0 : V1;
+                    V4<T> nbs[4];
+                    dk_load_nb(tp, Vin, nbs);
+                    if (stop_now()) break;
                     T outv[16];
                     uint32_t pk[4];
-                    diff = dk_step<T, false>(tp, cf, own, Vin, outv, pk);
+                    const T d = dk_step<T, false>(tp, cf, own, nbs, outv, pk);
+                    diff = own_cell ? d : (T)0;
                     if (own_cell) {
 #pragma unroll
                         for (int q = 0; q < 4; ++q)
                             *reinterpret_cast<V4<T> *>(Vout + cc * 16 + 4 * q) =
                                 V4<T>{{outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]}};
-                    } else {
-                        diff = (T)0;
                     }
 #pragma unroll
                     for (int l = 0; l < 16; ++l) own[l] = outv[l];
+                    if (k_target < 0) flag_write((double)diff >= geo.tol, flags, parity);
+                    __syncthreads();
+                    parity ^= 1;
                     cur ^= 1;
                     ++k;
-                    if (k_target < 0) {
-                        const bool more = block_any((double)diff >= geo.tol, flags, parity);
-                        parity ^= 1;
-                        if (!more || k >= geo.max_sweeps) break;
-                    } else {
-                        __syncthreads();
-                        if (k >= k_target) break;
-                    }
                 }
                 dvl = (double)block_max(diff, slots, 0);
                 if (own_cell) {
