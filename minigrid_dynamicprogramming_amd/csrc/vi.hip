@@ -522,6 +522,89 @@ __device__ __forceinline__ void fused_reduce(unsigned long long *red, unsigned i
     }
 }
 
+// Fast path of the fused solve (MAP_CELL, HW <= blockDim): one thread per cell, topology and
+// the cell's own V in registers; per sweep the only LDS traffic is the 4 front-cell reads and the
+// cell's own write.  LOCAL: stop on this grid's own rule; else run to k_target.  Right after each
+// barrier the previous sweep's convergence flags are read together with this sweep's front-cell
+// values (independent LDS reads), so the stop test costs no extra LDS round trip.
+template <typename T, int MODEL, bool SLIP, bool LOCAL>
+__device__ __forceinline__ void fused_fast(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *V0,
+                                           T *V1, int8_t *pis, T *slots, uint8_t *flags, int &k,
+                                           int k_target, int &cur, double &dvl) {
+    const int c = threadIdx.x;
+    const int cc = c < geo.HW ? c : 0;  // idle threads shadow cell 0 and never write
+    const bool own_cell = c < geo.HW;
+    const int k_start = k;
+    int parity = 0;
+    T diff = (T)0;
+    auto stop_now = [&]() -> bool {
+        if (!LOCAL) return k >= k_target;
+        if (k >= geo.max_sweeps) return true;
+        return k > k_start && !flags_any(flags, parity ^ 1);
+    };
+    if (MODEL == MGDP_MODEL_XYD) {
+        const XydTopo<T> tp = xyd_topo<T>(cl, geo, cc);
+        V4<T> own = *reinterpret_cast<const V4<T> *>(V0 + cc * 4);
+        while (true) {
+            const T *Vin = cur ? V1 : V0;
+            T *Vout = cur ? V0 : V1;
+            T nbv[4];
+            xyd_load_nb(tp, Vin, nbv);
+            if (stop_now()) break;
+            V4<T> out;
+            uint32_t pk;
+            const T d = xyd_step<T, SLIP, false>(tp, cf, own, nbv, out, pk);
+            diff = own_cell ? d : (T)0;
+            if (own_cell) *reinterpret_cast<V4<T> *>(Vout + cc * 4) = out;
+            own = out;
+            if (LOCAL) flag_write((double)diff >= geo.tol, flags, parity);
+            __syncthreads();
+            parity ^= 1;
+            cur ^= 1;
+            ++k;
+        }
+        dvl = (double)block_max(diff, slots, 0);
+        if (own_cell)  // pi of the last sweep = argmax on V_{k-1} (buffer cur ^ 1)
+            xyd_update<T, SLIP, false, true>(tp, cf, cur ? V0 : V1, nullptr, pis, cc);
+    } else {
+        const DkTopo tp = dk_topo(cl, geo, cc);
+        T own[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const V4<T> x = *reinterpret_cast<const V4<T> *>(V0 + cc * 16 + 4 * q);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) own[4 * q + j] = x.v[j];
+        }
+        while (true) {
+            const T *Vin = cur ? V1 : V0;
+            T *Vout = cur ? V0 : V1;
+            V4<T> nbs[4];
+            dk_load_nb(tp, Vin, nbs);
+            if (stop_now()) break;
+            T outv[16];
+            uint32_t pk[4];
+            const T d = dk_step<T, false>(tp, cf, own, nbs, outv, pk);
+            diff = own_cell ? d : (T)0;
+            if (own_cell) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    *reinterpret_cast<V4<T> *>(Vout + cc * 16 + 4 * q) =
+                        V4<T>{{outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]}};
+            }
+#pragma unroll
+            for (int l = 0; l < 16; ++l) own[l] = outv[l];
+            if (LOCAL) flag_write((double)diff >= geo.tol, flags, parity);
+            __syncthreads();
+            parity ^= 1;
+            cur ^= 1;
+            ++k;
+        }
+        dvl = (double)block_max(diff, slots, 0);
+        if (own_cell) dk_update<T, false, true>(tp, cf, cur ? V0 : V1, nullptr, pis, cc);
+    }
+    __syncthreads();
+}
+
 // ------------------------------------------------------------------------------------------------
 // Fused solve: blockIdx.x = grid index; the grid's cells, both V buffers and pi stay in LDS for
 // every sweep of the launch.  k_target < 0: sweep until this grid's own max|dV| < tol (or
@@ -564,86 +647,8 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
         int cur = 0, parity = 0;
         T diff = (T)0;
         if (fast) {
-            // One thread per cell: topology and the cell's own V live in registers; the only LDS
-            // traffic per sweep is the front-cell reads and the cell's own write.
-            const int c = threadIdx.x;
-            const int cc = c < geo.HW ? c : 0;  // idle threads shadow cell 0 and never write
-            const bool own_cell = c < geo.HW;
-            // Loop control: right after each barrier the previous sweep's convergence flags are
-            // read together with this sweep's front-cell values (independent LDS reads), so the
-            // stop test costs no extra LDS round trip.
-            const int k_start = k;
-            auto stop_now = [&]() -> bool {
-                if (k_target >= 0) return k >= k_target;
-                if (k >= geo.max_sweeps) return true;
-                return k > k_start && !flags_any(flags, parity ^ 1);
-            };
-            if (MODEL == MGDP_MODEL_XYD) {
-                const XydTopo<T> tp = xyd_topo<T>(cl, geo, cc);
-                V4<T> own = *reinterpret_cast<const V4<T> *>(V0 + cc * 4);
-                while (true) {
-                    const T *Vin = cur ? V1 : V0;
-                    T *Vout = cur ? V0 : V1;
-                    T nbv[4];
-                    xyd_load_nb(tp, Vin, nbv);
-                    if (stop_now()) break;
-                    V4<T> out;
-                    uint32_t pk;
-                    const T d = xyd_step<T, SLIP, false>(tp, cf, own, nbv, out, pk);
-                    diff = own_cell ? d : (T)0;
-                    if (own_cell) *reinterpret_cast<V4<T> *>(Vout + cc * 4) = out;
-                    own = out;
-                    if (k_target < 0) flag_write((double)diff >= geo.tol, flags, parity);
-                    __syncthreads();
-                    parity ^= 1;
-                    cur ^= 1;
-                    ++k;
-                }
-                dvl = (double)block_max(diff, slots, 0);
-                if (own_cell) {  // pi of the last sweep = argmax on V_{k-1} (buffer cur ^ 1)
-                    const T *Vprev = cur ? V0 : V1;
-                    xyd_update<T, SLIP, false, true>(tp, cf, Vprev, nullptr, pis, cc);
-                }
-            } else {
-                const DkTopo tp = dk_topo(cl, geo, cc);
-                T own[16];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const V4<T> x = *reinterpret_cast<const V4<T> *>(V0 + cc * 16 + 4 * q);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) own[4 * q + j] = x.v[j];
-                }
-                while (true) {
-                    const T *Vin = cur ? V1 : V0;
-                    T *Vout = cur ? V0 : V1;
-                    V4<T> nbs[4];
-                    dk_load_nb(tp, Vin, nbs);
-                    if (stop_now()) break;
-                    T outv[16];
-                    uint32_t pk[4];
-                    const T d = dk_step<T, false>(tp, cf, own, nbs, outv, pk);
-                    diff = own_cell ? d : (T)0;
-                    if (own_cell) {
-#pragma unroll
-                        for (int q = 0; q < 4; ++q)
-                            *reinterpret_cast<V4<T> *>(Vout + cc * 16 + 4 * q) =
-                                V4<T>{{outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]}};
-                    }
-#pragma unroll
-                    for (int l = 0; l < 16; ++l) own[l] = outv[l];
-                    if (k_target < 0) flag_write((double)diff >= geo.tol, flags, parity);
-                    __syncthreads();
-                    parity ^= 1;
-                    cur ^= 1;
-                    ++k;
-                }
-                dvl = (double)block_max(diff, slots, 0);
-                if (own_cell) {
-                    const T *Vprev = cur ? V0 : V1;
-                    dk_update<T, false, true>(tp, cf, Vprev, nullptr, pis, cc);
-                }
-            }
-            __syncthreads();
+            if (k_target < 0) fused_fast<T, MODEL, SLIP, true>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl);
+            else fused_fast<T, MODEL, SLIP, false>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl);
         } else {
             while (true) {
                 const T *Vin = cur ? V1 : V0;
