@@ -1,0 +1,51 @@
+"""Turn rocprofv3 --pmc passes (tools/pmc_traffic.sh) into profiles/pmc_traffic.json.
+
+HBM bytes per launch = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes).  The factor 2 is the gfx950
+correction of MI355X_MICROARCH.md section HBM: FETCH_SIZE reports exactly half the bytes of a wide
+coalesced streaming read.  Launches that wrote nothing (speculatively enqueued sweeps that exit
+immediately) are excluded, matching bench.py's event accounting."""
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+SRC = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+OUT = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_traffic.json"
+RUNS = {
+    "empty16": ("empty16/fused/cell/f32", "vi_fused_kernel"),
+    "empty16x65536_sweep": ("empty16x65536/sweep/cell/f32", "vi_sweep_kernel"),
+    "empty16x65536_fused": ("empty16x65536/fused/cell/f32", "vi_fused_kernel"),
+    "doorkey65536_fused": ("doorkey65536/fused/cell/f32", "vi_fused_kernel"),
+}
+
+
+def per_dispatch(path, kernel):
+    vals = []
+    for r in csv.DictReader(open(path)):
+        if r["Kernel_Name"].startswith(kernel):
+            vals.append(float(r["Counter_Value"]) * 1024.0)
+    return vals
+
+
+res = {}
+for run, (key, kernel) in RUNS.items():
+    f = per_dispatch(os.path.join(SRC, f"{run}_FETCH_SIZE", "run_counter_collection.csv"), kernel)
+    w = per_dispatch(os.path.join(SRC, f"{run}_WRITE_SIZE", "run_counter_collection.csv"), kernel)
+    n = min(len(f), len(w))
+    pairs = [(f[i], w[i]) for i in range(n) if w[i] > 4096]  # launches that did work
+    if not pairs:
+        continue
+    fetch = sum(p[0] for p in pairs) / len(pairs)
+    write = sum(p[1] for p in pairs) / len(pairs)
+    res[key] = {
+        "kernel": kernel,
+        "launches": len(pairs),
+        "fetch_size_bytes_raw": fetch,
+        "write_size_bytes": write,
+        "bytes_per_launch": 2.0 * fetch + write,
+        "note": "2*FETCH_SIZE + WRITE_SIZE per launch (gfx950 FETCH_SIZE half-count correction)",
+    }
+os.makedirs(os.path.dirname(OUT), exist_ok=True)
+json.dump(res, open(OUT, "w"), indent=1)
+print(json.dumps(res, indent=1))
