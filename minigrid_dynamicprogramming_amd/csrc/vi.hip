@@ -40,6 +40,7 @@ struct Geo {
     int B, W, H, HW, HWp, S;
     int off[4];  // cell offset of the front cell for dir 0..3 (+x, +y, -x, -y)
     int max_sweeps;
+    int nbuf;    // LDS V buffers of the fused kernel: 2, or 3 for the two-sweep XYD step
     double tol;
 };
 
@@ -451,16 +452,21 @@ __device__ __forceinline__ void copy_pi(int8_t *dst, const int8_t *src, int S) {
 }
 
 struct Smem {
-    int v_bytes, pi_bytes, cells_bytes, slot_bytes;
-    __host__ __device__ int total() const { return 2 * v_bytes + pi_bytes + cells_bytes + slot_bytes; }
+    int nbuf, v_bytes, pi_bytes, cells_bytes, slot_bytes;
+    __host__ __device__ int total() const { return nbuf * v_bytes + pi_bytes + cells_bytes + slot_bytes; }
+    __host__ __device__ int pi_off() const { return nbuf * v_bytes; }
+    __host__ __device__ int cells_off() const { return nbuf * v_bytes + pi_bytes; }
+    __host__ __device__ int slots_off() const { return nbuf * v_bytes + pi_bytes + cells_bytes; }
+    __host__ __device__ int flags_off() const { return slots_off() + 256; }
 };
 
-__host__ __device__ inline Smem smem_layout(int S, int HWp, int tsize) {
+__host__ __device__ inline Smem smem_layout(int S, int HWp, int tsize, int nbuf = 2) {
     Smem m;
+    m.nbuf = nbuf;
     m.v_bytes = S * tsize;  // S is a multiple of 4 -> 16-B multiple for f32, f64
     m.pi_bytes = (S + 15) / 16 * 16;
     m.cells_bytes = HWp;
-    m.slot_bytes = 2 * 16 * 8 + 32;  // block_max slots [2][16] + block_any flags [2][16]
+    m.slot_bytes = 256 + 64;  // block_max slots [2][16] x 8 B + convergence flags [2][2][16] B
     return m;
 }
 
@@ -605,6 +611,150 @@ __device__ __forceinline__ void fused_fast(const Geo &geo, const Coef<T> &cf, co
     __syncthreads();
 }
 
+// Two-sweep step for the XYD fast path (geo.nbuf == 3).  V_{k+2}[c, d] needs V_{k+1} only at
+// the cell itself and at state (front(c, d), d); the thread recomputes that neighbour state with
+// exactly the neighbour's own operations (bit-identical), so two Jacobi sweeps cost one barrier.
+// Buffers rotate: input X = V_k, outputs Y = V_{k+1}, Z = V_{k+2}; the convergence flags of both
+// sweeps are tested after the barrier, so the stopping sweep (and V_{K-1} for pi) is exact.
+template <typename T>
+struct Xyd2Topo {
+    XydTopo<T> b;
+    uint32_t nfree;   // bit d: the front cell n_d = c + off[d] is free (forward moves there)
+    uint32_t n2term;  // bit d: forward from state (n_d, d) is terminal
+    int nbase[4];     // V index of n_d's 4-state block (own block when not free)
+    int n2i[4];       // V index read by forward from (n_d, d)
+    T n2tq[4];
+};
+
+template <typename T>
+__device__ __forceinline__ Xyd2Topo<T> xyd2_topo(const uint8_t *cl, const Geo &geo, int c) {
+    Xyd2Topo<T> t;
+    t.b = xyd_topo<T>(cl, geo, c);
+    t.nfree = 0;
+    t.n2term = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const int n = c + geo.off[d];
+        const bool nf = t.b.valid && xyd_free(cl[n]);
+        t.nbase[d] = (nf ? n : c) * 4;
+        t.n2i[d] = c * 4 + d;
+        t.n2tq[d] = (T)0;
+        if (nf) {
+            t.nfree |= 1u << d;
+            const int n2 = n + geo.off[d];  // n is free, hence interior
+            const int tf = cl[n2];
+            t.n2i[d] = n * 4 + d;
+            if (tf == T_GOAL) { t.n2term |= 1u << d; t.n2tq[d] = (T)1; }
+            else if (tf == T_LAVA) { t.n2term |= 1u << d; }
+            else if (xyd_free(tf)) t.n2i[d] = n2 * 4 + d;
+        }
+    }
+    return t;
+}
+
+// Value of one XYD state from its four distinct action values (the WRITE_PI = false branch of
+// xyd_step, operation for operation).
+template <typename T, bool SLIP>
+__device__ __forceinline__ T xyd_value(const Coef<T> &cf, T qL, T qR, T qF, T qS) {
+    T a0 = qL, a1 = qR, a2 = qF, a3 = qS;
+    if (SLIP) {
+        T s6 = qL + qR;
+        s6 = s6 + qF;
+        s6 = s6 + qS;
+        s6 = s6 + qS;
+        s6 = s6 + qS;
+        const T tail = cf.c * s6;
+        a0 = cf.p * qL + tail;
+        a1 = cf.p * qR + tail;
+        a2 = cf.p * qF + tail;
+        a3 = cf.p * qS + tail;
+    }
+    return vmax(vmax(a0, a1), vmax(a2, a3));
+}
+
+template <typename T, bool SLIP, bool LOCAL>
+__device__ __forceinline__ void fused_fast_xyd2(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
+                                                T *const (&buf)[3], int8_t *pis, T *slots, uint8_t *flags,
+                                                int &k, int k_target, int &vfinal, double &dvl) {
+    const int c = threadIdx.x;
+    const int cc = c < geo.HW ? c : 0;
+    const bool own_cell = c < geo.HW;
+    const Xyd2Topo<T> tp = xyd2_topo<T>(cl, geo, cc);
+    const int limit = LOCAL ? geo.max_sweeps : k_target;
+    V4<T> own = *reinterpret_cast<const V4<T> *>(buf[0] + cc * 4);
+    int bx = 0, by = 1, bz = 2, last_n = 0, par = 0;
+    T dA = (T)0, dB = (T)0, dfin = (T)0;
+    int bfin = 0, bprev = 0, kfin = k;
+    while (true) {
+        // speculative loads from the buffer the next step would read
+        const T *X = buf[last_n == 2 ? bz : (last_n == 1 ? by : bx)];
+        V4<T> nb4[4];
+        T n2v[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            nb4[d] = *reinterpret_cast<const V4<T> *>(X + tp.nbase[d]);
+            n2v[d] = X[tp.n2i[d]];
+        }
+        if (last_n > 0) {
+            bool stop = false;
+            if (LOCAL && !flags_any(flags + (par ^ 1) * 32, 0)) {  // first sweep of the last step converged
+                stop = true; kfin = k - last_n + 1; bfin = by; bprev = bx; dfin = dA;
+            } else if (LOCAL && last_n == 2 && !flags_any(flags + (par ^ 1) * 32 + 16, 0)) {
+                stop = true; kfin = k; bfin = bz; bprev = by; dfin = dB;
+            } else if (k >= limit) {
+                stop = true; kfin = k;
+                bfin = last_n == 2 ? bz : by;
+                bprev = last_n == 2 ? by : bx;
+                dfin = last_n == 2 ? dB : dA;
+            }
+            if (stop) break;
+            if (last_n == 2) { const int t = bx; bx = bz; bz = by; by = t; }
+            else { const int t = bx; bx = by; by = bz; bz = t; }
+        }
+        const int n = k + 2 <= limit ? 2 : 1;
+        T nbv[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) nbv[d] = ((tp.nfree >> d) & 1u) ? nb4[d].v[d] : own.v[d];
+        V4<T> out1;
+        uint32_t pk;
+        dA = xyd_step<T, SLIP, false>(tp.b, cf, own, nbv, out1, pk);
+        if (own_cell) *reinterpret_cast<V4<T> *>(buf[by] + cc * 4) = out1;
+        else dA = (T)0;
+        if (n == 2) {
+            T nbv2[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const V4<T> &nv = nb4[d];
+                const T qL = cf.g * nv.v[(d + 3) & 3], qR = cf.g * nv.v[(d + 1) & 3], qS = cf.g * nv.v[d];
+                const T qF = ((tp.n2term >> d) & 1u) ? tp.n2tq[d] : cf.g * n2v[d];
+                const T vn = xyd_value<T, SLIP>(cf, qL, qR, qF, qS);  // V_{k+1}[n_d, d]
+                nbv2[d] = ((tp.nfree >> d) & 1u) ? vn : out1.v[d];
+            }
+            V4<T> out2;
+            dB = xyd_step<T, SLIP, false>(tp.b, cf, out1, nbv2, out2, pk);
+            if (own_cell) *reinterpret_cast<V4<T> *>(buf[bz] + cc * 4) = out2;
+            else dB = (T)0;
+            own = out2;
+        } else {
+            own = out1;
+            dB = (T)0;
+        }
+        if (LOCAL) {
+            flag_write((double)dA >= geo.tol, flags + par * 32, 0);
+            if (n == 2) flag_write((double)dB >= geo.tol, flags + par * 32 + 16, 0);
+        }
+        __syncthreads();
+        par ^= 1;
+        k += n;
+        last_n = n;
+    }
+    k = kfin;
+    vfinal = bfin;
+    dvl = (double)block_max(dfin, slots, 0);
+    if (own_cell) xyd_update<T, SLIP, false, true>(tp.b, cf, buf[bprev], nullptr, pis, cc);  // pi on V_{K-1}
+    __syncthreads();
+}
+
 // ------------------------------------------------------------------------------------------------
 // Fused solve: blockIdx.x = grid index; the grid's cells, both V buffers and pi stay in LDS for
 // every sweep of the launch.  k_target < 0: sweep until this grid's own max|dV| < tol (or
@@ -624,13 +774,14 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
                 unsigned int epoch) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int e = blockIdx.x;
-    const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T));
+    const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T), geo.nbuf);
     T *V0 = reinterpret_cast<T *>(smem);
     T *V1 = reinterpret_cast<T *>(smem + L.v_bytes);
-    int8_t *pis = reinterpret_cast<int8_t *>(smem + 2 * L.v_bytes);
-    uint8_t *cl = reinterpret_cast<uint8_t *>(smem + 2 * L.v_bytes + L.pi_bytes);
-    T *slots = reinterpret_cast<T *>(smem + 2 * L.v_bytes + L.pi_bytes + L.cells_bytes);
-    uint8_t *flags = reinterpret_cast<uint8_t *>(smem + 2 * L.v_bytes + L.pi_bytes + L.cells_bytes + 256);
+    T *V2 = reinterpret_cast<T *>(smem + 2 * L.v_bytes);  // used only when geo.nbuf == 3
+    int8_t *pis = reinterpret_cast<int8_t *>(smem + L.pi_off());
+    uint8_t *cl = reinterpret_cast<uint8_t *>(smem + L.cells_off());
+    T *slots = reinterpret_cast<T *>(smem + L.slots_off());
+    uint8_t *flags = reinterpret_cast<uint8_t *>(smem + L.flags_off());
 
     int k = fresh ? 0 : kenv[e];
     double dvl = fresh ? 0.0 : dvenv[e];
@@ -640,13 +791,20 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
         copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
         if (k == 0) zero16(V0, L.v_bytes);
         else copy16(V0, V + vb, L.v_bytes);
-        if (threadIdx.x < 32) flags[threadIdx.x] = 0;
+        if (threadIdx.x < 64) flags[threadIdx.x] = 0;
         __syncthreads();
 
         const bool fast = MAP == MGDP_MAP_CELL && geo.HW <= (int)blockDim.x;
         int cur = 0, parity = 0;
         T diff = (T)0;
-        if (fast) {
+        const T *Vfinal = nullptr;
+        if (fast && MODEL == MGDP_MODEL_XYD && geo.nbuf == 3) {
+            T *const bufs[3] = {V0, V1, V2};
+            int vf = 0;
+            if (k_target < 0) fused_fast_xyd2<T, SLIP, true>(geo, cf, cl, bufs, pis, slots, flags, k, k_target, vf, dvl);
+            else fused_fast_xyd2<T, SLIP, false>(geo, cf, cl, bufs, pis, slots, flags, k, k_target, vf, dvl);
+            Vfinal = bufs[vf];
+        } else if (fast) {
             if (k_target < 0) fused_fast<T, MODEL, SLIP, true>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl);
             else fused_fast<T, MODEL, SLIP, false>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl);
         } else {
@@ -671,7 +829,7 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
                 __syncthreads();
             }
         }
-        copy16(V + vb, cur ? V1 : V0, L.v_bytes);
+        copy16(V + vb, Vfinal ? Vfinal : (cur ? V1 : V0), L.v_bytes);
         copy_pi(pi + vb, pis, geo.S);
         if (threadIdx.x == 0) {
             kenv[e] = k;
@@ -738,9 +896,9 @@ vi_sweep_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, const T 
     const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T));
     T *Vi = reinterpret_cast<T *>(smem);
     T *Vo = reinterpret_cast<T *>(smem + L.v_bytes);
-    int8_t *pis = reinterpret_cast<int8_t *>(smem + 2 * L.v_bytes);
-    uint8_t *cl = reinterpret_cast<uint8_t *>(smem + 2 * L.v_bytes + L.pi_bytes);
-    T *slots = reinterpret_cast<T *>(smem + 2 * L.v_bytes + L.pi_bytes + L.cells_bytes);
+    int8_t *pis = reinterpret_cast<int8_t *>(smem + L.pi_off());
+    uint8_t *cl = reinterpret_cast<uint8_t *>(smem + L.cells_off());
+    T *slots = reinterpret_cast<T *>(smem + L.slots_off());
     const int nv16 = L.v_bytes >> 4, nc16 = geo.HWp >> 4;
     const uint4 *Vin16 = reinterpret_cast<const uint4 *>(Vin);
     const uint4 *C16 = reinterpret_cast<const uint4 *>(cells);
@@ -827,6 +985,7 @@ struct mgdp_vi {
     int sweep_grid = 2048;
     int fresh = 1;          // next fused launch starts from V_0 = 0
     unsigned int epoch = 0; // tag of the last fused launch; its result lands in h_out[3]
+    int nbuf = 2;                 // fused LDS V buffers (3 = two-sweep XYD step)
     bool sweep_prefetch = false;  // measured: register prefetch loses to plain staging (vmcnt drains)
     int sweep_block = 256;
 };
@@ -846,6 +1005,7 @@ Geo make_geo(const mgdp_vi *vi) {
     g.off[2] = -1;
     g.off[3] = -vi->d.W;
     g.max_sweeps = vi->d.max_sweeps;
+    g.nbuf = vi->nbuf;
     g.tol = vi->d.tol;
     return g;
 }
@@ -896,7 +1056,7 @@ int timed_collect(mgdp_vi *vi) {
 template <typename T, int MODEL, bool SLIP, int MAP>
 int launch_fused_t(mgdp_vi *vi, int k_target) {
     const Geo g = make_geo(vi);
-    const Smem L = smem_layout(vi->S, vi->HWp, sizeof(T));
+    const Smem L = smem_layout(vi->S, vi->HWp, sizeof(T), vi->nbuf);
     auto kern = vi_fused_kernel<T, MODEL, SLIP, MAP>;
     if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
     if (int rc = timed_begin(vi, -1)) return rc;
@@ -1102,7 +1262,15 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     vi->S = vi->HW * (d.model == MGDP_MODEL_XYD ? 4 : 16);
     vi->A = d.model == MGDP_MODEL_XYD ? 7 : 5;
     vi->tsize = d.dtype == MGDP_F32 ? 4 : 8;
-    const Smem L = smem_layout(vi->S, vi->HWp, vi->tsize);
+    // Two-sweep XYD step (3 LDS buffers): halves the barriers of the latency-bound fused loop;
+    // it costs 1.5x the VALU work, so by default it is used for small batches only.
+    {
+        const bool eligible = d.model == MGDP_MODEL_XYD && d.mapping == MGDP_MAP_CELL && vi->HW <= 1024;
+        int pair = d.B <= 64 ? 1 : 0;
+        if (const char *ev = std::getenv("MGDP_PAIR")) pair = std::atoi(ev);
+        vi->nbuf = eligible && pair ? 3 : 2;
+    }
+    const Smem L = smem_layout(vi->S, vi->HWp, vi->tsize, vi->nbuf);
     if (L.total() > 160 * 1024) {
         delete vi;
         set_error("grid too large for the LDS-resident kernels (%d B > 160 KiB)", L.total());

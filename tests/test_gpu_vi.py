@@ -159,3 +159,27 @@ def test_invalid_grids_raise():
     open_border[0, 0, 2] = 1
     with pytest.raises(ValueError):
         mg.value_iteration(open_border, model="xyd")
+
+
+@pytest.mark.parametrize("pair", ["0", "1"])
+@pytest.mark.parametrize("slip", [None, 0.9])
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_one_and_two_sweep_steps_bit_exact(pair, slip, dtype, monkeypatch):
+    """The fused XYD kernel's two-sweep step (3 LDS buffers) and one-sweep step agree with the oracle."""
+    monkeypatch.setenv("MGDP_PAIR", pair)
+    for env in ("fourrooms", "lava11n5"):
+        g = load(f"grids_{env}.npz")
+        cells = np.stack([cells_from_enc(e) for e in g["enc"]])
+        for sub in (cells[:1], cells[:7], cells):
+            r = gpu_vi(sub, "xyd", dtype, "fused", "cell", slip=slip)
+            o = oracle.value_iteration(0, sub, slip_p=slip, dtype=dtype)
+            assert r.sweeps == o["sweeps"]
+            np.testing.assert_array_equal(r.V, o["V"])
+            np.testing.assert_array_equal(r.pi, o["pi"])
+    t = load("table_empty16_s0.npz")
+    for ms in (1, 2, 9, 10, 11):  # odd/even caps end on a one-sweep step
+        r = gpu_vi(cells_from_enc(t["enc"]), "xyd", dtype, "fused", "cell", slip=slip, max_sweeps=ms)
+        o = oracle.value_iteration(0, cells_from_enc(t["enc"]), slip_p=slip, dtype=dtype, max_sweeps=ms)
+        assert r.sweeps == o["sweeps"] == ms
+        np.testing.assert_array_equal(r.V, o["V"])
+        np.testing.assert_array_equal(r.pi, o["pi"])
