@@ -1262,11 +1262,11 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     vi->S = vi->HW * (d.model == MGDP_MODEL_XYD ? 4 : 16);
     vi->A = d.model == MGDP_MODEL_XYD ? 7 : 5;
     vi->tsize = d.dtype == MGDP_F32 ? 4 : 8;
-    // Two-sweep XYD step (3 LDS buffers): halves the barriers of the latency-bound fused loop;
-    // it costs 1.5x the VALU work, so by default it is used for small batches only.
+    // Two-sweep XYD step (3 LDS buffers): halves the barriers of the fused loop at 1.5x the VALU
+    // work.  Off by default (MGDP_PAIR=1 enables it; tests cover both steps).
     {
         const bool eligible = d.model == MGDP_MODEL_XYD && d.mapping == MGDP_MAP_CELL && vi->HW <= 1024;
-        int pair = d.B <= 64 ? 1 : 0;
+        int pair = 0;  // measured slower than the one-sweep step on MI355X (VALU chain, not barriers, bound it)
         if (const char *ev = std::getenv("MGDP_PAIR")) pair = std::atoi(ev);
         vi->nbuf = eligible && pair ? 3 : 2;
     }
