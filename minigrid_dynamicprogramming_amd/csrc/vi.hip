@@ -41,6 +41,7 @@ struct Geo {
     int off[4];  // cell offset of the front cell for dir 0..3 (+x, +y, -x, -y)
     int max_sweeps;
     int nbuf;    // LDS V buffers of the fused kernel: 2, or 3 for the two-sweep XYD step
+    int quad;    // fused XYD: 4 threads per cell (one per direction) instead of one
     double tol;
 };
 
@@ -755,6 +756,99 @@ __device__ __forceinline__ void fused_fast_xyd2(const Geo &geo, const Coef<T> &c
     __syncthreads();
 }
 
+// DPP quad permutation (lane i of each group of 4 reads lane CTRL[i]); all lanes must be active.
+template <int CTRL>
+__device__ __forceinline__ float quad_perm(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double quad_perm(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+constexpr int kQuadLeft = 0x93;   // lane d reads lane (d+3)&3: the state after turning left
+constexpr int kQuadRight = 0x39;  // lane d reads lane (d+1)&3: the state after turning right
+
+// XYD fused fast path with 4 threads per cell, one per direction (geo.quad): each lane holds its
+// state's V in a register, gets the left/right-turn values from its quad by DPP (no LDS), reads
+// only the forward value from LDS and writes one word.  Shorter dependency chain per sweep than
+// one thread per cell; needs 4*HW <= blockDim.
+template <typename T, bool SLIP, bool LOCAL>
+__device__ __forceinline__ void fused_quad_xyd(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *V0,
+                                               T *V1, int8_t *pis, T *slots, uint8_t *flags, int &k,
+                                               int k_target, int &cur, double &dvl) {
+    const int c = threadIdx.x >> 2, d = threadIdx.x & 3;
+    const bool own_cell = c < geo.HW;
+    const int cc = own_cell ? c : 0;
+    const int s = cc * 4 + d;
+    const bool valid = own_cell && xyd_free(cl[cc]);
+    bool term = false;
+    T tq = (T)0;
+    int nbi = s;
+    if (valid) {
+        const int cfr = cc + geo.off[d];
+        const int tf = cl[cfr];
+        if (tf == T_GOAL) { term = true; tq = (T)1; }
+        else if (tf == T_LAVA) { term = true; }
+        else if (xyd_free(tf)) nbi = cfr * 4 + d;
+    }
+    const int k_start = k;
+    int parity = 0;
+    T v = (cur ? V1 : V0)[s];
+    T vprev = v;
+    T diff = (T)0;
+    while (true) {
+        const T *Vin = cur ? V1 : V0;
+        T *Vout = cur ? V0 : V1;
+        const T nb = Vin[nbi];
+        const T vl = quad_perm<kQuadLeft>(v), vr = quad_perm<kQuadRight>(v);
+        const bool stop = LOCAL ? (k >= geo.max_sweeps || (k > k_start && !flags_any(flags, parity ^ 1)))
+                                : k >= k_target;
+        if (stop) break;
+        const T qF = term ? tq : cf.g * nb;
+        T best = xyd_value<T, SLIP>(cf, cf.g * vl, cf.g * vr, qF, cf.g * v);
+        best = valid ? best : (T)0;
+        diff = vabs(best - v);
+        if (own_cell) Vout[s] = best;
+        vprev = v;
+        v = best;
+        if (LOCAL) flag_write((double)diff >= geo.tol, flags, parity);
+        __syncthreads();
+        parity ^= 1;
+        cur ^= 1;
+        ++k;
+    }
+    dvl = (double)block_max(diff, slots, 0);
+    {   // pi of the last sweep: argmax on V_{k-1} (vprev in registers, forward from buffer cur ^ 1)
+        const T *Vp = cur ? V0 : V1;
+        const T nb = Vp[nbi];
+        const T vl = quad_perm<kQuadLeft>(vprev), vr = quad_perm<kQuadRight>(vprev);
+        const T qL = cf.g * vl, qR = cf.g * vr, qS = cf.g * vprev, qF = term ? tq : cf.g * nb;
+        T a0 = qL, a1 = qR, a2 = qF, a3 = qS;
+        if (SLIP) {
+            T s6 = qL + qR;
+            s6 = s6 + qF;
+            s6 = s6 + qS;
+            s6 = s6 + qS;
+            s6 = s6 + qS;
+            const T tail = cf.c * s6;
+            a0 = cf.p * qL + tail;
+            a1 = cf.p * qR + tail;
+            a2 = cf.p * qF + tail;
+            a3 = cf.p * qS + tail;
+        }
+        int arg = 0;
+        T best = a0;
+        if (a1 > best) { best = a1; arg = 1; }
+        if (a2 > best) { best = a2; arg = 2; }
+        if (a3 > best) { best = a3; arg = 3; }
+        if (own_cell) pis[s] = valid ? (int8_t)arg : (int8_t)-1;
+    }
+    __syncthreads();
+}
+
 // ------------------------------------------------------------------------------------------------
 // Fused solve: blockIdx.x = grid index; the grid's cells, both V buffers and pi stay in LDS for
 // every sweep of the launch.  k_target < 0: sweep until this grid's own max|dV| < tol (or
@@ -804,6 +898,9 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
             if (k_target < 0) fused_fast_xyd2<T, SLIP, true>(geo, cf, cl, bufs, pis, slots, flags, k, k_target, vf, dvl);
             else fused_fast_xyd2<T, SLIP, false>(geo, cf, cl, bufs, pis, slots, flags, k, k_target, vf, dvl);
             Vfinal = bufs[vf];
+        } else if (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL && geo.quad && 4 * geo.HW <= (int)blockDim.x) {
+            if (k_target < 0) fused_quad_xyd<T, SLIP, true>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl);
+            else fused_quad_xyd<T, SLIP, false>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl);
         } else if (fast) {
             if (k_target < 0) fused_fast<T, MODEL, SLIP, true>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl);
             else fused_fast<T, MODEL, SLIP, false>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl);
@@ -986,6 +1083,8 @@ struct mgdp_vi {
     int fresh = 1;          // next fused launch starts from V_0 = 0
     unsigned int epoch = 0; // tag of the last fused launch; its result lands in h_out[3]
     int nbuf = 2;                 // fused LDS V buffers (3 = two-sweep XYD step)
+    int quad = 0;                 // fused XYD: 4 threads per cell
+    bool nbuf3() const { return nbuf == 3; }
     bool sweep_prefetch = false;  // measured: register prefetch loses to plain staging (vmcnt drains)
     int sweep_block = 256;
 };
@@ -1006,6 +1105,7 @@ Geo make_geo(const mgdp_vi *vi) {
     g.off[3] = -vi->d.W;
     g.max_sweeps = vi->d.max_sweeps;
     g.nbuf = vi->nbuf;
+    g.quad = vi->quad;
     g.tol = vi->d.tol;
     return g;
 }
@@ -1269,6 +1369,11 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
         int pair = 0;  // measured slower than the one-sweep step on MI355X (VALU chain, not barriers, bound it)
         if (const char *ev = std::getenv("MGDP_PAIR")) pair = std::atoi(ev);
         vi->nbuf = eligible && pair ? 3 : 2;
+        // Four threads per cell (one per direction, DPP quad exchange): for lone / small batches
+        // of grids with <= 256 cells, where the per-sweep dependency chain bounds the solve.
+        int quad = d.B <= 64 ? 1 : 0;
+        if (const char *ev = std::getenv("MGDP_QUAD")) quad = std::atoi(ev);
+        vi->quad = eligible && !vi->nbuf3() && quad && 4 * vi->HW <= 1024 ? 1 : 0;
     }
     const Smem L = smem_layout(vi->S, vi->HWp, vi->tsize, vi->nbuf);
     if (L.total() > 160 * 1024) {
@@ -1279,7 +1384,7 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     // fused: one workgroup per grid.  MAP_CELL: one thread per cell (register topology) when the
     // grid has <= 1024 cells; MAP_SA: 8 lanes per state, a lone grid gets the widest workgroup.
     if (d.mapping == MGDP_MAP_CELL) {
-        vi->fused_block = (int)std::min<int64_t>(1024, round_up(vi->HW, 64));
+        vi->fused_block = (int)std::min<int64_t>(1024, round_up(vi->HW * (vi->quad ? 4 : 1), 64));
     } else {
         int blk = d.B == 1 ? 1024 : 256;
         while (blk > 64 && blk / 2 >= vi->S * 8) blk /= 2;

@@ -161,12 +161,14 @@ def test_invalid_grids_raise():
         mg.value_iteration(open_border, model="xyd")
 
 
-@pytest.mark.parametrize("pair", ["0", "1"])
+@pytest.mark.parametrize("pair,quad", [("0", "0"), ("1", "0"), ("0", "1")])
 @pytest.mark.parametrize("slip", [None, 0.9])
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
-def test_one_and_two_sweep_steps_bit_exact(pair, slip, dtype, monkeypatch):
-    """The fused XYD kernel's two-sweep step (3 LDS buffers) and one-sweep step agree with the oracle."""
+def test_fused_xyd_variants_bit_exact(pair, quad, slip, dtype, monkeypatch):
+    """Every fused XYD loop -- one thread per cell, the two-sweep step (3 LDS buffers), four
+    threads per cell with DPP quad exchange -- agrees with the oracle bit for bit."""
     monkeypatch.setenv("MGDP_PAIR", pair)
+    monkeypatch.setenv("MGDP_QUAD", quad)
     for env in ("fourrooms", "lava11n5"):
         g = load(f"grids_{env}.npz")
         cells = np.stack([cells_from_enc(e) for e in g["enc"]])
