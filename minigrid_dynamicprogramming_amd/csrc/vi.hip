@@ -70,11 +70,34 @@ __device__ __forceinline__ double vmax(double a, double b) { return fmax(a, b); 
 __device__ __forceinline__ float vabs(float a) { return fabsf(a); }
 __device__ __forceinline__ double vabs(double a) { return fabs(a); }
 
+// DPP move of a 32/64-bit value (all lanes active).
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ float lane_read(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+__device__ __forceinline__ double lane_read(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Wave max of non-negative values: DPP within rows of 16 lanes (quad swaps, half-row and row
+// mirrors), then the four row results by readlane -- no LDS round trips.
 template <typename T>
 __device__ __forceinline__ T wave_max(T v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = tmax(v, (T)__shfl_xor(v, o));
-    return v;
+    v = tmax(v, dpp_mov<0xB1>(v));   // quad_perm [1,0,3,2]
+    v = tmax(v, dpp_mov<0x4E>(v));   // quad_perm [2,3,0,1]
+    v = tmax(v, dpp_mov<0x141>(v));  // row_half_mirror
+    v = tmax(v, dpp_mov<0x140>(v));  // row_mirror
+    return tmax(tmax(lane_read(v, 0), lane_read(v, 16)), tmax(lane_read(v, 32), lane_read(v, 48)));
 }
 
 // Block-wide max with ONE barrier; slots = [2][16] alternating by parity so that consecutive
@@ -494,9 +517,9 @@ __device__ __forceinline__ void publish(unsigned long long *host_out, unsigned l
 
 __device__ __forceinline__ void fused_reduce(unsigned long long *red, unsigned int *ticket,
                                              unsigned long long *host_out, int k, double dvl,
-                                             unsigned int *lds_flag, unsigned int epoch) {
-    if (gridDim.x == 1) {  // a lone grid publishes directly
-        if (threadIdx.x == 0)
+                                             unsigned int *lds_flag, unsigned int epoch, bool published) {
+    if (gridDim.x == 1) {  // a lone grid publishes directly (early, if it swept: see `done`)
+        if (threadIdx.x == 0 && !published)
             publish(host_out, (unsigned long long)k, (unsigned long long)__double_as_longlong(dvl),
                     (unsigned long long)k, epoch);
         return;
@@ -534,10 +557,10 @@ __device__ __forceinline__ void fused_reduce(unsigned long long *red, unsigned i
 // cell's own write.  LOCAL: stop on this grid's own rule; else run to k_target.  Right after each
 // barrier the previous sweep's convergence flags are read together with this sweep's front-cell
 // values (independent LDS reads), so the stop test costs no extra LDS round trip.
-template <typename T, int MODEL, bool SLIP, bool LOCAL>
+template <typename T, int MODEL, bool SLIP, bool LOCAL, typename Done>
 __device__ __forceinline__ void fused_fast(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *V0,
                                            T *V1, int8_t *pis, T *slots, uint8_t *flags, int &k,
-                                           int k_target, int &cur, double &dvl) {
+                                           int k_target, int &cur, double &dvl, const Done &done) {
     const int c = threadIdx.x;
     const int cc = c < geo.HW ? c : 0;  // idle threads shadow cell 0 and never write
     const bool own_cell = c < geo.HW;
@@ -571,6 +594,7 @@ __device__ __forceinline__ void fused_fast(const Geo &geo, const Coef<T> &cf, co
             ++k;
         }
         dvl = (double)block_max(diff, slots, 0);
+        done(k, dvl);
         if (own_cell)  // pi of the last sweep = argmax on V_{k-1} (buffer cur ^ 1)
             xyd_update<T, SLIP, false, true>(tp, cf, cur ? V0 : V1, nullptr, pis, cc);
     } else {
@@ -607,6 +631,7 @@ __device__ __forceinline__ void fused_fast(const Geo &geo, const Coef<T> &cf, co
             ++k;
         }
         dvl = (double)block_max(diff, slots, 0);
+        done(k, dvl);
         if (own_cell) dk_update<T, false, true>(tp, cf, cur ? V0 : V1, nullptr, pis, cc);
     }
     __syncthreads();
@@ -673,10 +698,11 @@ __device__ __forceinline__ T xyd_value(const Coef<T> &cf, T qL, T qR, T qF, T qS
     return vmax(vmax(a0, a1), vmax(a2, a3));
 }
 
-template <typename T, bool SLIP, bool LOCAL>
+template <typename T, bool SLIP, bool LOCAL, typename Done>
 __device__ __forceinline__ void fused_fast_xyd2(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
                                                 T *const (&buf)[3], int8_t *pis, T *slots, uint8_t *flags,
-                                                int &k, int k_target, int &vfinal, double &dvl) {
+                                                int &k, int k_target, int &vfinal, double &dvl,
+                                                const Done &done) {
     const int c = threadIdx.x;
     const int cc = c < geo.HW ? c : 0;
     const bool own_cell = c < geo.HW;
@@ -752,6 +778,7 @@ __device__ __forceinline__ void fused_fast_xyd2(const Geo &geo, const Coef<T> &c
     k = kfin;
     vfinal = bfin;
     dvl = (double)block_max(dfin, slots, 0);
+    done(k, dvl);
     if (own_cell) xyd_update<T, SLIP, false, true>(tp.b, cf, buf[bprev], nullptr, pis, cc);  // pi on V_{K-1}
     __syncthreads();
 }
@@ -775,10 +802,10 @@ constexpr int kQuadRight = 0x39;  // lane d reads lane (d+1)&3: the state after 
 // state's V in a register, gets the left/right-turn values from its quad by DPP (no LDS), reads
 // only the forward value from LDS and writes one word.  Shorter dependency chain per sweep than
 // one thread per cell; needs 4*HW <= blockDim.
-template <typename T, bool SLIP, bool LOCAL>
+template <typename T, bool SLIP, bool LOCAL, typename Done>
 __device__ __forceinline__ void fused_quad_xyd(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *V0,
                                                T *V1, int8_t *pis, T *slots, uint8_t *flags, int &k,
-                                               int k_target, int &cur, double &dvl) {
+                                               int k_target, int &cur, double &dvl, const Done &done) {
     const int c = threadIdx.x >> 2, d = threadIdx.x & 3;
     const bool own_cell = c < geo.HW;
     const int cc = own_cell ? c : 0;
@@ -821,6 +848,7 @@ __device__ __forceinline__ void fused_quad_xyd(const Geo &geo, const Coef<T> &cf
         ++k;
     }
     dvl = (double)block_max(diff, slots, 0);
+    done(k, dvl);
     {   // pi of the last sweep: argmax on V_{k-1} (vprev in registers, forward from buffer cur ^ 1)
         const T *Vp = cur ? V0 : V1;
         const T nb = Vp[nbi];
@@ -891,19 +919,27 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
         const bool fast = MAP == MGDP_MAP_CELL && geo.HW <= (int)blockDim.x;
         int cur = 0, parity = 0;
         T diff = (T)0;
+        // A lone grid publishes {k, dV} to the host as soon as they are known; pi extraction and
+        // the V/pi write-back then overlap the host's next launch (they stay stream-ordered).
+        const bool lone = in_kernel_reduce && gridDim.x == 1;
+        auto done = [&](int kk, double dv) {
+            if (lone && threadIdx.x == 0)
+                publish(host_out, (unsigned long long)kk, (unsigned long long)__double_as_longlong(dv),
+                        (unsigned long long)kk, epoch);
+        };
         const T *Vfinal = nullptr;
         if (fast && MODEL == MGDP_MODEL_XYD && geo.nbuf == 3) {
             T *const bufs[3] = {V0, V1, V2};
             int vf = 0;
-            if (k_target < 0) fused_fast_xyd2<T, SLIP, true>(geo, cf, cl, bufs, pis, slots, flags, k, k_target, vf, dvl);
-            else fused_fast_xyd2<T, SLIP, false>(geo, cf, cl, bufs, pis, slots, flags, k, k_target, vf, dvl);
+            if (k_target < 0) fused_fast_xyd2<T, SLIP, true>(geo, cf, cl, bufs, pis, slots, flags, k, k_target, vf, dvl, done);
+            else fused_fast_xyd2<T, SLIP, false>(geo, cf, cl, bufs, pis, slots, flags, k, k_target, vf, dvl, done);
             Vfinal = bufs[vf];
         } else if (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL && geo.quad && 4 * geo.HW <= (int)blockDim.x) {
-            if (k_target < 0) fused_quad_xyd<T, SLIP, true>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl);
-            else fused_quad_xyd<T, SLIP, false>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl);
+            if (k_target < 0) fused_quad_xyd<T, SLIP, true>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
+            else fused_quad_xyd<T, SLIP, false>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
         } else if (fast) {
-            if (k_target < 0) fused_fast<T, MODEL, SLIP, true>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl);
-            else fused_fast<T, MODEL, SLIP, false>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl);
+            if (k_target < 0) fused_fast<T, MODEL, SLIP, true>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
+            else fused_fast<T, MODEL, SLIP, false>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
         } else {
             while (true) {
                 const T *Vin = cur ? V1 : V0;
@@ -921,6 +957,7 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
                 }
             }
             dvl = (double)block_max(diff, slots, 0);
+            done(k, dvl);
             if (MAP == MGDP_MAP_CELL) {  // pi of the last sweep = argmax on V_{k-1}
                 sweep_lds<T, MODEL, SLIP, MAP, false, true>(geo, cf, cl, cur ? V0 : V1, nullptr, pis);
                 __syncthreads();
@@ -933,7 +970,7 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
             dvenv[e] = dvl;
         }
     }
-    if (in_kernel_reduce) fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16), epoch);
+    if (in_kernel_reduce) fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16), epoch, work);
 }
 
 // Large batches: one workgroup reduces the per-grid (kenv, dvenv) into host-mapped memory (a
@@ -1369,9 +1406,9 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
         int pair = 0;  // measured slower than the one-sweep step on MI355X (VALU chain, not barriers, bound it)
         if (const char *ev = std::getenv("MGDP_PAIR")) pair = std::atoi(ev);
         vi->nbuf = eligible && pair ? 3 : 2;
-        // Four threads per cell (one per direction, DPP quad exchange): for lone / small batches
-        // of grids with <= 256 cells, where the per-sweep dependency chain bounds the solve.
-        int quad = d.B <= 64 ? 1 : 0;
+        // Four threads per cell (one per direction, DPP quad exchange): MGDP_QUAD=1 enables it
+        // for grids with <= 256 cells (tests cover it).
+        int quad = 0;  // measured slower than one thread per cell (LDS/barrier latency bound it)
         if (const char *ev = std::getenv("MGDP_QUAD")) quad = std::atoi(ev);
         vi->quad = eligible && !vi->nbuf3() && quad && 4 * vi->HW <= 1024 ? 1 : 0;
     }
