@@ -1011,65 +1011,52 @@ __device__ __forceinline__ bool prev_sweep_converged(const unsigned long long *s
 }
 
 // ------------------------------------------------------------------------------------------------
-// One Jacobi sweep (index k, 1-based) of every grid, V double-buffered in HBM.  Per grid the V
-// tile and cells are staged HBM -> LDS, updated from LDS, written back with 16-B stores.  While a
-// grid is computed, the next grid's tile is already in flight into registers (PREFETCH), so the
-// HBM stream overlaps the LDS compute.  check_prev: skip when the previous sweep's global
-// max|dV| was already < tol.  POLICY: evaluate only, write pi.
+// One Jacobi sweep (index k, 1-based) of every grid, V double-buffered in HBM.  A workgroup
+// stages a group of `m` consecutive grids (their V rows and cells are contiguous in HBM) into LDS
+// with 16-B loads -- the LDS tile of the neighbourhood --, updates them from LDS and writes the
+// new rows back with 16-B stores; m > 1 keeps more bytes in flight per load phase and amortises
+// the barriers.  check_prev: skip when the previous sweep's global max|dV| was already < tol.
+// POLICY: evaluate only, write pi.
 // ------------------------------------------------------------------------------------------------
 constexpr int kSweepBlock = 256;
-constexpr int kPrefetchRegs = 8;  // 16-B registers per thread: tiles up to 32 KiB
 
-template <typename T, int MODEL, bool SLIP, int MAP, bool POLICY, bool PREFETCH>
+__host__ __device__ inline int sweep_smem_bytes(int S, int HWp, int tsize, int m) {
+    return 2 * m * S * tsize + m * ((S + 15) / 16 * 16) + m * HWp + 256;
+}
+
+template <typename T, int MODEL, bool SLIP, int MAP, bool POLICY>
 __global__ void __launch_bounds__(kSweepBlock)
 vi_sweep_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, const T *__restrict__ Vin,
                 T *__restrict__ Vout, int8_t *__restrict__ pi, unsigned long long *__restrict__ shards,
-                int k, int check_prev) {
+                int k, int check_prev, int m) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     if (check_prev && prev_sweep_converged(shards, k, geo.tol)) return;
-    const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T));
+    const int vbytes = geo.S * (int)sizeof(T), pib = (geo.S + 15) / 16 * 16;
     T *Vi = reinterpret_cast<T *>(smem);
-    T *Vo = reinterpret_cast<T *>(smem + L.v_bytes);
-    int8_t *pis = reinterpret_cast<int8_t *>(smem + L.pi_off());
-    uint8_t *cl = reinterpret_cast<uint8_t *>(smem + L.cells_off());
-    T *slots = reinterpret_cast<T *>(smem + L.slots_off());
-    const int nv16 = L.v_bytes >> 4, nc16 = geo.HWp >> 4;
-    const uint4 *Vin16 = reinterpret_cast<const uint4 *>(Vin);
-    const uint4 *C16 = reinterpret_cast<const uint4 *>(cells);
-
-    uint4 rv[PREFETCH ? kPrefetchRegs : 1];
-    uint4 rc = make_uint4(0, 0, 0, 0);
-    auto fetch = [&](int e) {
-#pragma unroll
-        for (int r = 0; r < (PREFETCH ? kPrefetchRegs : 1); ++r) {
-            const int i = threadIdx.x + r * blockDim.x;
-            if (i < nv16) rv[r] = Vin16[(long long)e * nv16 + i];
-        }
-        if ((int)threadIdx.x < nc16) rc = C16[(long long)e * nc16 + threadIdx.x];
-    };
-    if (PREFETCH && (int)blockIdx.x < geo.B) fetch(blockIdx.x);
+    T *Vo = reinterpret_cast<T *>(smem + m * vbytes);
+    int8_t *pis = reinterpret_cast<int8_t *>(smem + 2 * m * vbytes);
+    uint8_t *cl = reinterpret_cast<uint8_t *>(smem + 2 * m * vbytes + m * pib);
+    T *slots = reinterpret_cast<T *>(smem + 2 * m * vbytes + m * pib + m * geo.HWp);
+    const int ngroups = (geo.B + m - 1) / m;
 
     T acc = (T)0;
-    for (int e = blockIdx.x; e < geo.B; e += gridDim.x) {
-        const long long vb = (long long)e * geo.S;
-        __syncthreads();  // the previous grid's LDS tile is no longer read
-        if (PREFETCH) {
-#pragma unroll
-            for (int r = 0; r < kPrefetchRegs; ++r) {
-                const int i = threadIdx.x + r * blockDim.x;
-                if (i < nv16) reinterpret_cast<uint4 *>(Vi)[i] = rv[r];
-            }
-            if ((int)threadIdx.x < nc16) reinterpret_cast<uint4 *>(cl)[threadIdx.x] = rc;
-            if (e + (int)gridDim.x < geo.B) fetch(e + gridDim.x);  // in flight during the compute
+    for (int gidx = blockIdx.x; gidx < ngroups; gidx += gridDim.x) {
+        const int e0 = gidx * m;
+        const int me = min(m, geo.B - e0);
+        const long long vb = (long long)e0 * geo.S;
+        __syncthreads();  // the previous group's LDS tile is no longer read
+        copy16(cl, cells + (long long)e0 * geo.HWp, me * geo.HWp);
+        copy16(Vi, Vin + vb, me * vbytes);
+        __syncthreads();
+        for (int j = 0; j < me; ++j)
+            acc = vmax(acc, sweep_lds<T, MODEL, SLIP, MAP, !POLICY, POLICY || MAP == MGDP_MAP_SA>(
+                                geo, cf, cl + j * geo.HWp, Vi + j * geo.S, Vo + j * geo.S, pis + j * pib));
+        __syncthreads();
+        if (!POLICY) {
+            copy16(Vout + vb, Vo, me * vbytes);
         } else {
-            copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
-            copy16(Vi, Vin + vb, L.v_bytes);
+            for (int j = 0; j < me; ++j) copy_pi(pi + vb + (long long)j * geo.S, pis + j * pib, geo.S);
         }
-        __syncthreads();
-        acc = vmax(acc, sweep_lds<T, MODEL, SLIP, MAP, !POLICY, POLICY || MAP == MGDP_MAP_SA>(geo, cf, cl, Vi, Vo, pis));
-        __syncthreads();
-        if (!POLICY) copy16(Vout + vb, Vo, L.v_bytes);
-        else copy_pi(pi + vb, pis, geo.S);
     }
     if (!POLICY) {
         const T bdv = block_max(acc, slots, 0);
@@ -1122,8 +1109,8 @@ struct mgdp_vi {
     int nbuf = 2;                 // fused LDS V buffers (3 = two-sweep XYD step)
     int quad = 0;                 // fused XYD: 4 threads per cell
     bool nbuf3() const { return nbuf == 3; }
-    bool sweep_prefetch = false;  // measured: register prefetch loses to plain staging (vmcnt drains)
     int sweep_block = 256;
+    int sweep_m = 1;              // grids staged per workgroup iteration (measured: m>1 no faster)
 };
 
 namespace {
@@ -1212,14 +1199,16 @@ int launch_fused_t(mgdp_vi *vi, int k_target) {
     return 0;
 }
 
-template <typename T, int MODEL, bool SLIP, int MAP, bool POLICY, bool PREFETCH>
+template <typename T, int MODEL, bool SLIP, int MAP, bool POLICY>
 int launch_sweep_kernel(mgdp_vi *vi, const T *Vin, T *Vout, int k, int check_prev) {
-    const Smem L = smem_layout(vi->S, vi->HWp, sizeof(T));
-    auto kern = vi_sweep_kernel<T, MODEL, SLIP, MAP, POLICY, PREFETCH>;
-    if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
-    const int grid = std::min(vi->d.B, vi->sweep_grid);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(vi->sweep_block), L.total(), vi->stream, make_geo(vi), make_coef<T>(vi),
-                       vi->d_cells, Vin, Vout, vi->d_pi, POLICY ? nullptr : vi->d_shards, k, check_prev);
+    const int m = vi->sweep_m;
+    const int smem = sweep_smem_bytes(vi->S, vi->HWp, sizeof(T), m);
+    auto kern = vi_sweep_kernel<T, MODEL, SLIP, MAP, POLICY>;
+    if (smem > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
+    const int groups = (vi->d.B + m - 1) / m;
+    const int grid = std::min(groups, vi->sweep_grid);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(vi->sweep_block), smem, vi->stream, make_geo(vi), make_coef<T>(vi),
+                       vi->d_cells, Vin, Vout, vi->d_pi, POLICY ? nullptr : vi->d_shards, k, check_prev, m);
     MGDP_HIP(hipGetLastError());
     return 0;
 }
@@ -1228,12 +1217,9 @@ template <typename T, int MODEL, bool SLIP, int MAP>
 int launch_sweep_t(mgdp_vi *vi, int k, int check_prev, bool policy) {
     const T *Vin = (const T *)vi->d_V[(k - 1) & 1];
     T *Vout = (T *)vi->d_V[k & 1];
-    if (policy) return launch_sweep_kernel<T, MODEL, SLIP, MAP, true, false>(vi, Vin, Vout, k, 0);
+    if (policy) return launch_sweep_kernel<T, MODEL, SLIP, MAP, true>(vi, Vin, Vout, k, 0);
     if (int rc = timed_begin(vi, k)) return rc;
-    const bool pf = vi->sweep_prefetch && (int64_t)vi->S * sizeof(T) <= (int64_t)vi->sweep_block * kPrefetchRegs * 16;
-    const int rc = pf ? launch_sweep_kernel<T, MODEL, SLIP, MAP, false, true>(vi, Vin, Vout, k, check_prev)
-                      : launch_sweep_kernel<T, MODEL, SLIP, MAP, false, false>(vi, Vin, Vout, k, check_prev);
-    if (rc) return rc;
+    if (int rc = launch_sweep_kernel<T, MODEL, SLIP, MAP, false>(vi, Vin, Vout, k, check_prev)) return rc;
     return timed_end(vi);
 }
 
@@ -1447,7 +1433,9 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
         vi->own_stream = e == hipSuccess;
     }
     if (e == hipSuccess) e = hipMemset(vi->d_cells, 0, (size_t)d.B * vi->HWp);
-    if (const char *ev = std::getenv("MGDP_SWEEP_PREFETCH")) vi->sweep_prefetch = std::atoi(ev) != 0;
+    if (const char *ev = std::getenv("MGDP_SWEEP_M")) vi->sweep_m = std::max(1, std::atoi(ev));
+    // keep the staged group within the LDS budget (two groups per CU at least)
+    while (vi->sweep_m > 1 && sweep_smem_bytes(vi->S, vi->HWp, vi->tsize, vi->sweep_m) > 80 * 1024) --vi->sweep_m;
     if (const char *ev = std::getenv("MGDP_SWEEP_GRID")) vi->sweep_grid = std::max(1, std::atoi(ev));
     if (const char *ev = std::getenv("MGDP_SWEEP_BLOCK")) vi->sweep_block = std::min(256, std::max(64, std::atoi(ev) / 64 * 64));
     if (e == hipSuccess) {  // arm the fused reduction (every launch re-arms it for the next)
