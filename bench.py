@@ -98,14 +98,20 @@ def cpu_baseline(cells, model, gamma, tol, dtype, budget_s=8.0, nthreads=1):
                       f"({r['sweeps']} sweeps each, {dtype}), oracle/mgdp_oracle.c, {el:.1f} s"}
 
 
-def load_traffic(key):
+def load_traffic(key, solves_per_launch):
+    """HBM bytes per launch from the committed PMC passes (tools/pmc_traffic.sh).  A persistent
+    server launch serves many solves: its entry is per solve, scaled to this launch's solves."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
     with open(p) as f:
         d = json.load(f)
     v = d.get(key)
-    return None if v is None else v.get("bytes_per_launch")
+    if v is None:
+        return None
+    if "bytes_per_solve" in v:
+        return v["bytes_per_solve"] * solves_per_launch
+    return v.get("bytes_per_launch")
 
 
 def main():
@@ -199,12 +205,13 @@ def main():
     avg_launch_s = (kern_ms / 1000.0) / max(launches, 1)
     achieved = bytes_alg / max(launches, 1) / avg_launch_s / 1e9 if launches else 0.0
     comp_bytes = compulsory_bytes_per_sweep(vi.S, HW, tsize) * vi.B * (sum(sweeps))
-    kernel_name = "vi_fused_kernel" if args.method == "fused" else "vi_sweep_kernel"
+    persistent = vi.persistent
+    kernel_name = ("vi_serve_kernel" if persistent else "vi_fused_kernel") if args.method == "fused" else "vi_sweep_kernel"
     key = f"{args.workload}/{args.method}/{args.mapping}/{args.dtype}"
     roofline = {
         "bound": "hbm", "kernel": kernel_name,
         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-        "traffic": load_traffic(key),
+        "traffic": load_traffic(key, args.steps / max(launches, 1)),
         "launches": launches, "avg_launch_us": avg_launch_s * 1e6,
         "alg_bytes_per_launch": bytes_alg / max(launches, 1),
         "alg_bytes_per_update": bpu,
@@ -215,6 +222,10 @@ def main():
     if args.workload == "empty16":
         roofline["regime"] = ("single 8 KiB grid on one workgroup: latency/LDS bound, HBM-roofline fraction "
                               "is not meaningful here (SURVEY 8(d) caveats); see roofline_hbm")
+    if persistent:
+        roofline["launch_note"] = ("lone grid: one resident vi_serve_kernel launch serves every timed solve "
+                                   "(host posts a request word, the workgroup solves and publishes), so the "
+                                   "launch spans the timed region including host turnaround")
     out = {
         "metric": METRIC,
         "value": upd_total / elapsed_max,

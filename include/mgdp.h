@@ -101,8 +101,14 @@ int mgdp_vi_load_cells(mgdp_vi *vi, const uint8_t *cells);
 /* Same from device memory (already validated by the caller); async on the handle's stream. */
 int mgdp_vi_load_cells_device(mgdp_vi *vi, const uint8_t *d_cells);
 
-/* Whole solve on one device: V_0 = 0, sweeps until the global rule stops.  Synchronous. */
+/* Whole solve on one device: V_0 = 0, sweeps until the global rule stops.  Synchronous.
+ * A lone grid (B = 1, fused, MGDP_MAP_CELL) is served by a persistent workgroup that stays
+ * resident on the handle's stream between solves (no launch per solve); it leaves on any other
+ * call that uses the stream, after 100 us without a request, or after 2 s.  MGDP_PERSISTENT=0 in
+ * the environment (read at create) turns it off. */
 int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *converged_out);
+/* *on = 1 if mgdp_vi_solve on this handle goes through the persistent server. */
+int mgdp_vi_persistent(const mgdp_vi *vi, int32_t *on);
 
 /* Multi-device protocol (DESIGN.md "convergence across GPUs"): every rank calls
  *   mgdp_vi_reset -> mgdp_vi_run_local(&k_local) -> all-reduce(MAX) k -> mgdp_vi_run_to(k, &dv)

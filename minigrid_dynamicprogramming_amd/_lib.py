@@ -77,6 +77,7 @@ SIGNATURES = {
     "mgdp_vi_num_states": (ctypes.c_int, [ctypes.POINTER(ViDesc), _I64P]),
     "mgdp_vi_enable_timing": (ctypes.c_int, [_P, _I32]),
     "mgdp_vi_kernel_time": (ctypes.c_int, [_P, _DP, _I64P]),
+    "mgdp_vi_persistent": (ctypes.c_int, [_P, _I32P]),
     "mgdp_envs_create": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, ctypes.POINTER(_P)]),
     "mgdp_envs_destroy": (ctypes.c_int, [_P]),
     "mgdp_envs_set_stream": (ctypes.c_int, [_P, _P]),

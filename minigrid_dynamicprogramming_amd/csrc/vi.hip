@@ -25,7 +25,10 @@
 // Thread mappings (template MAP): MGDP_MAP_CELL = one thread per cell updating its 4 (XYD) or
 // 16 (DoorKey) states from 16-B LDS vectors; MGDP_MAP_SA = one thread per (state, action),
 // 8 lanes per state, wave shuffle max-reduce with the lowest action index winning ties.
+#include <hip/hip_ext.h>
+
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <climits>
@@ -887,15 +890,17 @@ __device__ __forceinline__ void fused_quad_xyd(const Geo &geo, const Coef<T> &cf
 // (|dV| >= tol) (ballot + one byte per wave, one barrier); after the loop the exact max |dV| is
 // reduced once and pi is extracted once from V_{k-1} (exactly what sweep k's argmax would give).
 // ------------------------------------------------------------------------------------------------
+// The whole fused solve of grid e by one workgroup: stage cells (and V unless fresh) in LDS, sweep
+// to the local stopping rule (k_target < 0) or to k_target, extract pi, write V / pi / (k, dV) back.
+// `lone`: this workgroup is the only one of the solve and publishes {k, dV} to the host as soon as
+// they are known (pi extraction and the write-back then overlap the host's reaction).
 template <typename T, int MODEL, bool SLIP, int MAP>
-__global__ void __launch_bounds__(1024)
-vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
-                int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
-                unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
-                unsigned long long *__restrict__ host_out, int k_target, int fresh, int in_kernel_reduce,
-                unsigned int epoch) {
+__device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, const uint8_t *__restrict__ cells,
+                                           T *__restrict__ V, int8_t *__restrict__ pi, int32_t *__restrict__ kenv,
+                                           double *__restrict__ dvenv, unsigned long long *__restrict__ host_out,
+                                           int k_target, int fresh, bool lone, unsigned int epoch, int e,
+                                           int &k, double &dvl) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int e = blockIdx.x;
     const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T), geo.nbuf);
     T *V0 = reinterpret_cast<T *>(smem);
     T *V1 = reinterpret_cast<T *>(smem + L.v_bytes);
@@ -905,72 +910,134 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
     T *slots = reinterpret_cast<T *>(smem + L.slots_off());
     uint8_t *flags = reinterpret_cast<uint8_t *>(smem + L.flags_off());
 
-    int k = fresh ? 0 : kenv[e];
-    double dvl = fresh ? 0.0 : dvenv[e];
+    k = fresh ? 0 : kenv[e];
+    dvl = fresh ? 0.0 : dvenv[e];
     const bool work = k_target < 0 ? (!(k > 0 && dvl < geo.tol) && k < geo.max_sweeps) : (k < k_target);
-    if (work) {
-        const long long vb = (long long)e * geo.S;
-        copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
-        if (k == 0) zero16(V0, L.v_bytes);
-        else copy16(V0, V + vb, L.v_bytes);
-        if (threadIdx.x < 64) flags[threadIdx.x] = 0;
-        __syncthreads();
+    if (!work) return false;
+    const long long vb = (long long)e * geo.S;
+    copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
+    if (k == 0) zero16(V0, L.v_bytes);
+    else copy16(V0, V + vb, L.v_bytes);
+    if (threadIdx.x < 64) flags[threadIdx.x] = 0;
+    __syncthreads();
 
-        const bool fast = MAP == MGDP_MAP_CELL && geo.HW <= (int)blockDim.x;
-        int cur = 0, parity = 0;
-        T diff = (T)0;
-        // A lone grid publishes {k, dV} to the host as soon as they are known; pi extraction and
-        // the V/pi write-back then overlap the host's next launch (they stay stream-ordered).
-        const bool lone = in_kernel_reduce && gridDim.x == 1;
-        auto done = [&](int kk, double dv) {
-            if (lone && threadIdx.x == 0)
-                publish(host_out, (unsigned long long)kk, (unsigned long long)__double_as_longlong(dv),
-                        (unsigned long long)kk, epoch);
-        };
-        const T *Vfinal = nullptr;
-        if (fast && MODEL == MGDP_MODEL_XYD && geo.nbuf == 3) {
-            T *const bufs[3] = {V0, V1, V2};
-            int vf = 0;
-            if (k_target < 0) fused_fast_xyd2<T, SLIP, true>(geo, cf, cl, bufs, pis, slots, flags, k, k_target, vf, dvl, done);
-            else fused_fast_xyd2<T, SLIP, false>(geo, cf, cl, bufs, pis, slots, flags, k, k_target, vf, dvl, done);
-            Vfinal = bufs[vf];
-        } else if (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL && geo.quad && 4 * geo.HW <= (int)blockDim.x) {
-            if (k_target < 0) fused_quad_xyd<T, SLIP, true>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
-            else fused_quad_xyd<T, SLIP, false>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
-        } else if (fast) {
-            if (k_target < 0) fused_fast<T, MODEL, SLIP, true>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
-            else fused_fast<T, MODEL, SLIP, false>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
-        } else {
-            while (true) {
-                const T *Vin = cur ? V1 : V0;
-                T *Vout = cur ? V0 : V1;
-                diff = sweep_lds<T, MODEL, SLIP, MAP, true, MAP == MGDP_MAP_SA>(geo, cf, cl, Vin, Vout, pis);
-                cur ^= 1;
-                ++k;
-                if (k_target < 0) {
-                    const bool more = block_any((double)diff >= geo.tol, flags, parity);
-                    parity ^= 1;
-                    if (!more || k >= geo.max_sweeps) break;
-                } else {
-                    __syncthreads();
-                    if (k >= k_target) break;
-                }
-            }
-            dvl = (double)block_max(diff, slots, 0);
-            done(k, dvl);
-            if (MAP == MGDP_MAP_CELL) {  // pi of the last sweep = argmax on V_{k-1}
-                sweep_lds<T, MODEL, SLIP, MAP, false, true>(geo, cf, cl, cur ? V0 : V1, nullptr, pis);
+    const bool fast = MAP == MGDP_MAP_CELL && geo.HW <= (int)blockDim.x;
+    int cur = 0, parity = 0;
+    T diff = (T)0;
+    auto done = [&](int kk, double dv) {
+        if (lone && threadIdx.x == 0)
+            publish(host_out, (unsigned long long)kk, (unsigned long long)__double_as_longlong(dv),
+                    (unsigned long long)kk, epoch);
+    };
+    const T *Vfinal = nullptr;
+    if (fast && MODEL == MGDP_MODEL_XYD && geo.nbuf == 3) {
+        T *const bufs[3] = {V0, V1, V2};
+        int vf = 0;
+        if (k_target < 0) fused_fast_xyd2<T, SLIP, true>(geo, cf, cl, bufs, pis, slots, flags, k, k_target, vf, dvl, done);
+        else fused_fast_xyd2<T, SLIP, false>(geo, cf, cl, bufs, pis, slots, flags, k, k_target, vf, dvl, done);
+        Vfinal = bufs[vf];
+    } else if (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL && geo.quad && 4 * geo.HW <= (int)blockDim.x) {
+        if (k_target < 0) fused_quad_xyd<T, SLIP, true>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
+        else fused_quad_xyd<T, SLIP, false>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
+    } else if (fast) {
+        if (k_target < 0) fused_fast<T, MODEL, SLIP, true>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
+        else fused_fast<T, MODEL, SLIP, false>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
+    } else {
+        while (true) {
+            const T *Vin = cur ? V1 : V0;
+            T *Vout = cur ? V0 : V1;
+            diff = sweep_lds<T, MODEL, SLIP, MAP, true, MAP == MGDP_MAP_SA>(geo, cf, cl, Vin, Vout, pis);
+            cur ^= 1;
+            ++k;
+            if (k_target < 0) {
+                const bool more = block_any((double)diff >= geo.tol, flags, parity);
+                parity ^= 1;
+                if (!more || k >= geo.max_sweeps) break;
+            } else {
                 __syncthreads();
+                if (k >= k_target) break;
             }
         }
-        copy16(V + vb, Vfinal ? Vfinal : (cur ? V1 : V0), L.v_bytes);
-        copy_pi(pi + vb, pis, geo.S);
-        if (threadIdx.x == 0) {
-            kenv[e] = k;
-            dvenv[e] = dvl;
+        dvl = (double)block_max(diff, slots, 0);
+        done(k, dvl);
+        if (MAP == MGDP_MAP_CELL) {  // pi of the last sweep = argmax on V_{k-1}
+            sweep_lds<T, MODEL, SLIP, MAP, false, true>(geo, cf, cl, cur ? V0 : V1, nullptr, pis);
+            __syncthreads();
         }
     }
+    copy16(V + vb, Vfinal ? Vfinal : (cur ? V1 : V0), L.v_bytes);
+    copy_pi(pi + vb, pis, geo.S);
+    if (threadIdx.x == 0) {
+        kenv[e] = k;
+        dvenv[e] = dvl;
+    }
+    return true;
+}
+
+template <typename T, int MODEL, bool SLIP, int MAP>
+__global__ void __launch_bounds__(1024)
+vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
+                int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
+                unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
+                unsigned long long *__restrict__ host_out, int k_target, int fresh, int in_kernel_reduce,
+                unsigned int epoch) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T), geo.nbuf);
+    T *slots = reinterpret_cast<T *>(smem + L.slots_off());
+    int k;
+    double dvl;
+    const bool lone = in_kernel_reduce && gridDim.x == 1;
+    const bool work = fused_grid<T, MODEL, SLIP, MAP>(geo, cf, cells, V, pi, kenv, dvenv, host_out, k_target, fresh,
+                                                      lone, epoch, blockIdx.x, k, dvl);
     if (in_kernel_reduce) fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16), epoch, work);
+}
+
+// Persistent solver for a lone grid: one workgroup stays resident and serves solve requests posted
+// in host-mapped memory, removing the launch and dispatch latency from every solve.  Lane 0 polls
+// the request word (relaxed system-scope loads + s_sleep); request r (r != served) runs a fresh
+// fused solve whose {k, dV} is published with epoch r.  Every wave leaves the loop on the quit
+// word, after `idle_ticks` without a request or after `life_ticks` in total (s_memrealtime,
+// 100 MHz); the host relaunches the server if a request finds it gone.
+constexpr unsigned long long kServeQuit = ~0ull;
+
+template <typename T, int MODEL, bool SLIP, int MAP>
+__global__ void __launch_bounds__(1024)
+vi_serve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
+                int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
+                unsigned long long *__restrict__ host_out, const unsigned long long *__restrict__ host_cmd,
+                unsigned long long served, unsigned long long idle_ticks, unsigned long long life_ticks) {
+    __shared__ unsigned long long s_cmd;
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t_last = t_start;
+    while (true) {
+        if (threadIdx.x == 0) {
+            unsigned long long cmd;
+            while (true) {
+                cmd = __hip_atomic_load(host_cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (cmd != served) break;
+                const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+                if (now - t_last > idle_ticks || now - t_start > life_ticks) {
+                    cmd = kServeQuit;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            s_cmd = cmd;
+        }
+        __syncthreads();
+        const unsigned long long cmd = s_cmd;
+        if (cmd == kServeQuit) break;
+        int k;
+        double dvl;
+        if (!fused_grid<T, MODEL, SLIP, MAP>(geo, cf, cells, V, pi, kenv, dvenv, host_out, -1, 1, true,
+                                             (unsigned int)cmd, 0, k, dvl) &&
+            threadIdx.x == 0)
+            publish(host_out, (unsigned long long)k, (unsigned long long)__double_as_longlong(dvl),
+                    (unsigned long long)k, (unsigned int)cmd);
+        served = cmd;
+        t_last = __builtin_amdgcn_s_memrealtime();
+        __syncthreads();  // s_cmd and the LDS tiles are reused by the next request
+    }
 }
 
 // Large batches: one workgroup reduces the per-grid (kenv, dvenv) into host-mapped memory (a
@@ -1086,7 +1153,7 @@ struct mgdp_vi {
     unsigned long long *d_shards = nullptr;
     unsigned long long *d_red = nullptr;    // fused reduction shards [64][4]
     unsigned int *d_ticket = nullptr;       // arrival ticket of the fused reduction
-    unsigned long long *h_out = nullptr;    // host-mapped {kmax, dV bits, kmin}
+    unsigned long long *h_out = nullptr;    // host-mapped {kmax, dV bits, kmin, epoch, request}
     unsigned long long *d_hout = nullptr;   // device alias of h_out
     int cur = 0;        // V buffer holding the current V (sweep method)
     int k_min = 0;      // min / max sweeps over grids after the last reduce (fused method)
@@ -1098,7 +1165,7 @@ struct mgdp_vi {
     bool cells_loaded = false;
     // timing of the dominant kernel
     bool timing = false;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev, ev_pool;
     std::vector<int> ev_sweep;  // sweep index of each timed sweep launch (-1 = fused launch)
     double total_ms = 0.0;
     int64_t launches = 0;
@@ -1111,6 +1178,14 @@ struct mgdp_vi {
     bool nbuf3() const { return nbuf == 3; }
     int sweep_block = 256;
     int sweep_m = 1;              // grids staged per workgroup iteration (measured: m>1 no faster)
+    // persistent solver (lone grid, fused one-thread-per-cell path): see vi_serve_kernel
+    bool persistent = true;       // MGDP_PERSISTENT=0 disables it
+    bool serving = false;         // a vi_serve_kernel launch may be resident on `stream`
+    // The server leaves after serve_idle_ticks without a request, which also bounds how long a
+    // device-wide synchronisation by another component can wait on it.
+    unsigned long long serve_idle_ticks = 10000;     // 100 us at 100 MHz
+    unsigned long long serve_life_ticks = 200000000; // 2 s
+    std::chrono::steady_clock::time_point serve_last{};  // host time of the last served result
 };
 
 namespace {
@@ -1144,19 +1219,25 @@ Coef<T> make_coef(const mgdp_vi *vi) {
     return c;
 }
 
-int timed_begin(mgdp_vi *vi, int sweep_idx) {
+// Timed launches go through hipExtLaunchKernelGGL with a start/stop event pair, so the events carry
+// the dispatch's own begin/end timestamps (what rocprofv3's kernel trace reports) rather than the
+// times of separate marker packets.  Event pairs are pooled: no hipEventCreate in the timed loop.
+struct TimedPair { hipEvent_t a = nullptr, b = nullptr; };
+int timed_begin(mgdp_vi *vi, int sweep_idx, TimedPair *tp) {
+    tp->a = tp->b = nullptr;
     if (!vi->timing) return 0;
-    hipEvent_t a, b;
-    MGDP_HIP(hipEventCreate(&a));
-    MGDP_HIP(hipEventCreate(&b));
-    MGDP_HIP(hipEventRecord(a, vi->stream));
-    vi->ev.push_back({a, b});
+    std::pair<hipEvent_t, hipEvent_t> e;
+    if (!vi->ev_pool.empty()) {
+        e = vi->ev_pool.back();
+        vi->ev_pool.pop_back();
+    } else {
+        MGDP_HIP(hipEventCreate(&e.first));
+        MGDP_HIP(hipEventCreate(&e.second));
+    }
+    vi->ev.push_back(e);
     vi->ev_sweep.push_back(sweep_idx);
-    return 0;
-}
-int timed_end(mgdp_vi *vi) {
-    if (!vi->timing) return 0;
-    MGDP_HIP(hipEventRecord(vi->ev.back().second, vi->stream));
+    tp->a = e.first;
+    tp->b = e.second;
     return 0;
 }
 // Fold completed events into total_ms (called after a stream sync).  Sweep launches past the
@@ -1169,8 +1250,7 @@ int timed_collect(mgdp_vi *vi) {
             vi->total_ms += ms;
             vi->launches += 1;
         }
-        (void)hipEventDestroy(vi->ev[i].first);
-        (void)hipEventDestroy(vi->ev[i].second);
+        vi->ev_pool.push_back(vi->ev[i]);
     }
     vi->ev.clear();
     vi->ev_sweep.clear();
@@ -1183,14 +1263,14 @@ int launch_fused_t(mgdp_vi *vi, int k_target) {
     const Smem L = smem_layout(vi->S, vi->HWp, sizeof(T), vi->nbuf);
     auto kern = vi_fused_kernel<T, MODEL, SLIP, MAP>;
     if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
-    if (int rc = timed_begin(vi, -1)) return rc;
-    hipLaunchKernelGGL(kern, dim3(vi->d.B), dim3(vi->fused_block), L.total(), vi->stream, g,
+    TimedPair tp;
+    if (int rc = timed_begin(vi, -1, &tp)) return rc;
+    hipExtLaunchKernelGGL(kern, dim3(vi->d.B), dim3(vi->fused_block), L.total(), vi->stream, tp.a, tp.b, 0, g,
                        make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv,
                        vi->d_dvenv, vi->d_red, vi->d_ticket, vi->d_hout, k_target, vi->fresh,
                        vi->d.B <= kInKernelReduceMaxB ? 1 : 0, ++vi->epoch);
     MGDP_HIP(hipGetLastError());
     vi->fresh = 0;
-    if (int rc = timed_end(vi)) return rc;
     if (vi->d.B > kInKernelReduceMaxB) {
         hipLaunchKernelGGL(vi_reduce_kernel, dim3(1), dim3(1024), 0, vi->stream, vi->d_kenv, vi->d_dvenv, vi->d.B,
                            vi->d_hout, vi->epoch);
@@ -1199,15 +1279,31 @@ int launch_fused_t(mgdp_vi *vi, int k_target) {
     return 0;
 }
 
+template <typename T, int MODEL, bool SLIP, int MAP>
+int launch_serve_t(mgdp_vi *vi, unsigned int served) {
+    const Geo g = make_geo(vi);
+    const Smem L = smem_layout(vi->S, vi->HWp, sizeof(T), vi->nbuf);
+    auto kern = vi_serve_kernel<T, MODEL, SLIP, MAP>;
+    if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
+    TimedPair tp;
+    if (int rc = timed_begin(vi, -1, &tp)) return rc;
+    hipExtLaunchKernelGGL(kern, dim3(1), dim3(vi->fused_block), L.total(), vi->stream, tp.a, tp.b, 0, g,
+                          make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv, vi->d_dvenv,
+                          vi->d_hout, vi->d_hout + 4, (unsigned long long)served, vi->serve_idle_ticks,
+                          vi->serve_life_ticks);
+    MGDP_HIP(hipGetLastError());
+    return 0;
+}
+
 template <typename T, int MODEL, bool SLIP, int MAP, bool POLICY>
-int launch_sweep_kernel(mgdp_vi *vi, const T *Vin, T *Vout, int k, int check_prev) {
+int launch_sweep_kernel(mgdp_vi *vi, const T *Vin, T *Vout, int k, int check_prev, TimedPair tp = {}) {
     const int m = vi->sweep_m;
     const int smem = sweep_smem_bytes(vi->S, vi->HWp, sizeof(T), m);
     auto kern = vi_sweep_kernel<T, MODEL, SLIP, MAP, POLICY>;
     if (smem > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
     const int groups = (vi->d.B + m - 1) / m;
     const int grid = std::min(groups, vi->sweep_grid);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(vi->sweep_block), smem, vi->stream, make_geo(vi), make_coef<T>(vi),
+    hipExtLaunchKernelGGL(kern, dim3(grid), dim3(vi->sweep_block), smem, vi->stream, tp.a, tp.b, 0, make_geo(vi), make_coef<T>(vi),
                        vi->d_cells, Vin, Vout, vi->d_pi, POLICY ? nullptr : vi->d_shards, k, check_prev, m);
     MGDP_HIP(hipGetLastError());
     return 0;
@@ -1218,9 +1314,9 @@ int launch_sweep_t(mgdp_vi *vi, int k, int check_prev, bool policy) {
     const T *Vin = (const T *)vi->d_V[(k - 1) & 1];
     T *Vout = (T *)vi->d_V[k & 1];
     if (policy) return launch_sweep_kernel<T, MODEL, SLIP, MAP, true>(vi, Vin, Vout, k, 0);
-    if (int rc = timed_begin(vi, k)) return rc;
-    if (int rc = launch_sweep_kernel<T, MODEL, SLIP, MAP, false>(vi, Vin, Vout, k, check_prev)) return rc;
-    return timed_end(vi);
+    TimedPair tp;
+    if (int rc = timed_begin(vi, k, &tp)) return rc;
+    return launch_sweep_kernel<T, MODEL, SLIP, MAP, false>(vi, Vin, Vout, k, check_prev, tp);
 }
 
 // Dispatch on (dtype, model, slip, mapping).
@@ -1247,6 +1343,10 @@ struct FusedF {
     static int run(mgdp_vi *vi, int k_target) { return launch_fused_t<T, MODEL, SLIP, MAP>(vi, k_target); }
 };
 template <typename T, int MODEL, bool SLIP, int MAP>
+struct ServeF {
+    static int run(mgdp_vi *vi, unsigned int served) { return launch_serve_t<T, MODEL, SLIP, MAP>(vi, served); }
+};
+template <typename T, int MODEL, bool SLIP, int MAP>
 struct SweepF {
     static int run(mgdp_vi *vi, int k, int check_prev, bool policy) {
         return launch_sweep_t<T, MODEL, SLIP, MAP>(vi, k, check_prev, policy);
@@ -1255,15 +1355,23 @@ struct SweepF {
 
 // Read the reduction the last fused launch published to host-mapped memory: max k, max dV, min k.
 int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
-    // The last workgroup (or the reduce kernel) publishes {kmax, dV, kmin, epoch} to host-mapped
-    // memory; poll the epoch instead of a stream synchronisation (lower completion latency).
-    // Everything else stays stream-ordered.  Poll the stream now and then to surface faults.
+    // The last workgroup (or the reduce kernel, or the persistent server) publishes {kmax, dV,
+    // kmin, epoch} to host-mapped memory; poll the epoch instead of a stream synchronisation
+    // (lower completion latency).  Everything else stays stream-ordered.  Poll the stream now and
+    // then to surface faults -- and, in serving mode, to relaunch a server that idled out before
+    // it saw the request.
     const volatile unsigned long long *h = vi->h_out;
+    int relaunches = 0;
     for (uint64_t spin = 0; h[3] != (unsigned long long)vi->epoch; ++spin) {
         if ((spin & 1023) == 1023) {
             const hipError_t q = hipStreamQuery(vi->stream);
             if (q == hipSuccess) {
                 if (h[3] == (unsigned long long)vi->epoch) break;
+                if (vi->serving && relaunches < 4) {
+                    ++relaunches;
+                    if (int rc = dispatch<ServeF>(vi, vi->epoch - 1u)) return rc;
+                    continue;
+                }
                 MGDP_CHECK(false, MGDP_E_HIP, "fused launch finished without publishing its result (epoch %u)", vi->epoch);
             }
             if (q != hipErrorNotReady) return hip_fail(q, "fused value-iteration launch", __FILE__, __LINE__);
@@ -1277,6 +1385,40 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
     vi->k_done_valid = true;
     if (kmax) *kmax = (int32_t)km;
     if (dvmax) *dvmax = vi->dv_red;
+    return 0;
+}
+
+// Persistent solver hand-off (lone grid on the one-thread-per-cell fused path).
+bool serve_eligible(const mgdp_vi *vi) {
+    return vi->persistent && vi->d.method == MGDP_METHOD_FUSED && vi->d.B == 1 && vi->d.mapping == MGDP_MAP_CELL &&
+           vi->HW <= vi->fused_block && vi->nbuf == 2 && !vi->quad;
+}
+// Ask a resident server to leave and drain the stream.  Every entry point that enqueues other
+// work on the stream, or reads results, calls this first.
+int server_stop(mgdp_vi *vi) {
+    if (!vi->serving) return 0;
+    __atomic_store_n(vi->h_out + 4, kServeQuit, __ATOMIC_RELEASE);
+    vi->serving = false;
+    MGDP_HIP(hipStreamSynchronize(vi->stream));
+    return 0;
+}
+// Post request `epoch` (the server serves any request word != the last epoch it served) and make
+// sure a server is resident; reduce_env then waits for the published result.
+int serve_request(mgdp_vi *vi) {
+    // A server idle for more than half its limit may be leaving: restart it deterministically
+    // (quit + drain, then a fresh launch) instead of discovering its exit while polling.
+    if (vi->serving) {
+        const double idle_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - vi->serve_last).count();
+        if (idle_us * 100.0 > 0.5 * (double)vi->serve_idle_ticks)
+            if (int rc = server_stop(vi)) return rc;
+    }
+    ++vi->epoch;
+    __atomic_store_n(vi->h_out + 4, (unsigned long long)vi->epoch, __ATOMIC_RELEASE);
+    if (!vi->serving) {
+        if (int rc = dispatch<ServeF>(vi, vi->epoch - 1u)) return rc;
+        vi->serving = true;
+    }
+    vi->fresh = 0;
     return 0;
 }
 
@@ -1425,7 +1567,7 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     al((void **)&vi->d_dvenv, sizeof(double) * d.B);
     al((void **)&vi->d_shards, sizeof(unsigned long long) * 8 * (size_t)(d.max_sweeps + 1));
     al((void **)&vi->d_red, sizeof(unsigned long long) * (kRedShards * 4 + 2));
-    if (e == hipSuccess) e = hipHostMalloc((void **)&vi->h_out, 4 * sizeof(unsigned long long),
+    if (e == hipSuccess) e = hipHostMalloc((void **)&vi->h_out, 8 * sizeof(unsigned long long),
                                            hipHostMallocMapped | hipHostMallocCoherent);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&vi->d_hout, vi->h_out, 0);
     if (e == hipSuccess) {
@@ -1438,6 +1580,12 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     while (vi->sweep_m > 1 && sweep_smem_bytes(vi->S, vi->HWp, vi->tsize, vi->sweep_m) > 80 * 1024) --vi->sweep_m;
     if (const char *ev = std::getenv("MGDP_SWEEP_GRID")) vi->sweep_grid = std::max(1, std::atoi(ev));
     if (const char *ev = std::getenv("MGDP_SWEEP_BLOCK")) vi->sweep_block = std::min(256, std::max(64, std::atoi(ev) / 64 * 64));
+    if (const char *ev = std::getenv("MGDP_PERSISTENT")) vi->persistent = std::atoi(ev) != 0;
+    if (const char *ev = std::getenv("MGDP_SERVE_IDLE_US"))  // s_memrealtime ticks at 100 MHz
+        vi->serve_idle_ticks = (unsigned long long)std::max(1LL, std::atoll(ev)) * 100ull;
+    if (const char *ev = std::getenv("MGDP_SERVE_LIFE_US"))
+        vi->serve_life_ticks = (unsigned long long)std::max(1LL, std::atoll(ev)) * 100ull;
+    if (vi->h_out) std::memset(vi->h_out, 0, 8 * sizeof(unsigned long long));
     if (e == hipSuccess) {  // arm the fused reduction (every launch re-arms it for the next)
         std::vector<unsigned long long> init((size_t)kRedShards * 4 + 2, 0ull);
         for (size_t i = 2; i < (size_t)kRedShards * 4; i += 4) init[i] = 0x7fffffffull;
@@ -1455,8 +1603,10 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
 int mgdp_vi_destroy(mgdp_vi *vi) {
     if (!vi) return 0;
     DeviceGuard guard(vi->d.device);
+    (void)server_stop(vi);
     if (vi->stream) (void)hipStreamSynchronize(vi->stream);
     for (auto &p : vi->ev) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
+    for (auto &p : vi->ev_pool) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
     (void)hipFree(vi->d_cells);
     (void)hipFree(vi->d_V[0]);
     (void)hipFree(vi->d_V[1]);
@@ -1474,6 +1624,7 @@ int mgdp_vi_destroy(mgdp_vi *vi) {
 int mgdp_vi_set_stream(mgdp_vi *vi, void *s) {
     MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
     DeviceGuard guard(vi->d.device);
+    if (int rc = server_stop(vi)) return rc;
     MGDP_HIP(hipStreamSynchronize(vi->stream));
     if (vi->own_stream) { (void)hipStreamDestroy(vi->stream); vi->own_stream = false; vi->stream = nullptr; }
     if (s) {
@@ -1489,6 +1640,7 @@ int mgdp_vi_load_cells(mgdp_vi *vi, const uint8_t *cells) {
     MGDP_CHECK(vi && cells, MGDP_E_INVALID, "null argument");
     if (int rc = validate_cells(vi->d, cells)) return rc;
     DeviceGuard guard(vi->d.device);
+    if (int rc = server_stop(vi)) return rc;
     std::vector<uint8_t> pad((size_t)vi->d.B * vi->HWp, 0);
     for (int b = 0; b < vi->d.B; ++b) std::memcpy(&pad[(size_t)b * vi->HWp], cells + (size_t)b * vi->HW, vi->HW);
     MGDP_HIP(hipMemcpyAsync(vi->d_cells, pad.data(), pad.size(), hipMemcpyHostToDevice, vi->stream));
@@ -1501,6 +1653,7 @@ int mgdp_vi_load_cells(mgdp_vi *vi, const uint8_t *cells) {
 int mgdp_vi_load_cells_device(mgdp_vi *vi, const uint8_t *d_cells) {
     MGDP_CHECK(vi && d_cells, MGDP_E_INVALID, "null argument");
     DeviceGuard guard(vi->d.device);
+    if (int rc = server_stop(vi)) return rc;
     MGDP_HIP(hipMemcpy2DAsync(vi->d_cells, vi->HWp, d_cells, vi->HW, vi->HW, vi->d.B, hipMemcpyDeviceToDevice, vi->stream));
     vi->cells_loaded = true;
     vi->k_done_valid = false;
@@ -1530,9 +1683,16 @@ int mgdp_vi_run_local(mgdp_vi *vi, int32_t *k_local_max) {
     MGDP_CHECK(vi->cells_loaded, MGDP_E_INVALID, "no cells loaded");
     DeviceGuard guard(vi->d.device);
     if (vi->d.method == MGDP_METHOD_FUSED) {
-        if (int rc = dispatch<FusedF>(vi, -1)) return rc;
+        const bool serve = serve_eligible(vi) && vi->fresh;
+        if (serve) {
+            if (int rc = serve_request(vi)) return rc;
+        } else {
+            if (int rc = server_stop(vi)) return rc;
+            if (int rc = dispatch<FusedF>(vi, -1)) return rc;
+        }
         int32_t km;
         if (int rc = reduce_env(vi, &km, nullptr)) return rc;
+        if (serve) vi->serve_last = std::chrono::steady_clock::now();
         *k_local_max = km;
         return 0;
     }
@@ -1551,6 +1711,7 @@ int mgdp_vi_run_to(mgdp_vi *vi, int32_t k_target, double *dv_out) {
             *dv_out = vi->dv_red;
             return 0;
         }
+        if (int rc = server_stop(vi)) return rc;
         if (int rc = dispatch<FusedF>(vi, k_target)) return rc;
         int32_t km;
         if (int rc = reduce_env(vi, &km, dv_out)) return rc;
@@ -1614,9 +1775,16 @@ int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *con
     return 0;
 }
 
+int mgdp_vi_persistent(const mgdp_vi *vi, int32_t *on) {
+    MGDP_CHECK(vi && on, MGDP_E_INVALID, "null argument");
+    *on = serve_eligible(vi) ? 1 : 0;
+    return 0;
+}
+
 int mgdp_vi_get_values(mgdp_vi *vi, void *V) {
     MGDP_CHECK(vi && V, MGDP_E_INVALID, "null argument");
     DeviceGuard guard(vi->d.device);
+    if (int rc = server_stop(vi)) return rc;
     const void *src = vi->d.method == MGDP_METHOD_SWEEP ? vi->d_V[vi->cur] : vi->d_V[0];
     MGDP_HIP(hipMemcpyAsync(V, src, (size_t)vi->d.B * vi->S * vi->tsize, hipMemcpyDeviceToHost, vi->stream));
     MGDP_HIP(hipStreamSynchronize(vi->stream));
@@ -1626,6 +1794,7 @@ int mgdp_vi_get_values(mgdp_vi *vi, void *V) {
 int mgdp_vi_get_policy(mgdp_vi *vi, int8_t *pi) {
     MGDP_CHECK(vi && pi, MGDP_E_INVALID, "null argument");
     DeviceGuard guard(vi->d.device);
+    if (int rc = server_stop(vi)) return rc;
     MGDP_HIP(hipMemcpyAsync(pi, vi->d_pi, (size_t)vi->d.B * vi->S, hipMemcpyDeviceToHost, vi->stream));
     MGDP_HIP(hipStreamSynchronize(vi->stream));
     return 0;
@@ -1634,6 +1803,7 @@ int mgdp_vi_get_policy(mgdp_vi *vi, int8_t *pi) {
 int mgdp_vi_get_dv_trace(mgdp_vi *vi, double *trace, int32_t n) {
     MGDP_CHECK(vi && trace && n >= 0 && n <= vi->d.max_sweeps, MGDP_E_INVALID, "bad argument");
     DeviceGuard guard(vi->d.device);
+    if (int rc = server_stop(vi)) return rc;
     std::vector<unsigned long long> sh((size_t)8 * n);
     if (n) MGDP_HIP(hipMemcpy(sh.data(), vi->d_shards, sh.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     for (int i = 0; i < n; ++i) trace[i] = shard_max(&sh[8 * (size_t)i]);
@@ -1642,6 +1812,8 @@ int mgdp_vi_get_dv_trace(mgdp_vi *vi, double *trace, int32_t n) {
 
 int mgdp_vi_device_buffers(mgdp_vi *vi, void **d_V, void **d_pi) {
     MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
+    DeviceGuard guard(vi->d.device);
+    if (int rc = server_stop(vi)) return rc;
     if (d_V) *d_V = vi->d.method == MGDP_METHOD_SWEEP ? vi->d_V[vi->cur] : vi->d_V[0];
     if (d_pi) *d_pi = vi->d_pi;
     return 0;
@@ -1649,6 +1821,10 @@ int mgdp_vi_device_buffers(mgdp_vi *vi, void **d_V, void **d_pi) {
 
 int mgdp_vi_enable_timing(mgdp_vi *vi, int32_t on) {
     MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
+    DeviceGuard guard(vi->d.device);
+    if (int rc = server_stop(vi)) return rc;
+    MGDP_HIP(hipStreamSynchronize(vi->stream));
+    if (int rc = timed_collect(vi)) return rc;  // drop launches timed before this call
     vi->timing = on != 0;
     vi->total_ms = 0.0;
     vi->launches = 0;
@@ -1658,6 +1834,7 @@ int mgdp_vi_enable_timing(mgdp_vi *vi, int32_t on) {
 int mgdp_vi_kernel_time(mgdp_vi *vi, double *total_ms, int64_t *launches) {
     MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
     DeviceGuard guard(vi->d.device);
+    if (int rc = server_stop(vi)) return rc;
     MGDP_HIP(hipStreamSynchronize(vi->stream));
     if (int rc = timed_collect(vi)) return rc;
     if (total_ms) *total_ms = vi->total_ms;

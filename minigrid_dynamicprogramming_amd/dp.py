@@ -11,7 +11,9 @@ All arithmetic runs in libmgdp.so on the GPU; results are bit-identical to the C
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -110,6 +112,20 @@ class VIResult:
         return DOORKEY_ACTIONS[lane] if self.model == "doorkey" else lane
 
 
+# Handles still open at interpreter exit are destroyed explicitly: a lone-grid handle may keep a
+# persistent solver resident on its stream, and destroy() asks it to leave and drains the stream.
+_LIVE: "weakref.WeakSet[ValueIteration]" = weakref.WeakSet()
+
+
+@atexit.register
+def _close_live_handles():
+    for vi in list(_LIVE):
+        try:
+            vi.close()
+        except Exception:
+            pass
+
+
 class ValueIteration:
     """A batch of B grids resident on one GPU (an mgdp_vi handle); solve() may be called repeatedly.
 
@@ -152,10 +168,27 @@ class ValueIteration:
         h = ctypes.c_void_p()
         _lib.check(self.L.mgdp_vi_create(ctypes.byref(d), ctypes.byref(h)), "mgdp_vi_create")
         self.h = h
+        _LIVE.add(self)
         if stream is not None:
             _lib.check(self.L.mgdp_vi_set_stream(h, ctypes.c_void_p(int(stream))), "mgdp_vi_set_stream")
+        self.load(cells)
+
+    @property
+    def persistent(self) -> bool:
+        """Whether solve() is served by the resident vi_serve_kernel (lone grid, fused, cell)."""
+        on = ctypes.c_int32(0)
+        _lib.check(self.L.mgdp_vi_persistent(self.h, ctypes.byref(on)), "mgdp_vi_persistent")
+        return bool(on.value)
+
+    def load(self, grids):
+        """Install new grids of the same shape (mgdp_vi_load_cells); the next solve uses them."""
+        cells, enc = to_cells(grids)
+        if cells.shape != (self.B, self.H, self.W):
+            raise ValueError(f"grids of shape {cells.shape} do not match the handle's {(self.B, self.H, self.W)}")
+        if self.model == "doorkey" and enc is not None:
+            check_doorkey_encoding(enc)
         cells = np.ascontiguousarray(cells, np.uint8)
-        _lib.check(self.L.mgdp_vi_load_cells(h, _lib.ptr(cells)), "mgdp_vi_load_cells")
+        _lib.check(self.L.mgdp_vi_load_cells(self.h, _lib.ptr(cells)), "mgdp_vi_load_cells")
         self.sweeps = 0
         self.converged = False
         self.dv = float("nan")

@@ -185,3 +185,89 @@ def test_fused_xyd_variants_bit_exact(pair, quad, slip, dtype, monkeypatch):
         assert r.sweeps == o["sweeps"] == ms
         np.testing.assert_array_equal(r.V, o["V"])
         np.testing.assert_array_equal(r.pi, o["pi"])
+
+
+def _solve_one(cells, dtype="f32", **kw):
+    vi = mg.ValueIteration(cells, dtype=dtype, **kw)
+    vi.solve()
+    out = (vi.sweeps, vi.values(), vi.policy())
+    vi.close()
+    return out
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_persistent_server_matches_launches(dtype, monkeypatch):
+    """A lone grid is solved by the resident vi_serve_kernel; it agrees bit for bit with one fused
+    launch per solve (MGDP_PERSISTENT=0) and with the oracle."""
+    for name in ("empty16_s0", "fourrooms_s1", "lava11n5_s0", "doorkey8_s2", "doorkey16_s0"):
+        t = load(f"table_{name}.npz")
+        cells = cells_from_enc(t["enc"])[None]
+        monkeypatch.setenv("MGDP_PERSISTENT", "1")
+        k1, V1, p1 = _solve_one(cells, dtype)
+        monkeypatch.setenv("MGDP_PERSISTENT", "0")
+        k0, V0, p0 = _solve_one(cells, dtype)
+        o = oracle.value_iteration(int(t["model"]), cells, dtype=dtype)
+        assert k1 == k0 == o["sweeps"]
+        np.testing.assert_array_equal(V1, V0)
+        np.testing.assert_array_equal(p1, p0)
+        np.testing.assert_array_equal(V1, o["V"])
+        np.testing.assert_array_equal(p1, o["pi"])
+
+
+def test_persistent_server_requests_and_handoffs(monkeypatch):
+    """Back-to-back requests, new grids loaded between requests, result reads between requests, the
+    multi-device protocol pieces after a served solve, and a server that idled out (relaunched by
+    the host when the next request finds the stream empty)."""
+    import time
+
+    monkeypatch.setenv("MGDP_PERSISTENT", "1")
+    monkeypatch.setenv("MGDP_SERVE_IDLE_US", "500")
+    g = load("grids_fourrooms.npz")
+    cells = [cells_from_enc(e)[None] for e in g["enc"][:6]]
+    want = [oracle.value_iteration(0, c, dtype="f32") for c in cells]
+    vi = mg.ValueIteration(cells[0], dtype="f32")
+    for rep in range(3):
+        for i, c in enumerate(cells):
+            vi.load(c)
+            assert vi.solve() == want[i]["sweeps"]
+            assert vi.solve() == want[i]["sweeps"]  # back to back on the same grid
+            if (i + rep) % 2 == 0:
+                np.testing.assert_array_equal(vi.values(), want[i]["V"])
+                np.testing.assert_array_equal(vi.policy(), want[i]["pi"])
+            if i == 2:
+                time.sleep(0.02)  # the server leaves after 0.5 ms idle
+    # protocol pieces after a served solve (one device: the local rule is the global rule)
+    vi.load(cells[1])
+    vi.reset()
+    k = vi.run_local()
+    assert k == want[1]["sweeps"]
+    assert vi.run_to(k) < vi.tol
+    vi.finish(k, 0.0)
+    np.testing.assert_array_equal(vi.values(), want[1]["V"])
+    # timing: one resident launch serves every timed request
+    vi.enable_timing(True)
+    for _ in range(10):
+        vi.solve()
+    ms, n = vi.kernel_time()
+    assert 1 <= n <= 3 and ms > 0  # one launch unless a scheduling hiccup outlasted the 0.5 ms idle limit
+    vi.close()
+
+
+def test_persistent_server_lifetime_cap_relaunch(monkeypatch):
+    """Servers that leave on their lifetime cap while the host still counts them resident: the
+    host finds the stream drained with its request unserved and relaunches; results stay exact."""
+    monkeypatch.setenv("MGDP_PERSISTENT", "1")
+    monkeypatch.setenv("MGDP_SERVE_LIFE_US", "300")
+    t = load("table_lava11n5_s0.npz")
+    cells = cells_from_enc(t["enc"])[None]
+    o = oracle.value_iteration(0, cells, dtype="f32")
+    vi = mg.ValueIteration(cells, dtype="f32")
+    assert vi.persistent
+    vi.enable_timing(True)
+    for _ in range(200):
+        assert vi.solve() == o["sweeps"]
+    ms, n = vi.kernel_time()
+    assert n > 1  # the cap ended several servers
+    np.testing.assert_array_equal(vi.values(), o["V"])
+    np.testing.assert_array_equal(vi.policy(), o["pi"])
+    vi.close()

@@ -12,11 +12,14 @@ from collections import defaultdict
 
 SRC = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 OUT = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_traffic.json"
+# run -> (bench key, kernel, solves per launch for a persistent server launch or None)
 RUNS = {
-    "empty16": ("empty16/fused/cell/f32", "vi_fused_kernel"),
-    "empty16x65536_sweep": ("empty16x65536/sweep/cell/f32", "vi_sweep_kernel"),
-    "empty16x65536_fused": ("empty16x65536/fused/cell/f32", "vi_fused_kernel"),
-    "doorkey65536_fused": ("doorkey65536/fused/cell/f32", "vi_fused_kernel"),
+    "empty16": ("empty16/fused/cell/f32", "vi_serve_kernel", 20),
+    "empty16x65536_sweep": ("empty16x65536/sweep/cell/f32", "vi_sweep_kernel", None),
+    "empty16x65536_fused": ("empty16x65536/fused/cell/f32", "vi_fused_kernel", None),
+    "doorkey65536_fused": ("doorkey65536/fused/cell/f32", "vi_fused_kernel", None),
+    "lava65536_fused": ("lava65536/fused/cell/f32", "vi_fused_kernel", None),
+    "fourrooms4096_fused": ("fourrooms4096/fused/cell/f32", "vi_fused_kernel", None),
 }
 
 
@@ -29,7 +32,9 @@ def per_dispatch(path, kernel):
 
 
 res = {}
-for run, (key, kernel) in RUNS.items():
+for run, (key, kernel, solves) in RUNS.items():
+    if not os.path.isdir(os.path.join(SRC, f"{run}_FETCH_SIZE")):
+        continue
     f = per_dispatch(os.path.join(SRC, f"{run}_FETCH_SIZE", "run_counter_collection.csv"), kernel)
     w = per_dispatch(os.path.join(SRC, f"{run}_WRITE_SIZE", "run_counter_collection.csv"), kernel)
     n = min(len(f), len(w))
@@ -46,6 +51,9 @@ for run, (key, kernel) in RUNS.items():
         "bytes_per_launch": 2.0 * fetch + write,
         "note": "2*FETCH_SIZE + WRITE_SIZE per launch (gfx950 FETCH_SIZE half-count correction)",
     }
+    if solves:  # one resident launch served `solves` requests (bench.py scales per solve)
+        res[key]["solves_per_launch"] = solves
+        res[key]["bytes_per_solve"] = res[key]["bytes_per_launch"] / solves
 os.makedirs(os.path.dirname(OUT), exist_ok=True)
 json.dump(res, open(OUT, "w"), indent=1)
 print(json.dumps(res, indent=1))
