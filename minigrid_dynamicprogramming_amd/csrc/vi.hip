@@ -32,6 +32,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <climits>
+#include <limits>
 #include <cstring>
 #include <vector>
 
@@ -45,12 +46,14 @@ struct Geo {
     int max_sweeps;
     int nbuf;    // LDS V buffers of the fused kernel: 2, or 3 for the two-sweep XYD step
     int quad;    // fused XYD: 4 threads per cell (one per direction) instead of one
+    int pair;    // fused XYD: two-sweep step
     double tol;
 };
 
 template <typename T>
 struct Coef {
     T g, p, c;  // gamma, slip keep-prob, (1-p)/6   (all rounded to T once on the host)
+    T tol;      // smallest T >= tol: for x of type T, x >= tol (T)  <=>  (double)x >= tol
 };
 
 template <typename T>
@@ -518,6 +521,17 @@ __device__ __forceinline__ void publish(unsigned long long *host_out, unsigned l
     __hip_atomic_store(host_out + 3, (unsigned long long)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Persistent-server result: three 8-byte words, each tagged with the request epoch in its high half
+// ({k}, {dV bits 63..32}, {dV bits 31..0}), so they may land in any order and need no drain between
+// them; the host waits until all three carry its epoch.
+__device__ __forceinline__ void publish_tagged(unsigned long long *host_out, int k, double dv, unsigned int epoch) {
+    const unsigned long long tag = (unsigned long long)epoch << 32;
+    const unsigned long long b = (unsigned long long)__double_as_longlong(dv);
+    __hip_atomic_store(host_out + 5, tag | (unsigned int)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host_out + 6, tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host_out + 7, tag | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ __forceinline__ void fused_reduce(unsigned long long *red, unsigned int *ticket,
                                              unsigned long long *host_out, int k, double dvl,
                                              unsigned int *lds_flag, unsigned int epoch, bool published) {
@@ -559,7 +573,9 @@ __device__ __forceinline__ void fused_reduce(unsigned long long *red, unsigned i
 // the cell's own V in registers; per sweep the only LDS traffic is the 4 front-cell reads and the
 // cell's own write.  LOCAL: stop on this grid's own rule; else run to k_target.  Right after each
 // barrier the previous sweep's convergence flags are read together with this sweep's front-cell
-// values (independent LDS reads), so the stop test costs no extra LDS round trip.
+// values (independent LDS reads), so the stop test costs no extra LDS round trip.  (Measured
+// alternatives that lost on MI355X: taking the stop test after the update with a third buffer,
+// and same-address flag stores from every converging lane instead of one ballot per wave.)
 template <typename T, int MODEL, bool SLIP, bool LOCAL, typename Done>
 __device__ __forceinline__ void fused_fast(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *V0,
                                            T *V1, int8_t *pis, T *slots, uint8_t *flags, int &k,
@@ -574,6 +590,13 @@ __device__ __forceinline__ void fused_fast(const Geo &geo, const Coef<T> &cf, co
         if (!LOCAL) return k >= k_target;
         if (k >= geo.max_sweeps) return true;
         return k > k_start && !flags_any(flags, parity ^ 1);
+    };
+    auto advance = [&]() {
+        if (LOCAL) flag_write(diff >= cf.tol, flags, parity);
+        __syncthreads();
+        parity ^= 1;
+        cur ^= 1;
+        ++k;
     };
     if (MODEL == MGDP_MODEL_XYD) {
         const XydTopo<T> tp = xyd_topo<T>(cl, geo, cc);
@@ -590,11 +613,7 @@ __device__ __forceinline__ void fused_fast(const Geo &geo, const Coef<T> &cf, co
             diff = own_cell ? d : (T)0;
             if (own_cell) *reinterpret_cast<V4<T> *>(Vout + cc * 4) = out;
             own = out;
-            if (LOCAL) flag_write((double)diff >= geo.tol, flags, parity);
-            __syncthreads();
-            parity ^= 1;
-            cur ^= 1;
-            ++k;
+            advance();
         }
         dvl = (double)block_max(diff, slots, 0);
         done(k, dvl);
@@ -627,11 +646,7 @@ __device__ __forceinline__ void fused_fast(const Geo &geo, const Coef<T> &cf, co
             }
 #pragma unroll
             for (int l = 0; l < 16; ++l) own[l] = outv[l];
-            if (LOCAL) flag_write((double)diff >= geo.tol, flags, parity);
-            __syncthreads();
-            parity ^= 1;
-            cur ^= 1;
-            ++k;
+            advance();
         }
         dvl = (double)block_max(diff, slots, 0);
         done(k, dvl);
@@ -640,7 +655,7 @@ __device__ __forceinline__ void fused_fast(const Geo &geo, const Coef<T> &cf, co
     __syncthreads();
 }
 
-// Two-sweep step for the XYD fast path (geo.nbuf == 3).  V_{k+2}[c, d] needs V_{k+1} only at
+// Two-sweep step for the XYD fast path (geo.pair, three LDS buffers).  V_{k+2}[c, d] needs V_{k+1} only at
 // the cell itself and at state (front(c, d), d); the thread recomputes that neighbour state with
 // exactly the neighbour's own operations (bit-identical), so two Jacobi sweeps cost one barrier.
 // Buffers rotate: input X = V_k, outputs Y = V_{k+1}, Z = V_{k+2}; the convergence flags of both
@@ -703,21 +718,24 @@ __device__ __forceinline__ T xyd_value(const Coef<T> &cf, T qL, T qR, T qF, T qS
 
 template <typename T, bool SLIP, bool LOCAL, typename Done>
 __device__ __forceinline__ void fused_fast_xyd2(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
-                                                T *const (&buf)[3], int8_t *pis, T *slots, uint8_t *flags,
+                                                T *vbase, int8_t *pis, T *slots, uint8_t *flags,
                                                 int &k, int k_target, int &vfinal, double &dvl,
                                                 const Done &done) {
+    // buffer i = vbase + i*S: offsets from the LDS base keep every access a ds_* instruction (a
+    // pointer picked from an array of buffers would degrade to flat loads/stores)
+    auto buf = [&](int i) -> T * { return vbase + i * geo.S; };
     const int c = threadIdx.x;
     const int cc = c < geo.HW ? c : 0;
     const bool own_cell = c < geo.HW;
     const Xyd2Topo<T> tp = xyd2_topo<T>(cl, geo, cc);
     const int limit = LOCAL ? geo.max_sweeps : k_target;
-    V4<T> own = *reinterpret_cast<const V4<T> *>(buf[0] + cc * 4);
+    V4<T> own = *reinterpret_cast<const V4<T> *>(buf(0) + cc * 4);
     int bx = 0, by = 1, bz = 2, last_n = 0, par = 0;
     T dA = (T)0, dB = (T)0, dfin = (T)0;
     int bfin = 0, bprev = 0, kfin = k;
     while (true) {
         // speculative loads from the buffer the next step would read
-        const T *X = buf[last_n == 2 ? bz : (last_n == 1 ? by : bx)];
+        const T *X = buf(last_n == 2 ? bz : (last_n == 1 ? by : bx));
         V4<T> nb4[4];
         T n2v[4];
 #pragma unroll
@@ -748,7 +766,7 @@ __device__ __forceinline__ void fused_fast_xyd2(const Geo &geo, const Coef<T> &c
         V4<T> out1;
         uint32_t pk;
         dA = xyd_step<T, SLIP, false>(tp.b, cf, own, nbv, out1, pk);
-        if (own_cell) *reinterpret_cast<V4<T> *>(buf[by] + cc * 4) = out1;
+        if (own_cell) *reinterpret_cast<V4<T> *>(buf(by) + cc * 4) = out1;
         else dA = (T)0;
         if (n == 2) {
             T nbv2[4];
@@ -762,7 +780,7 @@ __device__ __forceinline__ void fused_fast_xyd2(const Geo &geo, const Coef<T> &c
             }
             V4<T> out2;
             dB = xyd_step<T, SLIP, false>(tp.b, cf, out1, nbv2, out2, pk);
-            if (own_cell) *reinterpret_cast<V4<T> *>(buf[bz] + cc * 4) = out2;
+            if (own_cell) *reinterpret_cast<V4<T> *>(buf(bz) + cc * 4) = out2;
             else dB = (T)0;
             own = out2;
         } else {
@@ -770,8 +788,8 @@ __device__ __forceinline__ void fused_fast_xyd2(const Geo &geo, const Coef<T> &c
             dB = (T)0;
         }
         if (LOCAL) {
-            flag_write((double)dA >= geo.tol, flags + par * 32, 0);
-            if (n == 2) flag_write((double)dB >= geo.tol, flags + par * 32 + 16, 0);
+            flag_write(dA >= cf.tol, flags + par * 32, 0);
+            if (n == 2) flag_write(dB >= cf.tol, flags + par * 32 + 16, 0);
         }
         __syncthreads();
         par ^= 1;
@@ -782,7 +800,7 @@ __device__ __forceinline__ void fused_fast_xyd2(const Geo &geo, const Coef<T> &c
     vfinal = bfin;
     dvl = (double)block_max(dfin, slots, 0);
     done(k, dvl);
-    if (own_cell) xyd_update<T, SLIP, false, true>(tp.b, cf, buf[bprev], nullptr, pis, cc);  // pi on V_{K-1}
+    if (own_cell) xyd_update<T, SLIP, false, true>(tp.b, cf, buf(bprev), nullptr, pis, cc);  // pi on V_{K-1}
     __syncthreads();
 }
 
@@ -844,7 +862,7 @@ __device__ __forceinline__ void fused_quad_xyd(const Geo &geo, const Coef<T> &cf
         if (own_cell) Vout[s] = best;
         vprev = v;
         v = best;
-        if (LOCAL) flag_write((double)diff >= geo.tol, flags, parity);
+        if (LOCAL) flag_write(diff >= cf.tol, flags, parity);
         __syncthreads();
         parity ^= 1;
         cur ^= 1;
@@ -893,8 +911,9 @@ __device__ __forceinline__ void fused_quad_xyd(const Geo &geo, const Coef<T> &cf
 // The whole fused solve of grid e by one workgroup: stage cells (and V unless fresh) in LDS, sweep
 // to the local stopping rule (k_target < 0) or to k_target, extract pi, write V / pi / (k, dV) back.
 // `lone`: this workgroup is the only one of the solve and publishes {k, dV} to the host as soon as
-// they are known (pi extraction and the write-back then overlap the host's reaction).
-template <typename T, int MODEL, bool SLIP, int MAP>
+// they are known (pi extraction and the write-back then overlap the host's reaction); `served`:
+// it does so in the persistent server's tagged form, and the cells are already staged in LDS.
+template <typename T, int MODEL, bool SLIP, int MAP, bool SERVED = false>
 __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, const uint8_t *__restrict__ cells,
                                            T *__restrict__ V, int8_t *__restrict__ pi, int32_t *__restrict__ kenv,
                                            double *__restrict__ dvenv, unsigned long long *__restrict__ host_out,
@@ -904,7 +923,6 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T), geo.nbuf);
     T *V0 = reinterpret_cast<T *>(smem);
     T *V1 = reinterpret_cast<T *>(smem + L.v_bytes);
-    T *V2 = reinterpret_cast<T *>(smem + 2 * L.v_bytes);  // used only when geo.nbuf == 3
     int8_t *pis = reinterpret_cast<int8_t *>(smem + L.pi_off());
     uint8_t *cl = reinterpret_cast<uint8_t *>(smem + L.cells_off());
     T *slots = reinterpret_cast<T *>(smem + L.slots_off());
@@ -915,7 +933,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     const bool work = k_target < 0 ? (!(k > 0 && dvl < geo.tol) && k < geo.max_sweeps) : (k < k_target);
     if (!work) return false;
     const long long vb = (long long)e * geo.S;
-    copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
+    if (!SERVED) copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
     if (k == 0) zero16(V0, L.v_bytes);
     else copy16(V0, V + vb, L.v_bytes);
     if (threadIdx.x < 64) flags[threadIdx.x] = 0;
@@ -925,17 +943,19 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     int cur = 0, parity = 0;
     T diff = (T)0;
     auto done = [&](int kk, double dv) {
-        if (lone && threadIdx.x == 0)
+        if (SERVED) {
+            if (threadIdx.x == 0) publish_tagged(host_out, kk, dv, epoch);
+        } else if (lone && threadIdx.x == 0) {
             publish(host_out, (unsigned long long)kk, (unsigned long long)__double_as_longlong(dv),
                     (unsigned long long)kk, epoch);
+        }
     };
     const T *Vfinal = nullptr;
-    if (fast && MODEL == MGDP_MODEL_XYD && geo.nbuf == 3) {
-        T *const bufs[3] = {V0, V1, V2};
+    if (fast && MODEL == MGDP_MODEL_XYD && geo.pair) {
         int vf = 0;
-        if (k_target < 0) fused_fast_xyd2<T, SLIP, true>(geo, cf, cl, bufs, pis, slots, flags, k, k_target, vf, dvl, done);
-        else fused_fast_xyd2<T, SLIP, false>(geo, cf, cl, bufs, pis, slots, flags, k, k_target, vf, dvl, done);
-        Vfinal = bufs[vf];
+        if (k_target < 0) fused_fast_xyd2<T, SLIP, true>(geo, cf, cl, V0, pis, slots, flags, k, k_target, vf, dvl, done);
+        else fused_fast_xyd2<T, SLIP, false>(geo, cf, cl, V0, pis, slots, flags, k, k_target, vf, dvl, done);
+        Vfinal = V0 + vf * geo.S;
     } else if (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL && geo.quad && 4 * geo.HW <= (int)blockDim.x) {
         if (k_target < 0) fused_quad_xyd<T, SLIP, true>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
         else fused_quad_xyd<T, SLIP, false>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
@@ -950,7 +970,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
             cur ^= 1;
             ++k;
             if (k_target < 0) {
-                const bool more = block_any((double)diff >= geo.tol, flags, parity);
+                const bool more = block_any(diff >= cf.tol, flags, parity);
                 parity ^= 1;
                 if (!more || k >= geo.max_sweeps) break;
             } else {
@@ -993,9 +1013,12 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
 }
 
 // Persistent solver for a lone grid: one workgroup stays resident and serves solve requests posted
-// in host-mapped memory, removing the launch and dispatch latency from every solve.  Lane 0 polls
-// the request word (relaxed system-scope loads + s_sleep); request r (r != served) runs a fresh
-// fused solve whose {k, dV} is published with epoch r.  Every wave leaves the loop on the quit
+// in host-mapped memory, removing the launch and dispatch latency from every solve.  The cells
+// cannot change while it is resident (every other entry point stops it first), so they are staged
+// in LDS once.  Lane 0 of every wave polls the request word (relaxed system-scope loads, the waves
+// staggered by s_sleep so a new request is seen a fraction of a round trip after it lands) and
+// also watches the LDS word another wave may already have set.  Request r (!= the last served)
+// runs a fresh fused solve whose {k, dV} is published tagged with r.  Every wave leaves on the quit
 // word, after `idle_ticks` without a request or after `life_ticks` in total (s_memrealtime,
 // 100 MHz); the host relaunches the server if a request finds it gone.
 constexpr unsigned long long kServeQuit = ~0ull;
@@ -1006,37 +1029,45 @@ vi_serve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ host_out, const unsigned long long *__restrict__ host_cmd,
                 unsigned long long served, unsigned long long idle_ticks, unsigned long long life_ticks) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ unsigned long long s_cmd;
+    const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T), geo.nbuf);
+    copy16(smem + L.cells_off(), cells, geo.HWp);
+    if (threadIdx.x == 0) s_cmd = served;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     unsigned long long t_last = t_start;
+    __syncthreads();
     while (true) {
-        if (threadIdx.x == 0) {
-            unsigned long long cmd;
+        if (lane == 0) {
+            for (int i = 0; i < wave; ++i) __builtin_amdgcn_s_sleep(8);  // stagger the pollers
             while (true) {
-                cmd = __hip_atomic_load(host_cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (cmd != served) break;
+                const unsigned long long cmd = __hip_atomic_load(host_cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (cmd != served) {
+                    __hip_atomic_store(&s_cmd, cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    break;
+                }
+                if (__hip_atomic_load(&s_cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != served) break;
                 const unsigned long long now = __builtin_amdgcn_s_memrealtime();
                 if (now - t_last > idle_ticks || now - t_start > life_ticks) {
-                    cmd = kServeQuit;
+                    __hip_atomic_store(&s_cmd, kServeQuit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);
             }
-            s_cmd = cmd;
         }
         __syncthreads();
         const unsigned long long cmd = s_cmd;
         if (cmd == kServeQuit) break;
         int k;
         double dvl;
-        if (!fused_grid<T, MODEL, SLIP, MAP>(geo, cf, cells, V, pi, kenv, dvenv, host_out, -1, 1, true,
-                                             (unsigned int)cmd, 0, k, dvl) &&
+        if (!fused_grid<T, MODEL, SLIP, MAP, true>(geo, cf, cells, V, pi, kenv, dvenv, host_out, -1, 1, true,
+                                                   (unsigned int)cmd, 0, k, dvl) &&
             threadIdx.x == 0)
-            publish(host_out, (unsigned long long)k, (unsigned long long)__double_as_longlong(dvl),
-                    (unsigned long long)k, (unsigned int)cmd);
+            publish_tagged(host_out, k, dvl, (unsigned int)cmd);
         served = cmd;
         t_last = __builtin_amdgcn_s_memrealtime();
-        __syncthreads();  // s_cmd and the LDS tiles are reused by the next request
+        __syncthreads();  // every wave is past s_cmd and the LDS tiles before the next request
     }
 }
 
@@ -1175,7 +1206,7 @@ struct mgdp_vi {
     unsigned int epoch = 0; // tag of the last fused launch; its result lands in h_out[3]
     int nbuf = 2;                 // fused LDS V buffers (3 = two-sweep XYD step)
     int quad = 0;                 // fused XYD: 4 threads per cell
-    bool nbuf3() const { return nbuf == 3; }
+    int pair = 0;                 // fused XYD: two-sweep step
     int sweep_block = 256;
     int sweep_m = 1;              // grids staged per workgroup iteration (measured: m>1 no faster)
     // persistent solver (lone grid, fused one-thread-per-cell path): see vi_serve_kernel
@@ -1205,6 +1236,7 @@ Geo make_geo(const mgdp_vi *vi) {
     g.max_sweeps = vi->d.max_sweeps;
     g.nbuf = vi->nbuf;
     g.quad = vi->quad;
+    g.pair = vi->pair;
     g.tol = vi->d.tol;
     return g;
 }
@@ -1216,6 +1248,9 @@ Coef<T> make_coef(const mgdp_vi *vi) {
     const double p = vi->d.slip_p;
     c.p = (T)p;
     c.c = (T)((1.0 - p) / 6.0);
+    T t = (T)vi->d.tol;
+    if ((double)t < vi->d.tol) t = std::nextafter(t, std::numeric_limits<T>::infinity());
+    c.tol = t;
     return c;
 }
 
@@ -1355,19 +1390,25 @@ struct SweepF {
 
 // Read the reduction the last fused launch published to host-mapped memory: max k, max dV, min k.
 int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
-    // The last workgroup (or the reduce kernel, or the persistent server) publishes {kmax, dV,
-    // kmin, epoch} to host-mapped memory; poll the epoch instead of a stream synchronisation
-    // (lower completion latency).  Everything else stays stream-ordered.  Poll the stream now and
-    // then to surface faults -- and, in serving mode, to relaunch a server that idled out before
-    // it saw the request.
+    // The last workgroup (or the reduce kernel) publishes {kmax, dV, kmin, epoch} to host-mapped
+    // memory; the persistent server publishes three epoch-tagged words instead.  Poll them rather
+    // than synchronise the stream (lower completion latency); everything else stays stream-ordered.
+    // Poll the stream now and then to surface faults -- and, in serving mode, to relaunch a server
+    // that left before it saw the request.
     const volatile unsigned long long *h = vi->h_out;
+    const unsigned long long ep = (unsigned long long)vi->epoch;
+    const bool tagged = vi->serving;
+    auto ready = [&]() -> bool {
+        if (!tagged) return h[3] == ep;
+        return (h[5] >> 32) == ep && (h[6] >> 32) == ep && (h[7] >> 32) == ep;
+    };
     int relaunches = 0;
-    for (uint64_t spin = 0; h[3] != (unsigned long long)vi->epoch; ++spin) {
+    for (uint64_t spin = 0; !ready(); ++spin) {
         if ((spin & 1023) == 1023) {
             const hipError_t q = hipStreamQuery(vi->stream);
             if (q == hipSuccess) {
-                if (h[3] == (unsigned long long)vi->epoch) break;
-                if (vi->serving && relaunches < 4) {
+                if (ready()) break;
+                if (tagged && relaunches < 4) {
                     ++relaunches;
                     if (int rc = dispatch<ServeF>(vi, vi->epoch - 1u)) return rc;
                     continue;
@@ -1378,7 +1419,15 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
         }
     }
     std::atomic_thread_fence(std::memory_order_acquire);
-    const unsigned long long km = h[0], dvb = h[1], kmin = h[2];
+    unsigned long long km, dvb, kmin;
+    if (tagged) {
+        km = kmin = h[5] & 0xffffffffull;
+        dvb = ((h[6] & 0xffffffffull) << 32) | (h[7] & 0xffffffffull);
+    } else {
+        km = h[0];
+        dvb = h[1];
+        kmin = h[2];
+    }
     std::memcpy(&vi->dv_red, (const void *)&dvb, sizeof(double));  // non-negative doubles order like their bits
     vi->k_min = (int)kmin;
     vi->k_max = (int)km;
@@ -1391,7 +1440,7 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
 // Persistent solver hand-off (lone grid on the one-thread-per-cell fused path).
 bool serve_eligible(const mgdp_vi *vi) {
     return vi->persistent && vi->d.method == MGDP_METHOD_FUSED && vi->d.B == 1 && vi->d.mapping == MGDP_MAP_CELL &&
-           vi->HW <= vi->fused_block && vi->nbuf == 2 && !vi->quad;
+           vi->HW <= vi->fused_block && !vi->pair && !vi->quad;
 }
 // Ask a resident server to leave and drain the stream.  Every entry point that enqueues other
 // work on the stream, or reads results, calls this first.
@@ -1533,12 +1582,13 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
         const bool eligible = d.model == MGDP_MODEL_XYD && d.mapping == MGDP_MAP_CELL && vi->HW <= 1024;
         int pair = 0;  // measured slower than the one-sweep step on MI355X (VALU chain, not barriers, bound it)
         if (const char *ev = std::getenv("MGDP_PAIR")) pair = std::atoi(ev);
-        vi->nbuf = eligible && pair ? 3 : 2;
+        vi->pair = eligible && pair ? 1 : 0;
         // Four threads per cell (one per direction, DPP quad exchange): MGDP_QUAD=1 enables it
         // for grids with <= 256 cells (tests cover it).
         int quad = 0;  // measured slower than one thread per cell (LDS/barrier latency bound it)
         if (const char *ev = std::getenv("MGDP_QUAD")) quad = std::atoi(ev);
-        vi->quad = eligible && !vi->nbuf3() && quad && 4 * vi->HW <= 1024 ? 1 : 0;
+        vi->quad = eligible && !vi->pair && quad && 4 * vi->HW <= 1024 ? 1 : 0;
+        vi->nbuf = vi->pair ? 3 : 2;
     }
     const Smem L = smem_layout(vi->S, vi->HWp, vi->tsize, vi->nbuf);
     if (L.total() > 160 * 1024) {

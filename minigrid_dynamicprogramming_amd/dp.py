@@ -165,6 +165,7 @@ class ValueIteration:
         d.tol = float(tol)
         d.slip_p = -1.0 if slip_p is None else float(slip_p)
         self.desc = d
+        self._solve_args = None
         h = ctypes.c_void_p()
         _lib.check(self.L.mgdp_vi_create(ctypes.byref(d), ctypes.byref(h)), "mgdp_vi_create")
         self.h = h
@@ -197,6 +198,7 @@ class ValueIteration:
         if getattr(self, "h", None):
             self.L.mgdp_vi_destroy(self.h)
             self.h = None
+            self._solve_args = None
 
     def __del__(self):
         try:
@@ -206,11 +208,13 @@ class ValueIteration:
 
     # -- single-device solve
     def solve(self) -> int:
-        k = ctypes.c_int32(0)
-        dv = ctypes.c_double(0)
-        conv = ctypes.c_int32(0)
-        _lib.check(self.L.mgdp_vi_solve(self.h, ctypes.byref(k), ctypes.byref(dv), ctypes.byref(conv)),
-                   "mgdp_vi_solve")
+        if self._solve_args is None:  # reused out-parameters: no ctypes allocations per solve
+            self._out = (ctypes.c_int32(0), ctypes.c_double(0), ctypes.c_int32(0))
+            self._solve_args = (self.h,) + tuple(ctypes.byref(o) for o in self._out)
+        rc = self.L.mgdp_vi_solve(*self._solve_args)
+        if rc:
+            _lib.check(rc, "mgdp_vi_solve")
+        k, dv, conv = self._out
         self.sweeps, self.dv, self.converged = k.value, dv.value, bool(conv.value)
         return self.sweeps
 

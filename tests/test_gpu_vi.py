@@ -271,3 +271,41 @@ def test_persistent_server_lifetime_cap_relaunch(monkeypatch):
     np.testing.assert_array_equal(vi.values(), o["V"])
     np.testing.assert_array_equal(vi.policy(), o["pi"])
     vi.close()
+
+
+@pytest.mark.parametrize("persistent", ["0", "1"])
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_fused_doorkey_lone_and_batched_bit_exact(persistent, dtype, monkeypatch):
+    """DoorKey fused local loop, lone (persistent server or one launch) and batched, including
+    max_sweeps caps that end the loop before convergence."""
+    monkeypatch.setenv("MGDP_PERSISTENT", persistent)
+    for env in ("doorkey8", "doorkey16"):
+        g = load(f"grids_{env}.npz")
+        cells = np.stack([cells_from_enc(e) for e in g["enc"]])
+        for sub in (cells[:1], cells[:7], cells):
+            r = gpu_vi(sub, "doorkey", dtype, "fused", "cell")
+            o = oracle.value_iteration(1, sub, dtype=dtype)
+            assert r.sweeps == o["sweeps"]
+            np.testing.assert_array_equal(r.V, o["V"])
+            np.testing.assert_array_equal(r.pi, o["pi"])
+        for ms in (1, 2, 17):
+            r = gpu_vi(cells[:3], "doorkey", dtype, "fused", "cell", max_sweeps=ms)
+            o = oracle.value_iteration(1, cells[:3], dtype=dtype, max_sweeps=ms)
+            assert r.sweeps == o["sweeps"] == ms
+            np.testing.assert_array_equal(r.V, o["V"])
+            np.testing.assert_array_equal(r.pi, o["pi"])
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_tolerance_threshold_edges(dtype):
+    """The kernels test |dV| >= tol against tol rounded up to the value type; exact for tolerances
+    that are (2^-20) and are not (1e-6, 3e-7, 0.01) representable in it."""
+    g = load("grids_lava11n5.npz")
+    cells = np.stack([cells_from_enc(e) for e in g["enc"][:7]])
+    for tol in (2.0 ** -20, 1e-6, 3e-7, 0.01):
+        for sub in (cells[:1], cells):
+            for method in ("fused", "sweep"):
+                r = gpu_vi(sub, "xyd", dtype, method, "cell", slip=0.9, tol=tol)
+                o = oracle.value_iteration(0, sub, slip_p=0.9, dtype=dtype, tol=tol)
+                assert r.sweeps == o["sweeps"]
+                np.testing.assert_array_equal(r.V, o["V"])
