@@ -185,6 +185,27 @@ __device__ __forceinline__ void xyd_load_nb(const XydTopo<T> &tp, const T *Vin, 
 template <typename T, bool SLIP, bool WRITE_PI>
 __device__ __forceinline__ T xyd_step(const XydTopo<T> &tp, const Coef<T> &cf, const V4<T> &own,
                                       const T (&nbv)[4], V4<T> &out, uint32_t &pk) {
+    if (!SLIP && !WRITE_PI) {
+        // Deterministic value-only form.  Rounding is monotone and g >= 0, V >= 0, so
+        //   max_a fl(g * x_a) = fl(g * max_a x_a)   and   max(., 0) is the identity:
+        // V'[d] = max(fl(g_eff * max(V[d-1], V[d], V[d+1], F[d])), tq[d]) with F[d] the value
+        // forward reads (own V[d] when blocked / terminal), tq[d] = 1 for a goal ahead, 0
+        // otherwise (lava: Q = 0), and g_eff = 0 for absorbing cells (V' = +0).  Bit-identical to
+        // the per-action form below (which the policy pass keeps).
+        const T ge = tp.valid ? cf.g : (T)0;
+        const T m02 = vmax(own.v[0], own.v[2]), m13 = vmax(own.v[1], own.v[3]);
+        const T m[4] = {vmax(vmax(own.v[0], m13), nbv[0]), vmax(vmax(own.v[1], m02), nbv[1]),
+                        vmax(vmax(own.v[2], m13), nbv[2]), vmax(vmax(own.v[3], m02), nbv[3])};
+        T dv = (T)0;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const T best = vmax(ge * m[d], tp.tq[d]);
+            out.v[d] = best;
+            dv = vmax(dv, vabs(best - own.v[d]));
+        }
+        pk = 0;
+        return dv;
+    }
     T gv[4];
 #pragma unroll
     for (int d = 0; d < 4; ++d) gv[d] = cf.g * own.v[d];
@@ -270,6 +291,43 @@ __device__ __forceinline__ void dk_load_nb(const DkTopo &tp, const T *Vin, V4<T>
 template <typename T, bool WRITE_PI>
 __device__ __forceinline__ T dk_step(const DkTopo &tp, const Coef<T> &cf, const T (&own)[16],
                                      const V4<T> (&nbs)[4], T (&outv)[16], uint32_t (&pk)[4]) {
+    if (!WRITE_PI) {
+        // Value-only form (see xyd_step): every non-terminal Q is fl(g * x) with x >= 0, so the
+        // max over actions is fl(g * max x) -- one multiply per state -- and a goal ahead adds the
+        // constant 1, lava the constant 0 (a no-op under max).  Bit-identical to the per-action
+        // form below.
+        T dv = (T)0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pk[q] = 0;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const uint32_t f = tp.f[d];
+            const V4<T> &nb = nbs[d];
+            const bool key = f & 64u, door = f & 128u;
+            const uint32_t fw = (f & 48u) ? 0u : f;  // forward reads the front state only when it is not terminal
+            const T tqd = (f & 16u) ? (T)1 : (T)0;
+#pragma unroll
+            for (int hk = 0; hk < 2; ++hk) {
+#pragma unroll
+                for (int dop = 0; dop < 2; ++dop) {
+                    const int l = (d * 2 + hk) * 2 + dop;
+                    const int hd = hk * 2 + dop;
+                    const T xS = own[l];
+                    const T xL = own[(((d + 3) & 3) * 2 + hk) * 2 + dop];
+                    const T xR = own[(((d + 1) & 3) * 2 + hk) * 2 + dop];
+                    const T xF = ((fw >> hd) & 1u) ? nb.v[hd] : xS;
+                    const T xP = (!hk && key) ? own[(d * 2 + 1) * 2 + dop] : xS;
+                    const T xD = dop ? own[(d * 2 + hk) * 2 + 0] : (hk ? own[(d * 2 + hk) * 2 + 1] : xS);
+                    const T xT = door ? xD : xS;
+                    const T M = vmax(vmax(vmax(xL, xR), xS), vmax(vmax(xF, xP), xT));
+                    const T best = ((tp.walk >> hd) & 1u) ? vmax(cf.g * M, tqd) : (T)0;
+                    outv[l] = best;
+                    dv = vmax(dv, vabs(best - own[l]));
+                }
+            }
+        }
+        return dv;
+    }
     T gv[16];
 #pragma unroll
     for (int l = 0; l < 16; ++l) gv[l] = cf.g * own[l];
@@ -569,90 +627,171 @@ __device__ __forceinline__ void fused_reduce(unsigned long long *red, unsigned i
     }
 }
 
-// Fast path of the fused solve (MAP_CELL, HW <= blockDim): one thread per cell, topology and
-// the cell's own V in registers; per sweep the only LDS traffic is the 4 front-cell reads and the
-// cell's own write.  LOCAL: stop on this grid's own rule; else run to k_target.  Right after each
-// barrier the previous sweep's convergence flags are read together with this sweep's front-cell
-// values (independent LDS reads), so the stop test costs no extra LDS round trip.  (Measured
-// alternatives that lost on MI355X: taking the stop test after the update with a third buffer,
-// and same-address flag stores from every converging lane instead of one ballot per wave.)
-template <typename T, int MODEL, bool SLIP, bool LOCAL, typename Done>
-__device__ __forceinline__ void fused_fast(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *V0,
-                                           T *V1, int8_t *pis, T *slots, uint8_t *flags, int &k,
-                                           int k_target, int &cur, double &dvl, const Done &done) {
+// XYD fast path with the LDS V tiles in direction-major (SoA) order, V_d[c] at d*HW + c: the four
+// front-cell reads of a wave are then four unit-stride ds_read_b32 (no bank conflicts; the cell-
+// major order made every read a 4-way conflict), and the cell's own update is four unit-stride
+// writes.  The HBM rows stay in the ABI's cell-major order: each thread loads / stores its own cell's
+// 16 B (V4) directly, and writes its 4 pi lanes directly, so no LDS transposition pass is needed.
+template <typename T>
+__device__ __forceinline__ XydTopo<T> xyd_topo_soa(const uint8_t *cl, const Geo &geo, int c) {
+    XydTopo<T> tp = xyd_topo<T>(cl, geo, c);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const int cell = tp.nbi[d] >> 2;  // cell-major index (cell*4 + d) -> direction-major
+        tp.nbi[d] = d * geo.HW + cell;
+    }
+    return tp;
+}
+
+template <typename T, bool SLIP, bool LOCAL, typename Done>
+__device__ __forceinline__ void fused_fast_xyd_soa(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
+                                                   T *V0, T *V1, T *slots, uint8_t *flags,
+                                                   const T *Vg, T *Vg_out, int8_t *pig, int &k,
+                                                   int k_target, double &dvl, const Done &done) {
     const int c = threadIdx.x;
     const int cc = c < geo.HW ? c : 0;  // idle threads shadow cell 0 and never write
     const bool own_cell = c < geo.HW;
+    const int HW = geo.HW;
     const int k_start = k;
-    int parity = 0;
+    const XydTopo<T> tp = xyd_topo_soa<T>(cl, geo, cc);
+    V4<T> own;
+    if (k == 0) {
+        own = V4<T>{{(T)0, (T)0, (T)0, (T)0}};
+    } else {
+        own = *reinterpret_cast<const V4<T> *>(Vg + cc * 4);
+    }
+    if (own_cell) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) V0[d * HW + c] = own.v[d];
+    }
+    __syncthreads();
+    int cur = 0, parity = 0;
     T diff = (T)0;
-    auto stop_now = [&]() -> bool {
-        if (!LOCAL) return k >= k_target;
-        if (k >= geo.max_sweeps) return true;
-        return k > k_start && !flags_any(flags, parity ^ 1);
-    };
-    auto advance = [&]() {
+    while (true) {
+        const T *Vin = cur ? V1 : V0;
+        T *Vout = cur ? V0 : V1;
+        T nbv[4];
+        xyd_load_nb(tp, Vin, nbv);
+        if (LOCAL) {
+            if (k >= geo.max_sweeps) break;
+            if (k > k_start && !flags_any(flags, parity ^ 1)) break;
+        } else if (k >= k_target) {
+            break;
+        }
+        V4<T> out;
+        uint32_t pk;
+        const T d = xyd_step<T, SLIP, false>(tp, cf, own, nbv, out, pk);
+        diff = own_cell ? d : (T)0;
+        if (own_cell) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) Vout[q * HW + c] = out.v[q];
+        }
+        own = out;
         if (LOCAL) flag_write(diff >= cf.tol, flags, parity);
         __syncthreads();
         parity ^= 1;
         cur ^= 1;
         ++k;
-    };
-    if (MODEL == MGDP_MODEL_XYD) {
-        const XydTopo<T> tp = xyd_topo<T>(cl, geo, cc);
-        V4<T> own = *reinterpret_cast<const V4<T> *>(V0 + cc * 4);
-        while (true) {
-            const T *Vin = cur ? V1 : V0;
-            T *Vout = cur ? V0 : V1;
-            T nbv[4];
-            xyd_load_nb(tp, Vin, nbv);
-            if (stop_now()) break;
-            V4<T> out;
-            uint32_t pk;
-            const T d = xyd_step<T, SLIP, false>(tp, cf, own, nbv, out, pk);
-            diff = own_cell ? d : (T)0;
-            if (own_cell) *reinterpret_cast<V4<T> *>(Vout + cc * 4) = out;
-            own = out;
-            advance();
-        }
-        dvl = (double)block_max(diff, slots, 0);
-        done(k, dvl);
-        if (own_cell)  // pi of the last sweep = argmax on V_{k-1} (buffer cur ^ 1)
-            xyd_update<T, SLIP, false, true>(tp, cf, cur ? V0 : V1, nullptr, pis, cc);
-    } else {
-        const DkTopo tp = dk_topo(cl, geo, cc);
-        T own[16];
+    }
+    dvl = (double)block_max(diff, slots, 0);
+    done(k, dvl);
+    if (own_cell) {
+        // pi of the last sweep = argmax on V_{k-1} (buffer cur ^ 1, intact); V_k is `own`
+        const T *Vp = cur ? V0 : V1;
+        V4<T> op;
+        T nbv[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const V4<T> x = *reinterpret_cast<const V4<T> *>(V0 + cc * 16 + 4 * q);
+        for (int q = 0; q < 4; ++q) op.v[q] = Vp[q * HW + c];
+        xyd_load_nb(tp, Vp, nbv);
+        V4<T> tmp;
+        uint32_t pk;
+        xyd_step<T, SLIP, true>(tp, cf, op, nbv, tmp, pk);
+        *reinterpret_cast<uint32_t *>(pig + c * 4) = pk;
+        *reinterpret_cast<V4<T> *>(Vg_out + c * 4) = own;
+    }
+}
+
+// DoorKey fast path with the LDS tiles direction-major: the 4 (has_key, door_open) values of
+// state group (c, d) are the V4 at (d*HW + c)*4, so a wave's front-cell reads and own writes are
+// unit-stride 16-B accesses.  HBM rows stay cell-major (c*16 + d*4 + hk*2 + door_open).
+__device__ __forceinline__ DkTopo dk_topo_soa(const uint8_t *cl, const Geo &geo, int c) {
+    DkTopo tp = dk_topo(cl, geo, c);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) own[4 * q + j] = x.v[j];
-        }
-        while (true) {
-            const T *Vin = cur ? V1 : V0;
-            T *Vout = cur ? V0 : V1;
-            V4<T> nbs[4];
-            dk_load_nb(tp, Vin, nbs);
-            if (stop_now()) break;
-            T outv[16];
-            uint32_t pk[4];
-            const T d = dk_step<T, false>(tp, cf, own, nbs, outv, pk);
-            diff = own_cell ? d : (T)0;
-            if (own_cell) {
+    for (int d = 0; d < 4; ++d) tp.nb[d] = (d * geo.HW + (tp.nb[d] >> 4)) * 4;
+    return tp;
+}
+
+template <typename T, bool LOCAL, typename Done>
+__device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
+                                                  T *V0, T *V1, T *slots, uint8_t *flags,
+                                                  const T *Vg, T *Vg_out, int8_t *pig, int &k,
+                                                  int k_target, double &dvl, const Done &done) {
+    const int c = threadIdx.x;
+    const int cc = c < geo.HW ? c : 0;
+    const bool own_cell = c < geo.HW;
+    const int HW = geo.HW;
+    const int k_start = k;
+    const DkTopo tp = dk_topo_soa(cl, geo, cc);
+    T own[16];
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    *reinterpret_cast<V4<T> *>(Vout + cc * 16 + 4 * q) =
-                        V4<T>{{outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]}};
-            }
+    for (int q = 0; q < 4; ++q) {
+        const V4<T> x = k == 0 ? V4<T>{{(T)0, (T)0, (T)0, (T)0}} : *reinterpret_cast<const V4<T> *>(Vg + cc * 16 + 4 * q);
 #pragma unroll
-            for (int l = 0; l < 16; ++l) own[l] = outv[l];
-            advance();
-        }
-        dvl = (double)block_max(diff, slots, 0);
-        done(k, dvl);
-        if (own_cell) dk_update<T, false, true>(tp, cf, cur ? V0 : V1, nullptr, pis, cc);
+        for (int j = 0; j < 4; ++j) own[4 * q + j] = x.v[j];
+        if (own_cell) *reinterpret_cast<V4<T> *>(V0 + (q * HW + c) * 4) = x;
     }
     __syncthreads();
+    int cur = 0, parity = 0;
+    T diff = (T)0;
+    while (true) {
+        const T *Vin = cur ? V1 : V0;
+        T *Vout = cur ? V0 : V1;
+        V4<T> nbs[4];
+        dk_load_nb(tp, Vin, nbs);
+        if (LOCAL) {
+            if (k >= geo.max_sweeps) break;
+            if (k > k_start && !flags_any(flags, parity ^ 1)) break;
+        } else if (k >= k_target) {
+            break;
+        }
+        T outv[16];
+        uint32_t pk[4];
+        const T d = dk_step<T, false>(tp, cf, own, nbs, outv, pk);
+        diff = own_cell ? d : (T)0;
+        if (own_cell) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                *reinterpret_cast<V4<T> *>(Vout + (q * HW + c) * 4) =
+                    V4<T>{{outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]}};
+        }
+#pragma unroll
+        for (int l = 0; l < 16; ++l) own[l] = outv[l];
+        if (LOCAL) flag_write(diff >= cf.tol, flags, parity);
+        __syncthreads();
+        parity ^= 1;
+        cur ^= 1;
+        ++k;
+    }
+    dvl = (double)block_max(diff, slots, 0);
+    done(k, dvl);
+    if (own_cell) {  // pi on V_{k-1} (buffer cur ^ 1); V_k is `own`
+        const T *Vp = cur ? V0 : V1;
+        T op[16], tmp[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const V4<T> x = *reinterpret_cast<const V4<T> *>(Vp + (q * HW + c) * 4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) op[4 * q + j] = x.v[j];
+        }
+        V4<T> nbs[4];
+        dk_load_nb(tp, Vp, nbs);
+        uint32_t pk[4];
+        dk_step<T, true>(tp, cf, op, nbs, tmp, pk);
+        *reinterpret_cast<uint4 *>(pig + c * 16) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<V4<T> *>(Vg_out + c * 16 + 4 * q) = V4<T>{{own[4 * q], own[4 * q + 1], own[4 * q + 2], own[4 * q + 3]}};
+    }
 }
 
 // Two-sweep step for the XYD fast path (geo.pair, three LDS buffers).  V_{k+2}[c, d] needs V_{k+1} only at
@@ -933,13 +1072,16 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     const bool work = k_target < 0 ? (!(k > 0 && dvl < geo.tol) && k < geo.max_sweeps) : (k < k_target);
     if (!work) return false;
     const long long vb = (long long)e * geo.S;
+    const bool fast = MAP == MGDP_MAP_CELL && geo.HW <= (int)blockDim.x;
+    const bool soa = fast && !geo.pair && !geo.quad;
     if (!SERVED) copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
-    if (k == 0) zero16(V0, L.v_bytes);
-    else copy16(V0, V + vb, L.v_bytes);
+    if (!soa) {
+        if (k == 0) zero16(V0, L.v_bytes);
+        else copy16(V0, V + vb, L.v_bytes);
+    }
     if (threadIdx.x < 64) flags[threadIdx.x] = 0;
     __syncthreads();
 
-    const bool fast = MAP == MGDP_MAP_CELL && geo.HW <= (int)blockDim.x;
     int cur = 0, parity = 0;
     T diff = (T)0;
     auto done = [&](int kk, double dv) {
@@ -951,7 +1093,20 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
         }
     };
     const T *Vfinal = nullptr;
-    if (fast && MODEL == MGDP_MODEL_XYD && geo.pair) {
+    if (soa) {
+        if (MODEL == MGDP_MODEL_XYD) {
+            if (k_target < 0) fused_fast_xyd_soa<T, SLIP, true>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+            else fused_fast_xyd_soa<T, SLIP, false>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+        } else {
+            if (k_target < 0) fused_fast_dk_soa<T, true>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+            else fused_fast_dk_soa<T, false>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+        }
+        if (threadIdx.x == 0) {
+            kenv[e] = k;
+            dvenv[e] = dvl;
+        }
+        return true;  // V and pi were written by their owner threads
+    } else if (fast && MODEL == MGDP_MODEL_XYD && geo.pair) {
         int vf = 0;
         if (k_target < 0) fused_fast_xyd2<T, SLIP, true>(geo, cf, cl, V0, pis, slots, flags, k, k_target, vf, dvl, done);
         else fused_fast_xyd2<T, SLIP, false>(geo, cf, cl, V0, pis, slots, flags, k, k_target, vf, dvl, done);
@@ -959,9 +1114,6 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     } else if (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL && geo.quad && 4 * geo.HW <= (int)blockDim.x) {
         if (k_target < 0) fused_quad_xyd<T, SLIP, true>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
         else fused_quad_xyd<T, SLIP, false>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
-    } else if (fast) {
-        if (k_target < 0) fused_fast<T, MODEL, SLIP, true>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
-        else fused_fast<T, MODEL, SLIP, false>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
     } else {
         while (true) {
             const T *Vin = cur ? V1 : V0;
