@@ -12,9 +12,11 @@ SOURCES = ["lib.cpp", "vi.hip", "envs.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MGDP_ARCH", "gfx950")
 
-# -ffp-contract=off: no FMA contraction, so fp32/fp64 arithmetic matches the CPU oracle bit for bit
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", f"--offload-arch={ARCH}",
-         "-Wall", "-Wno-unused-result"]
+# -ffp-contract=off: no FMA contraction, so fp32/fp64 arithmetic matches the CPU oracle bit for bit.
+# Device code: -fno-honor-nans (V, Q and rewards are finite by construction), which lets max/min
+# select v_max_f32 directly instead of canonicalising both operands first under IEEE mode.
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Xarch_device", "-fno-honor-nans",
+         f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result"]
 
 
 def needs_build() -> bool:

@@ -667,21 +667,21 @@ __device__ __forceinline__ void fused_fast_xyd_soa(const Geo &geo, const Coef<T>
     __syncthreads();
     int cur = 0, parity = 0;
     T diff = (T)0;
-    while (true) {
-        const T *Vin = cur ? V1 : V0;
-        T *Vout = cur ? V0 : V1;
+    // One sweep from Vin to Vout; false = the rule stopped before it.  The ping-pong is unrolled
+    // by two below, so each copy has fixed LDS addresses and a fixed flag parity.  Idle threads
+    // shadow cell 0, so their |dV| equals cell 0's and needs no masking.
+    auto sweep = [&](const T *Vin, T *Vout) -> bool {
         T nbv[4];
         xyd_load_nb(tp, Vin, nbv);
         if (LOCAL) {
-            if (k >= geo.max_sweeps) break;
-            if (k > k_start && !flags_any(flags, parity ^ 1)) break;
+            if (k >= geo.max_sweeps) return false;
+            if (k > k_start && !flags_any(flags, parity ^ 1)) return false;
         } else if (k >= k_target) {
-            break;
+            return false;
         }
         V4<T> out;
         uint32_t pk;
-        const T d = xyd_step<T, SLIP, false>(tp, cf, own, nbv, out, pk);
-        diff = own_cell ? d : (T)0;
+        diff = xyd_step<T, SLIP, false>(tp, cf, own, nbv, out, pk);
         if (own_cell) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) Vout[q * HW + c] = out.v[q];
@@ -690,8 +690,12 @@ __device__ __forceinline__ void fused_fast_xyd_soa(const Geo &geo, const Coef<T>
         if (LOCAL) flag_write(diff >= cf.tol, flags, parity);
         __syncthreads();
         parity ^= 1;
-        cur ^= 1;
         ++k;
+        return true;
+    };
+    while (true) {
+        if (!sweep(V0, V1)) { cur = 0; break; }
+        if (!sweep(V1, V0)) { cur = 1; break; }
     }
     dvl = (double)block_max(diff, slots, 0);
     done(k, dvl);
@@ -743,21 +747,18 @@ __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> 
     __syncthreads();
     int cur = 0, parity = 0;
     T diff = (T)0;
-    while (true) {
-        const T *Vin = cur ? V1 : V0;
-        T *Vout = cur ? V0 : V1;
+    auto sweep = [&](const T *Vin, T *Vout) -> bool {  // see fused_fast_xyd_soa
         V4<T> nbs[4];
         dk_load_nb(tp, Vin, nbs);
         if (LOCAL) {
-            if (k >= geo.max_sweeps) break;
-            if (k > k_start && !flags_any(flags, parity ^ 1)) break;
+            if (k >= geo.max_sweeps) return false;
+            if (k > k_start && !flags_any(flags, parity ^ 1)) return false;
         } else if (k >= k_target) {
-            break;
+            return false;
         }
         T outv[16];
         uint32_t pk[4];
-        const T d = dk_step<T, false>(tp, cf, own, nbs, outv, pk);
-        diff = own_cell ? d : (T)0;
+        diff = dk_step<T, false>(tp, cf, own, nbs, outv, pk);
         if (own_cell) {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
@@ -769,8 +770,12 @@ __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> 
         if (LOCAL) flag_write(diff >= cf.tol, flags, parity);
         __syncthreads();
         parity ^= 1;
-        cur ^= 1;
         ++k;
+        return true;
+    };
+    while (true) {
+        if (!sweep(V0, V1)) { cur = 0; break; }
+        if (!sweep(V1, V0)) { cur = 1; break; }
     }
     dvl = (double)block_max(diff, slots, 0);
     done(k, dvl);
