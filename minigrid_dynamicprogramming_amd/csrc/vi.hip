@@ -137,6 +137,8 @@ __device__ __forceinline__ void flag_write(bool p, uint8_t *flags, int parity) {
     if ((threadIdx.x & 63) == 0) flags[parity * 16 + (threadIdx.x >> 6)] = b != 0ull;
 }
 __device__ __forceinline__ bool flags_any(const uint8_t *flags, int parity) {
+    if (blockDim.x <= 256)  // <= 4 waves: their flag bytes are one dword
+        return *reinterpret_cast<const uint32_t *>(flags + parity * 16) != 0u;
     const uint4 f = *reinterpret_cast<const uint4 *>(flags + parity * 16);
     return (f.x | f.y | f.z | f.w) != 0u;
 }
@@ -670,7 +672,7 @@ __device__ __forceinline__ void fused_fast_xyd_soa(const Geo &geo, const Coef<T>
     // One sweep from Vin to Vout; false = the rule stopped before it.  The ping-pong is unrolled
     // by two below, so each copy has fixed LDS addresses and a fixed flag parity.  Idle threads
     // shadow cell 0, so their |dV| equals cell 0's and needs no masking.
-    auto sweep = [&](const T *Vin, T *Vout) -> bool {
+    auto sweep = [&](const T *Vin, T *Vout, const V4<T> &in, V4<T> &out) -> bool {
         T nbv[4];
         xyd_load_nb(tp, Vin, nbv);
         if (LOCAL) {
@@ -679,23 +681,22 @@ __device__ __forceinline__ void fused_fast_xyd_soa(const Geo &geo, const Coef<T>
         } else if (k >= k_target) {
             return false;
         }
-        V4<T> out;
         uint32_t pk;
-        diff = xyd_step<T, SLIP, false>(tp, cf, own, nbv, out, pk);
+        diff = xyd_step<T, SLIP, false>(tp, cf, in, nbv, out, pk);
         if (own_cell) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) Vout[q * HW + c] = out.v[q];
         }
-        own = out;
         if (LOCAL) flag_write(diff >= cf.tol, flags, parity);
         __syncthreads();
         parity ^= 1;
         ++k;
         return true;
     };
+    V4<T> alt;  // the two register sets alternate with the LDS buffers: no copies between sweeps
     while (true) {
-        if (!sweep(V0, V1)) { cur = 0; break; }
-        if (!sweep(V1, V0)) { cur = 1; break; }
+        if (!sweep(V0, V1, own, alt)) { cur = 0; break; }
+        if (!sweep(V1, V0, alt, own)) { cur = 1; own = alt; break; }
     }
     dvl = (double)block_max(diff, slots, 0);
     done(k, dvl);
@@ -747,7 +748,7 @@ __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> 
     __syncthreads();
     int cur = 0, parity = 0;
     T diff = (T)0;
-    auto sweep = [&](const T *Vin, T *Vout) -> bool {  // see fused_fast_xyd_soa
+    auto sweep = [&](const T *Vin, T *Vout, const T (&in)[16], T (&outv)[16]) -> bool {  // see fused_fast_xyd_soa
         V4<T> nbs[4];
         dk_load_nb(tp, Vin, nbs);
         if (LOCAL) {
@@ -756,26 +757,29 @@ __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> 
         } else if (k >= k_target) {
             return false;
         }
-        T outv[16];
         uint32_t pk[4];
-        diff = dk_step<T, false>(tp, cf, own, nbs, outv, pk);
+        diff = dk_step<T, false>(tp, cf, in, nbs, outv, pk);
         if (own_cell) {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 *reinterpret_cast<V4<T> *>(Vout + (q * HW + c) * 4) =
                     V4<T>{{outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]}};
         }
-#pragma unroll
-        for (int l = 0; l < 16; ++l) own[l] = outv[l];
         if (LOCAL) flag_write(diff >= cf.tol, flags, parity);
         __syncthreads();
         parity ^= 1;
         ++k;
         return true;
     };
+    T alt[16];
     while (true) {
-        if (!sweep(V0, V1)) { cur = 0; break; }
-        if (!sweep(V1, V0)) { cur = 1; break; }
+        if (!sweep(V0, V1, own, alt)) { cur = 0; break; }
+        if (!sweep(V1, V0, alt, own)) {
+            cur = 1;
+#pragma unroll
+            for (int l = 0; l < 16; ++l) own[l] = alt[l];
+            break;
+        }
     }
     dvl = (double)block_max(diff, slots, 0);
     done(k, dvl);
