@@ -125,7 +125,7 @@ def main():
     ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
     ap.add_argument("--gamma", type=float, default=0.99)
     ap.add_argument("--tol", type=float, default=1e-6)
-    ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of CPU baseline sampling")
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline sampling")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-hbm", action="store_true", help="skip the HBM-roofline side measurement")
     args = ap.parse_args()
@@ -294,7 +294,7 @@ def hbm_side_measurement(args, n_solves=3):
                        "updates_per_s": upd / el, "sweeps": ks[-1], "launches": n, "avg_launch_us": avg * 1e6,
                        "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                        "compulsory_gbs": comp, "compulsory_frac": comp / HBM_PEAK_GBS,
-                       "traffic": load_traffic(f"empty16x65536/{method}/{args.mapping}/{args.dtype}")}
+                       "traffic": load_traffic(f"empty16x65536/{method}/{args.mapping}/{args.dtype}", n_solves / max(n, 1))}
         vi.close()
     res["workload"] = "empty16x65536"
     return res

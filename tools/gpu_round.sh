@@ -10,7 +10,7 @@ mkdir -p $OUT
 timeout -k 10 900 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; exit 1; }
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; exit 1; }
 timeout -k 10 600 python bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err || { echo "bench failed"; exit 1; }
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d $OUT/prof_default -o run --output-format csv -- python3 bench.py --no-cpu --no-hbm > $OUT/prof_default.log 2>&1 || { echo "rocprof failed"; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d $OUT/prof_default -o run --output-format csv -- python3 bench.py --warmup 0 --no-cpu --no-hbm > $OUT/prof_default.log 2>&1 || { echo "rocprof failed"; exit 1; }
 for w in empty16x65536 fourrooms4096 lava65536 doorkey65536; do
   timeout -k 10 600 python bench.py --workload $w --steps 5 --warmup 1 --no-cpu > $OUT/bench_${w}.json 2> $OUT/bench_${w}.err || { echo "bench $w failed"; exit 1; }
 done
