@@ -12,5 +12,6 @@ from .minigrid_env import MiniGridEnv, MissionSpace
 from .envs import CrossingEnv, DoorKeyEnv, EmptyEnv, FourRoomsEnv
 from .registry import EnvSpec, make, register, registry
 from .dp import ValueIteration, VIResult, value_iteration
+from .vector import MiniGridVecEnv
 
 __version__ = "0.1.0"
