@@ -9,7 +9,7 @@ and the multi-GPU driver.  See DESIGN.md.
 from .core import (COLOR_NAMES, COLOR_TO_IDX, DIR_TO_VEC, IDX_TO_COLOR, IDX_TO_OBJECT, OBJECT_TO_IDX,
                    STATE_TO_IDX, Actions, Ball, Box, Door, Floor, Goal, Grid, Key, Lava, Wall, WorldObj)
 from .minigrid_env import MiniGridEnv, MissionSpace
-from .envs import CrossingEnv, DoorKeyEnv, EmptyEnv, FourRoomsEnv
+from .envs import CrossingEnv, DistShiftEnv, DoorKeyEnv, EmptyEnv, FourRoomsEnv, LavaGapEnv
 from .registry import EnvSpec, make, register, registry
 from .dp import ValueIteration, VIResult, value_iteration
 from .vector import MiniGridVecEnv

@@ -7,6 +7,10 @@ tests/test_host_envs.py against grids and sha256 digests captured from the refer
   FourRoomsEnv  minigrid/envs/fourrooms.py:60-128
   CrossingEnv   minigrid/envs/crossing.py:87-184   (LavaCrossing / SimpleCrossing)
   DoorKeyEnv    minigrid/envs/doorkey.py:63-100
+and two sibling families with the same cell types, whose grids the XYD DP
+model covers unchanged:
+  LavaGapEnv    minigrid/envs/lavagap.py:69-136
+  DistShiftEnv  minigrid/envs/distshift.py:65-121
 """
 from __future__ import annotations
 
@@ -182,4 +186,77 @@ class DoorKeyEnv(MiniGridEnv):
         self.mission = "use the key to open the door and then get to the goal"
 
 
-__all__ = ["EmptyEnv", "FourRoomsEnv", "CrossingEnv", "DoorKeyEnv", "Wall", "Lava"]
+class LavaGapEnv(MiniGridEnv):
+    """A vertical strip of lava (or walls) with one gap between the agent at (1,1) and the goal at
+    (W-2, H-2); lavagap.py:69-136."""
+
+    def __init__(self, size, obstacle_type=Lava, max_steps: int | None = None, **kwargs):
+        self.obstacle_type = obstacle_type
+        self.size = size
+        mission_space = MissionSpace(mission_func=self._gen_mission_lava if obstacle_type == Lava
+                                     else self._gen_mission)
+        if max_steps is None:
+            max_steps = 4 * size**2
+        super().__init__(mission_space=mission_space, width=size, height=size, see_through_walls=False,
+                         max_steps=max_steps, **kwargs)
+
+    @staticmethod
+    def _gen_mission_lava():
+        return "avoid the lava and get to the green goal square"
+
+    @staticmethod
+    def _gen_mission():
+        return "find the opening and get to the green goal square"
+
+    def _gen_grid(self, width, height):
+        assert width >= 5 and height >= 5
+        self.grid = Grid(width, height)
+        self.grid.wall_rect(0, 0, width, height)
+        self.agent_pos = np.array((1, 1))
+        self.agent_dir = 0
+        self.goal_pos = np.array((width - 2, height - 2))
+        self.put_obj(Goal(), *self.goal_pos)
+        # the gap: one random column in [2, W-2), one random row in [1, H-1), in that draw order
+        self.gap_pos = np.array((self._rand_int(2, width - 2), self._rand_int(1, height - 1)))
+        self.grid.vert_wall(self.gap_pos[0], 1, height - 2, self.obstacle_type)
+        self.grid.set(*self.gap_pos, None)
+        self.mission = ("avoid the lava and get to the green goal square" if self.obstacle_type == Lava
+                        else "find the opening and get to the green goal square")
+
+
+class DistShiftEnv(MiniGridEnv):
+    """Two lava strips between the agent and the goal at (W-2, 1); the second strip's row is the
+    distributional-shift knob; distshift.py:65-121."""
+
+    def __init__(self, width=9, height=7, agent_start_pos=(1, 1), agent_start_dir=0, strip2_row=2,
+                 max_steps: int | None = None, **kwargs):
+        self.agent_start_pos = agent_start_pos
+        self.agent_start_dir = agent_start_dir
+        self.goal_pos = (width - 2, 1)
+        self.strip2_row = strip2_row
+        mission_space = MissionSpace(mission_func=self._gen_mission)
+        if max_steps is None:
+            max_steps = 4 * width * height
+        super().__init__(mission_space=mission_space, width=width, height=height, see_through_walls=True,
+                         max_steps=max_steps, **kwargs)
+
+    @staticmethod
+    def _gen_mission():
+        return "get to the green goal square"
+
+    def _gen_grid(self, width, height):
+        self.grid = Grid(width, height)
+        self.grid.wall_rect(0, 0, width, height)
+        self.put_obj(Goal(), *self.goal_pos)
+        for i in range(self.width - 6):
+            self.grid.set(3 + i, 1, Lava())
+            self.grid.set(3 + i, self.strip2_row, Lava())
+        if self.agent_start_pos is not None:
+            self.agent_pos = self.agent_start_pos
+            self.agent_dir = self.agent_start_dir
+        else:
+            self.place_agent()
+        self.mission = "get to the green goal square"
+
+
+__all__ = ["EmptyEnv", "FourRoomsEnv", "CrossingEnv", "DoorKeyEnv", "LavaGapEnv", "DistShiftEnv", "Wall", "Lava"]

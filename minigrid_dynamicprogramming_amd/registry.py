@@ -62,6 +62,11 @@ def register_minigrid_envs():
     register("MiniGrid-Empty-16x16-v0", ep + "EmptyEnv", {"size": 16})
     # FourRooms, :223-226
     register("MiniGrid-FourRooms-v0", ep + "FourRoomsEnv")
+    # DistShift, :85-98 and LavaGap, :301-320 (same cell types as the XYD model)
+    register("MiniGrid-DistShift1-v0", ep + "DistShiftEnv", {"strip2_row": 2})
+    register("MiniGrid-DistShift2-v0", ep + "DistShiftEnv", {"strip2_row": 5})
+    for s in (5, 6, 7):
+        register(f"MiniGrid-LavaGapS{s}-v0", ep + "LavaGapEnv", {"size": s})
 
 
 register_minigrid_envs()

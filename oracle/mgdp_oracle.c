@@ -20,6 +20,10 @@
  *                                       Grid.slice/rotate_left/encode/process_vis
  *                                                                        minigrid/core/grid.py:110-143,244-328
  *   orc_reward                        _reward()                         minigrid/minigrid_env.py:235-240
+ *   orc_vi_ex                         the same VI with the SURVEY 8(f) options: NoDeath lava
+ *                                     (minigrid/wrappers.py:799-872) and the finite-horizon DP over
+ *                                     step_count with the exact _reward() (minigrid_env.py:235-240,
+ *                                     step_count incremented first at :522, truncation at :582-583)
  *
  * Build: oracle/Makefile (gcc -O3 -ffp-contract=off).  Floating point is evaluated without
  * contraction so fp32 and fp64 results are bit-identical to the HIP kernels (also built with
@@ -44,7 +48,8 @@ enum { D_OPEN = 0, D_CLOSED = 1, D_LOCKED = 2 };
 static const int DX[4] = {1, 0, -1, 0};
 static const int DY[4] = {0, 1, 0, -1};
 
-int orc_abi_version(void) { return 1; }
+int orc_abi_version(void) { return 2; }
+double orc_reward(int step_count, int max_steps);
 
 /* ------------------------------------------------------------------------------------------- */
 /* DP models (A9).  cells = H*W OBJECT_TO_IDX codes, row-major y*W+x (grid.py:72,78).           */
@@ -128,6 +133,39 @@ int orc_doorkey_next(const uint8_t *cells, int W, int H, int s, int a, int *sp, 
             if (dopen) *sp = (((c * 4 + d) * 2 + hk) * 2) + 0;
             else if (hk) *sp = (((c * 4 + d) * 2 + hk) * 2) + 1;
         }
+    }
+    return 1;
+}
+
+/* XYD transition under NoDeath(no_death_types=("lava",), death_cost), wrappers.py:799-872: the
+ * wrapped step moves the agent onto the lava (can_overlap, world_object.py:142-143) and the
+ * wrapper turns terminated=True into False with reward 0 + death_cost; the agent may then stand on
+ * lava (a valid state) and every action from there is the unwrapped one (a forward into another
+ * lava cell is again a death -> death_cost; forward into the goal terminates normally). */
+static int xyd_valid_nd(const uint8_t *cells, int W, int H, int s) {
+    int c = s >> 2;
+    if (c < 0 || c >= W * H) return 0;
+    return xyd_free(cells[c]) || cells[c] == T_LAVA;
+}
+
+int orc_xyd_next_nodeath(const uint8_t *cells, int W, int H, int s, int a, double death_cost, int *sp,
+                         double *r, int *done) {
+    if (!xyd_valid_nd(cells, W, H, s)) return 0;
+    int c = s >> 2, d = s & 3, x = c % W, y = c / W;
+    *r = 0.0;
+    *done = 0;
+    *sp = s;
+    if (a == 0) {
+        *sp = c * 4 + ((d + 3) & 3);
+    } else if (a == 1) {
+        *sp = c * 4 + ((d + 1) & 3);
+    } else if (a == 2) {
+        int nx = x + DX[d], ny = y + DY[d];
+        if (nx < 0 || ny < 0 || nx >= W || ny >= H) return 1;
+        int t = cells[ny * W + nx];
+        if (t == T_EMPTY || t == T_FLOOR || t == T_GOAL || t == T_LAVA) *sp = (ny * W + nx) * 4 + d;
+        if (t == T_GOAL) { *done = 1; *r = 1.0; }
+        if (t == T_LAVA) { *r = 0.0 + death_cost; }
     }
     return 1;
 }
@@ -253,6 +291,122 @@ int orc_vi(int model, int dtype, int B, int W, int H, const uint8_t *cells, doub
                       sweeps, dv_trace, dv_last);
     return vi_f64(model, B, W, H, cells, gamma, tol, slip_p, max_sweeps, nthreads, (double *)V, pi,
                   sweeps, dv_trace, dv_last);
+}
+
+/* ------------------------------------------------------------------------------------------- */
+/* VI with the SURVEY 8(f) options.                                                              */
+/*   lava_mode 1 (XYD only): NoDeath lava as above (R = death_cost on entering, not terminal).   */
+/*   horizon H > 0: finite-horizon backward induction over t = step_count before the action:     */
+/*     V_H = 0;  V_t[s] = max_a Q_t[s,a],  Q_t = done ? R_t : R_t + g*V_{t+1}[s']                */
+/*     with R_t = _reward() at step_count t+1 = (T)(1 - 0.9*((t+1)/H)) on entering the goal,     */
+/*     the table's R otherwise; truncation at step_count >= H (minigrid_env.py:582-583) is       */
+/*     V_H = 0.  Output V_0, pi_0 (and every pi_t into pi_t[H][B][S] when pi_t != NULL);         */
+/*     sweeps = H, no stopping rule.                                                             */
+/*   Otherwise identical to orc_vi.                                                              */
+/* ------------------------------------------------------------------------------------------- */
+#define DEFINE_VI_EX(T, NAME)                                                                     \
+    static int NAME(int model, int B, int W, int H, const uint8_t *cells, double gamma, double tol, \
+                    double slip_p, int max_sweeps, int nthreads, int lava_mode, double death_cost, \
+                    int horizon, T *V, int8_t *pi, int8_t *pi_t, int *sweeps_out, double *dv_last) { \
+        const int A = model == 0 ? 7 : 5;                                                         \
+        const int S = W * H * (model == 0 ? 4 : 16);                                              \
+        const long long BS = (long long)B * S;                                                    \
+        const int slip = slip_p >= 0.0;                                                           \
+        if (slip && model != 0) return -3;                                                        \
+        if (lava_mode && model != 0) return -3;                                                   \
+        int32_t *nxt = (int32_t *)malloc(sizeof(int32_t) * BS * A);                               \
+        double *rew = (double *)malloc(sizeof(double) * BS * A);                                  \
+        uint8_t *dn = (uint8_t *)malloc(BS * A);                                                  \
+        T *Vn = (T *)malloc(sizeof(T) * BS);                                                      \
+        if (!nxt || !rew || !dn || !Vn) { free(nxt); free(rew); free(dn); free(Vn); return -2; }  \
+        for (int b = 0; b < B; ++b) {                                                             \
+            const uint8_t *cb = cells + (long long)b * W * H;                                     \
+            for (int s = 0; s < S; ++s)                                                           \
+                for (int a = 0; a < A; ++a) {                                                     \
+                    const long long o = ((long long)b * S + s) * A + a;                           \
+                    int sp, d_;                                                                   \
+                    double r;                                                                     \
+                    int ok = model == 1 ? orc_doorkey_next(cb, W, H, s, a, &sp, &r, &d_)          \
+                             : lava_mode ? orc_xyd_next_nodeath(cb, W, H, s, a, death_cost, &sp, &r, &d_) \
+                                         : orc_xyd_next(cb, W, H, s, a, &sp, &r, &d_);            \
+                    nxt[o] = ok ? sp : -1;                                                        \
+                    rew[o] = ok ? r : 0.0;                                                        \
+                    dn[o] = ok ? (uint8_t)d_ : 0;                                                 \
+                }                                                                                 \
+        }                                                                                         \
+        const T g = (T)gamma, p = (T)slip_p, cc = (T)((1.0 - slip_p) / 6.0);                      \
+        for (long long i = 0; i < BS; ++i) V[i] = (T)0;                                           \
+        const int K = horizon > 0 ? horizon : max_sweeps;                                         \
+        int k = 0;                                                                                \
+        double dv = 0.0;                                                                          \
+        (void)nthreads;                                                                           \
+        while (1) {                                                                               \
+            ++k;                                                                                  \
+            const int t = horizon - k; /* finite horizon: this sweep computes V_t */              \
+            const T rgoal = horizon > 0 ? (T)orc_reward(t + 1, horizon) : (T)1.0;                 \
+            int8_t *pout = (horizon > 0 && pi_t) ? pi_t + (long long)t * BS : pi;                 \
+            double dvk = 0.0;                                                                     \
+            _Pragma("omp parallel for reduction(max : dvk) num_threads(nthreads) schedule(static)") \
+            for (long long i = 0; i < BS; ++i) {                                                  \
+                const long long b = i / S;                                                        \
+                const int32_t *nx = nxt + i * A;                                                  \
+                if (nx[0] < 0) { Vn[i] = (T)0; pout[i] = -1; continue; }                          \
+                const T *Vb = V + b * S;                                                          \
+                T qd[7];                                                                          \
+                for (int a = 0; a < A; ++a) {                                                     \
+                    const double r64 = rew[i * A + a];                                            \
+                    const T r = (dn[i * A + a] && r64 == 1.0) ? rgoal : (T)r64;                   \
+                    qd[a] = dn[i * A + a] ? r : (T)(r + g * Vb[nx[a]]);                           \
+                }                                                                                 \
+                T best = 0;                                                                       \
+                int arg = 0;                                                                      \
+                if (slip) {                                                                       \
+                    T s6 = qd[0] + qd[1];                                                         \
+                    s6 = s6 + qd[2];                                                              \
+                    s6 = s6 + qd[3];                                                              \
+                    s6 = s6 + qd[4];                                                              \
+                    s6 = s6 + qd[5];                                                              \
+                    const T tail = cc * s6;                                                       \
+                    for (int a = 0; a < A; ++a) {                                                 \
+                        const T q = (T)(p * qd[a]) + tail;                                        \
+                        if (a == 0 || q > best) { best = q; arg = a; }                            \
+                    }                                                                             \
+                } else {                                                                          \
+                    for (int a = 0; a < A; ++a)                                                   \
+                        if (a == 0 || qd[a] > best) { best = qd[a]; arg = a; }                    \
+                }                                                                                 \
+                Vn[i] = best;                                                                     \
+                pout[i] = (int8_t)arg;                                                            \
+                const T diff = best > V[i] ? best - V[i] : V[i] - best;                           \
+                if ((double)diff > dvk) dvk = (double)diff;                                       \
+            }                                                                                     \
+            memcpy(V, Vn, sizeof(T) * BS);                                                        \
+            dv = dvk;                                                                             \
+            if (horizon > 0 ? k >= horizon : (dvk < tol || k >= max_sweeps)) break;               \
+        }                                                                                         \
+        if (horizon > 0 && pi_t) memcpy(pi, pi_t, BS); /* pi_0 */                                 \
+        (void)K;                                                                                  \
+        *sweeps_out = k;                                                                          \
+        if (dv_last) *dv_last = dv;                                                               \
+        free(nxt); free(rew); free(dn); free(Vn);                                                 \
+        return 0;                                                                                 \
+    }
+
+DEFINE_VI_EX(float, vi_ex_f32)
+DEFINE_VI_EX(double, vi_ex_f64)
+
+int orc_vi_ex(int model, int dtype, int B, int W, int H, const uint8_t *cells, double gamma,
+              double tol, double slip_p, int max_sweeps, int nthreads, int lava_mode,
+              double death_cost, int horizon, void *V, int8_t *pi, int8_t *pi_t, int *sweeps,
+              double *dv_last) {
+    if (model != 0 && model != 1) return -1;
+    if (B <= 0 || W < 3 || H < 3 || max_sweeps <= 0 || horizon < 0) return -1;
+    if (nthreads <= 0) nthreads = 1;
+    if (dtype == 0)
+        return vi_ex_f32(model, B, W, H, cells, gamma, tol, slip_p, max_sweeps, nthreads, lava_mode,
+                         death_cost, horizon, (float *)V, pi, pi_t, sweeps, dv_last);
+    return vi_ex_f64(model, B, W, H, cells, gamma, tol, slip_p, max_sweeps, nthreads, lava_mode,
+                     death_cost, horizon, (double *)V, pi, pi_t, sweeps, dv_last);
 }
 
 /* ------------------------------------------------------------------------------------------- */

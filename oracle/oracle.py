@@ -38,14 +38,16 @@ def lib():
         L.orc_vi.argtypes = [_I, _I, _I, _I, _I, _P, _D, _D, _D, _I, _I, _P, _P, _P, _P, _P]
         L.orc_step.argtypes = [_I, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]
         L.orc_gen_obs.argtypes = [_I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]
+        L.orc_vi_ex.argtypes = [_I, _I, _I, _I, _I, _P, _D, _D, _D, _I, _I, _I, _D, _I, _P, _P, _P, _P, _P]
+        L.orc_xyd_next_nodeath.argtypes = [_P, _I, _I, _I, _I, _D, _P, _P, _P]
         L.orc_reward.argtypes = [_I, _I]
         L.orc_reward.restype = _D
         _lib = L
     return _lib
 
 
-def _ptr(a: np.ndarray):
-    return a.ctypes.data_as(ctypes.c_void_p)
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
 
 
 def n_actions(model: int) -> int:
@@ -89,6 +91,34 @@ def value_iteration(model: int, cells: np.ndarray, gamma=0.99, tol=1e-6, slip_p=
         raise ValueError(f"orc_vi failed rc={rc}")
     k = sweeps.value
     return {"V": V, "pi": pi, "sweeps": k, "dv_trace": trace[:k].copy(), "dv": dv_last.value}
+
+
+def value_iteration_ex(model: int, cells: np.ndarray, gamma=0.99, tol=1e-6, slip_p=None,
+                       max_sweeps=10000, dtype="f64", nthreads=1, lava_mode=0, death_cost=-1.0,
+                       horizon=0, keep_policy_t=False):
+    """orc_vi_ex: value_iteration plus NoDeath lava (lava_mode=1) and the finite-horizon DP with the
+    exact _reward() (horizon = max_steps > 0).  Returns dict(V, pi, sweeps, dv[, pi_t (H,B,S)])."""
+    cells = np.ascontiguousarray(cells, dtype=np.uint8)
+    if cells.ndim == 2:
+        cells = cells[None]
+    B, H, W = cells.shape
+    S = n_states(model, W, H)
+    npdt = np.float32 if dtype == "f32" else np.float64
+    V = np.empty((B, S), npdt)
+    pi = np.empty((B, S), np.int8)
+    pi_t = np.empty((horizon, B, S), np.int8) if (horizon > 0 and keep_policy_t) else None
+    sweeps = ctypes.c_int(0)
+    dv_last = ctypes.c_double(0)
+    rc = lib().orc_vi_ex(model, 0 if dtype == "f32" else 1, B, W, H, _ptr(cells), gamma, tol,
+                         -1.0 if slip_p is None else float(slip_p), max_sweeps, nthreads, int(lava_mode),
+                         float(death_cost), int(horizon), _ptr(V), _ptr(pi), _ptr(pi_t),
+                         ctypes.byref(sweeps), ctypes.byref(dv_last))
+    if rc != 0:
+        raise ValueError(f"orc_vi_ex failed rc={rc}")
+    out = {"V": V, "pi": pi, "sweeps": sweeps.value, "dv": dv_last.value}
+    if pi_t is not None:
+        out["pi_t"] = pi_t
+    return out
 
 
 def reward(step_count: int, max_steps: int) -> float:

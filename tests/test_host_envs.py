@@ -20,6 +20,11 @@ IDS = {
     "lava11n5": "MiniGrid-LavaCrossingS11N5-v0",
     "doorkey16": "MiniGrid-DoorKey-16x16-v0",
     "doorkey8": "MiniGrid-DoorKey-8x8-v0",
+    "lavagap5": "MiniGrid-LavaGapS5-v0",
+    "lavagap6": "MiniGrid-LavaGapS6-v0",
+    "lavagap7": "MiniGrid-LavaGapS7-v0",
+    "distshift1": "MiniGrid-DistShift1-v0",
+    "distshift2": "MiniGrid-DistShift2-v0",
 }
 
 
@@ -43,6 +48,27 @@ def test_grid_digests_match_reference(name, n):
         enc, agent = env.generate(seed=seed)
         h.update(enc.tobytes() + np.array(agent, dtype=np.int32).tobytes())
     assert h.hexdigest() == d["sha256"]
+
+
+def test_sibling_digest_and_attributes():
+    # LavaGap / DistShift, tests/golden/make_golden_f3.py
+    import json
+    import os
+
+    from tests.golden_util import GOLDEN
+
+    with open(os.path.join(GOLDEN, "digests_f3.json")) as f:
+        d = json.load(f)["lavagap7"]
+    env = mg.make(IDS["lavagap7"])
+    h = hashlib.sha256()
+    for seed in range(d["seeds"]):
+        enc, agent = env.generate(seed=seed)
+        h.update(enc.tobytes() + np.array(agent, dtype=np.int32).tobytes())
+    assert h.hexdigest() == d["sha256"]
+    for name in ("lavagap5", "lavagap6", "lavagap7", "distshift1", "distshift2"):
+        g = load(f"grids_{name}.npz")
+        e = mg.make(IDS[name])
+        assert e.max_steps == int(g["max_steps"]) and e.see_through_walls == bool(g["see_through"])
 
 
 def test_rng_stream_doctest():

@@ -4,6 +4,8 @@ Transition tables were extracted by driving the reference MiniGridEnv.step()
 (minigrid/minigrid_env.py:520-590) from every enumerated state; trajectories are 256-step rollouts
 of the reference env; V*/pi*/sweeps come from an independent numpy Jacobi over those tables.
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -91,3 +93,62 @@ def test_unknown_action_raises():
     with pytest.raises(ValueError):
         env.step(7)
     assert env.state[3] == 1  # step_count is incremented before the raise (minigrid_env.py:523,579)
+
+
+# ---------------------------------------------------------------------------------------------
+# NoDeath lava and the finite-horizon DP, pinned by make_golden_f3.py fixtures
+# ---------------------------------------------------------------------------------------------
+import glob as _glob  # noqa: E402
+import os as _os  # noqa: E402
+
+from tests.golden_util import GOLDEN as _GOLDEN  # noqa: E402
+
+
+def _f3(prefix):
+    return sorted(_os.path.basename(p)[:-4] for p in _glob.glob(_os.path.join(_GOLDEN, prefix + "_*.npz")))
+
+
+@pytest.mark.parametrize("name", _f3("nodeath"))
+def test_oracle_nodeath_vs_reference_wrapper(name):
+    """NoDeath(no_death_types=("lava",)) transition table through the reference wrapper and a numpy
+    VI over it (wrappers.py:799-872) == the oracle's lava_mode=1 model."""
+    t = load(f"{name}.npz")
+    cells = cells_from_enc(t["enc"])
+    dc = float(t["death_cost"])
+    H, W = cells.shape
+    S = W * H * 4
+    # the oracle's NoDeath transition, state by state, against the reference table
+    lib = oracle.lib()
+    sp, dn = ctypes.c_int(0), ctypes.c_int(0)
+    r = ctypes.c_double(0)
+    for s in range(S):
+        for a in range(7):
+            ok = lib.orc_xyd_next_nodeath(oracle._ptr(cells), W, H, s, a, dc, ctypes.byref(sp), ctypes.byref(r),
+                                          ctypes.byref(dn))
+            if t["nxt"][s, 0] < 0:
+                assert ok == 0
+                continue
+            assert ok == 1 and sp.value == t["nxt"][s, a] and dn.value == t["done"][s, a]
+            assert r.value == t["rew"][s, a]
+    o = oracle.value_iteration_ex(0, cells, dtype="f64", lava_mode=1, death_cost=dc)
+    assert o["sweeps"] == int(t["sweeps"])
+    np.testing.assert_array_equal(o["pi"][0], t["pi"])
+    np.testing.assert_allclose(o["V"][0], t["V"], rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("name", _f3("horizon"))
+def test_oracle_finite_horizon_vs_reference_rewards(name):
+    """The exact _reward() of every step_count (observed from reference step()) and a numpy
+    backward induction over the reference table == the oracle's horizon mode, bit for bit."""
+    t = load(f"{name}.npz")
+    cells = cells_from_enc(t["enc"])
+    model = int(t["model"])
+    Hh = int(t["max_steps"])
+    for step in range(Hh):
+        assert oracle.reward(step + 1, Hh) == t["goal_reward"][step]
+    for tag, g in (("g1", 1.0), ("g099", 0.99)):
+        o = oracle.value_iteration_ex(model, cells, gamma=g, dtype="f64", horizon=Hh, keep_policy_t=True)
+        assert o["sweeps"] == Hh
+        np.testing.assert_array_equal(o["V"][0], t[f"V_{tag}"])
+        np.testing.assert_array_equal(o["pi"][0], t[f"pi0_{tag}"])
+        np.testing.assert_array_equal(o["pi_t"][:, 0], t[f"pi_{tag}"])
