@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MGDP_ABI_VERSION 1
+#define MGDP_ABI_VERSION 2
 
 enum {
     MGDP_OK = 0,
@@ -74,6 +74,16 @@ enum {
     MGDP_MAP_CELL = 0, /* one thread per grid cell updates that cell's 4 (or 16) states            */
     MGDP_MAP_SA = 1,   /* one thread per (state, action), 8 lanes per state, wave max-reduce      */
 };
+/* DP options from the reference's own semantics (fused + MGDP_MAP_CELL only):
+ *   lava_mode MGDP_LAVA_NODEATH: NoDeath(no_death_types=("lava",), death_cost), wrappers.py:799-872
+ *     -- lava cells are states, entering lava gives R = death_cost and does not terminate (XYD).
+ *   horizon H > 0: finite-horizon DP over step_count t = 0..H-1 (H = the env's max_steps):
+ *     V_H = 0, V_t = max_a Q_t with the exact time-dependent goal reward of _reward()
+ *     (minigrid_env.py:235-240; step_count is incremented before it, :522; truncation at
+ *     step_count >= max_steps, :582-583, is V_H = 0).  Exactly H backward sweeps, no stopping
+ *     rule; V / pi report t = 0; flag MGDP_KEEP_POLICY_T keeps pi_t for every t. */
+enum { MGDP_LAVA_TERMINAL = 0, MGDP_LAVA_NODEATH = 1 };
+enum { MGDP_KEEP_POLICY_T = 1 };
 
 typedef struct {
     int32_t model;      /* MGDP_MODEL_*                                                            */
@@ -87,6 +97,11 @@ typedef struct {
     double gamma;       /* discount                                                                */
     double tol;         /* stopping threshold on max|V_k - V_{k-1}|                                 */
     double slip_p;      /* < 0: deterministic; else keep-action probability (XYD only)            */
+    int32_t horizon;    /* 0: discounted, stopping rule; H > 0: finite horizon (see above)         */
+    int32_t lava_mode;  /* MGDP_LAVA_TERMINAL | MGDP_LAVA_NODEATH                                 */
+    int32_t flags;      /* MGDP_KEEP_POLICY_T                                                      */
+    int32_t reserved2;
+    double death_cost;  /* NoDeath reward for entering lava (the wrapper's death_cost)             */
 } mgdp_vi_desc;
 
 typedef struct mgdp_vi mgdp_vi;
@@ -129,6 +144,8 @@ int mgdp_vi_finish(mgdp_vi *vi, int32_t sweeps);
 /* Results (host).  V: B*S of float or double per dtype; pi: B*S int8 (-1 = absorbing state). */
 int mgdp_vi_get_values(mgdp_vi *vi, void *V);
 int mgdp_vi_get_policy(mgdp_vi *vi, int8_t *pi);
+/* Finite horizon with MGDP_KEEP_POLICY_T: pi_t as H*B*S int8, t-major (pi_t[t][b][s]). */
+int mgdp_vi_get_policy_t(mgdp_vi *vi, int8_t *pi_t);
 /* Per-sweep global max|dV| (method SWEEP only; fused runs record only the last): n <= max_sweeps */
 int mgdp_vi_get_dv_trace(mgdp_vi *vi, double *trace, int32_t n);
 /* Device pointers of the handle's V (current) and pi buffers, for zero-copy consumers. */

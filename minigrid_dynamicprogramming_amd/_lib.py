@@ -46,6 +46,11 @@ class ViDesc(ctypes.Structure):
         ("gamma", ctypes.c_double),
         ("tol", ctypes.c_double),
         ("slip_p", ctypes.c_double),
+        ("horizon", ctypes.c_int32),
+        ("lava_mode", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
+        ("reserved2", ctypes.c_int32),
+        ("death_cost", ctypes.c_double),
     ]
 
 
@@ -78,6 +83,7 @@ SIGNATURES = {
     "mgdp_vi_enable_timing": (ctypes.c_int, [_P, _I32]),
     "mgdp_vi_kernel_time": (ctypes.c_int, [_P, _DP, _I64P]),
     "mgdp_vi_persistent": (ctypes.c_int, [_P, _I32P]),
+    "mgdp_vi_get_policy_t": (ctypes.c_int, [_P, _P]),
     "mgdp_envs_create": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, ctypes.POINTER(_P)]),
     "mgdp_envs_destroy": (ctypes.c_int, [_P]),
     "mgdp_envs_set_stream": (ctypes.c_int, [_P, _P]),
@@ -110,7 +116,7 @@ def load():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.mgdp_abi_version() != 1:
+    if L.mgdp_abi_version() != 2:
         raise MgdpError("libmgdp ABI version mismatch")
     _lib = L
     return L

@@ -21,6 +21,7 @@ extern "C" {
 
 const char *mgdp_last_error(void) { return mgdp::g_err; }
 
+static_assert(sizeof(mgdp_vi_desc) == 88, "mgdp_vi_desc layout is part of the ABI");
 int mgdp_abi_version(void) { return MGDP_ABI_VERSION; }
 
 int mgdp_device_count(int32_t *n) {

@@ -54,6 +54,7 @@ template <typename T>
 struct Coef {
     T g, p, c;  // gamma, slip keep-prob, (1-p)/6   (all rounded to T once on the host)
     T tol;      // smallest T >= tol: for x of type T, x >= tol (T)  <=>  (double)x >= tol
+    T dc;       // NoDeath: reward for entering lava (the wrapper's death_cost)
 };
 
 template <typename T>
@@ -154,13 +155,16 @@ struct XydTopo {
     uint32_t term;   // bit d: forward from dir d enters a terminal cell (goal / lava)
     int nbi[4];      // V index read by forward from dir d (own state when blocked / terminal / invalid)
     T tq[4];         // terminal forward value: 1 (goal, R = 1) or 0 (lava)
+    uint32_t lavaF;  // NoDeath: bit d = forward from dir d enters (walkable, non-terminal) lava
 };
 
-template <typename T>
+template <typename T, bool ND = false>
 __device__ __forceinline__ XydTopo<T> xyd_topo(const uint8_t *cl, const Geo &geo, int c) {
     XydTopo<T> tp;
-    tp.valid = xyd_free(cl[c]);
+    // NoDeath (wrappers.py:799-872): the agent may stand on lava; entering it is not terminal
+    tp.valid = xyd_free(cl[c]) || (ND && cl[c] == T_LAVA);
     tp.term = 0;
+    tp.lavaF = 0;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
         const int cfr = c + geo.off[d];
@@ -168,7 +172,10 @@ __device__ __forceinline__ XydTopo<T> xyd_topo(const uint8_t *cl, const Geo &geo
         tp.tq[d] = (T)0;
         tp.nbi[d] = c * 4 + d;
         if (tf == T_GOAL) { tp.term |= 1u << d; tp.tq[d] = (T)1; }
-        else if (tf == T_LAVA) { tp.term |= 1u << d; }
+        else if (tf == T_LAVA) {
+            if (ND) { tp.lavaF |= 1u << d; tp.nbi[d] = cfr * 4 + d; }
+            else tp.term |= 1u << d;
+        }
         else if (xyd_free(tf)) tp.nbi[d] = cfr * 4 + d;
     }
     return tp;
@@ -184,24 +191,32 @@ __device__ __forceinline__ void xyd_load_nb(const XydTopo<T> &tp, const T *Vin, 
     for (int d = 0; d < 4; ++d) nbv[d] = Vin[tp.nbi[d]];
 }
 
-template <typename T, bool SLIP, bool WRITE_PI>
+// ND: NoDeath lava (entering it: Q = death_cost + g*V[lava state]); FH: finite horizon, the goal
+// reward of this sweep is rg (the exact _reward() of its step_count) instead of 1.
+template <typename T, bool SLIP, bool WRITE_PI, bool ND = false, bool FH = false>
 __device__ __forceinline__ T xyd_step(const XydTopo<T> &tp, const Coef<T> &cf, const V4<T> &own,
-                                      const T (&nbv)[4], V4<T> &out, uint32_t &pk) {
+                                      const T (&nbv)[4], V4<T> &out, uint32_t &pk, T rg = (T)1) {
     if (!SLIP && !WRITE_PI) {
         // Deterministic value-only form.  Rounding is monotone and g >= 0, V >= 0, so
         //   max_a fl(g * x_a) = fl(g * max_a x_a)   and   max(., 0) is the identity:
         // V'[d] = max(fl(g_eff * max(V[d-1], V[d], V[d+1], F[d])), tq[d]) with F[d] the value
         // forward reads (own V[d] when blocked / terminal), tq[d] = 1 for a goal ahead, 0
         // otherwise (lava: Q = 0), and g_eff = 0 for absorbing cells (V' = +0).  Bit-identical to
-        // the per-action form below (which the policy pass keeps).
+        // the per-action form below (which the policy pass keeps).  NoDeath: the lava move
+        // carries a reward, so it is its own candidate fl(dc + fl(g * F[d])); V >= 0 still holds
+        // (turning in place is always worth g*V >= 0), so max with 0 stays the identity.
         const T ge = tp.valid ? cf.g : (T)0;
+        T f[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) f[d] = (ND && ((tp.lavaF >> d) & 1u)) ? own.v[d] : nbv[d];
         const T m02 = vmax(own.v[0], own.v[2]), m13 = vmax(own.v[1], own.v[3]);
-        const T m[4] = {vmax(vmax(own.v[0], m13), nbv[0]), vmax(vmax(own.v[1], m02), nbv[1]),
-                        vmax(vmax(own.v[2], m13), nbv[2]), vmax(vmax(own.v[3], m02), nbv[3])};
+        const T m[4] = {vmax(vmax(own.v[0], m13), f[0]), vmax(vmax(own.v[1], m02), f[1]),
+                        vmax(vmax(own.v[2], m13), f[2]), vmax(vmax(own.v[3], m02), f[3])};
         T dv = (T)0;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
-            const T best = vmax(ge * m[d], tp.tq[d]);
+            T best = vmax(ge * m[d], FH ? tp.tq[d] * rg : tp.tq[d]);
+            if (ND) best = vmax(best, ((tp.lavaF >> d) & 1u) ? cf.dc + cf.g * nbv[d] : (T)0);
             out.v[d] = best;
             dv = vmax(dv, vabs(best - own.v[d]));
         }
@@ -215,7 +230,8 @@ __device__ __forceinline__ T xyd_step(const XydTopo<T> &tp, const Coef<T> &cf, c
     pk = 0;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-        const T qF = ((tp.term >> d) & 1u) ? tp.tq[d] : cf.g * nbv[d];
+        const T qM = (ND && ((tp.lavaF >> d) & 1u)) ? cf.dc + cf.g * nbv[d] : cf.g * nbv[d];
+        const T qF = ((tp.term >> d) & 1u) ? (FH ? tp.tq[d] * rg : tp.tq[d]) : qM;
         const T qL = gv[(d + 3) & 3], qR = gv[(d + 1) & 3], qS = gv[d];
         T a0 = qL, a1 = qR, a2 = qF, a3 = qS;  // Q of actions 0..3 (4..6 equal action 3)
         if (SLIP) {
@@ -290,9 +306,10 @@ __device__ __forceinline__ void dk_load_nb(const DkTopo &tp, const T *Vin, V4<T>
     for (int d = 0; d < 4; ++d) nb[d] = *reinterpret_cast<const V4<T> *>(Vin + tp.nb[d]);
 }
 
-template <typename T, bool WRITE_PI>
+// FH: finite horizon, the goal reward of this sweep is rg instead of 1 (see xyd_step).
+template <typename T, bool WRITE_PI, bool FH = false>
 __device__ __forceinline__ T dk_step(const DkTopo &tp, const Coef<T> &cf, const T (&own)[16],
-                                     const V4<T> (&nbs)[4], T (&outv)[16], uint32_t (&pk)[4]) {
+                                     const V4<T> (&nbs)[4], T (&outv)[16], uint32_t (&pk)[4], T rg = (T)1) {
     if (!WRITE_PI) {
         // Value-only form (see xyd_step): every non-terminal Q is fl(g * x) with x >= 0, so the
         // max over actions is fl(g * max x) -- one multiply per state -- and a goal ahead adds the
@@ -307,7 +324,7 @@ __device__ __forceinline__ T dk_step(const DkTopo &tp, const Coef<T> &cf, const 
             const V4<T> &nb = nbs[d];
             const bool key = f & 64u, door = f & 128u;
             const uint32_t fw = (f & 48u) ? 0u : f;  // forward reads the front state only when it is not terminal
-            const T tqd = (f & 16u) ? (T)1 : (T)0;
+            const T tqd = (f & 16u) ? (FH ? rg : (T)1) : (T)0;
 #pragma unroll
             for (int hk = 0; hk < 2; ++hk) {
 #pragma unroll
@@ -351,7 +368,7 @@ __device__ __forceinline__ T dk_step(const DkTopo &tp, const Coef<T> &cf, const 
                 const T qL = gv[(((d + 3) & 3) * 2 + hk) * 2 + dop];
                 const T qR = gv[(((d + 1) & 3) * 2 + hk) * 2 + dop];
                 const T qM = ((f >> hd) & 1u) ? cf.g * nb.v[hd] : qS;
-                const T qF = goal ? (T)1 : (lava ? (T)0 : qM);
+                const T qF = goal ? (FH ? rg : (T)1) : (lava ? (T)0 : qM);
                 const T qP = (!hk && key) ? gv[(d * 2 + 1) * 2 + dop] : qS;
                 const T qD = dop ? gv[(d * 2 + hk) * 2 + 0] : (hk ? gv[(d * 2 + hk) * 2 + 1] : qS);
                 const T qT = door ? qD : qS;
@@ -634,9 +651,9 @@ __device__ __forceinline__ void fused_reduce(unsigned long long *red, unsigned i
 // major order made every read a 4-way conflict), and the cell's own update is four unit-stride
 // writes.  The HBM rows stay in the ABI's cell-major order: each thread loads / stores its own cell's
 // 16 B (V4) directly, and writes its 4 pi lanes directly, so no LDS transposition pass is needed.
-template <typename T>
+template <typename T, bool ND = false>
 __device__ __forceinline__ XydTopo<T> xyd_topo_soa(const uint8_t *cl, const Geo &geo, int c) {
-    XydTopo<T> tp = xyd_topo<T>(cl, geo, c);
+    XydTopo<T> tp = xyd_topo<T, ND>(cl, geo, c);
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
         const int cell = tp.nbi[d] >> 2;  // cell-major index (cell*4 + d) -> direction-major
@@ -645,17 +662,22 @@ __device__ __forceinline__ XydTopo<T> xyd_topo_soa(const uint8_t *cl, const Geo 
     return tp;
 }
 
-template <typename T, bool SLIP, bool LOCAL, typename Done>
+// Options: ND = NoDeath lava; HMODE 1 = finite horizon (k_target = H sweeps,
+// sweep k+1 computes V_{H-k-1} with goal reward rgoal[H-k-1]), 2 = the same keeping pi_t (per-action
+// form every sweep, 4 lanes per cell stored to pit + t*pit_stride).
+template <typename T, bool SLIP, bool LOCAL, bool ND = false, int HMODE = 0, typename Done>
 __device__ __forceinline__ void fused_fast_xyd_soa(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
                                                    T *V0, T *V1, T *slots, uint8_t *flags,
                                                    const T *Vg, T *Vg_out, int8_t *pig, int &k,
-                                                   int k_target, double &dvl, const Done &done) {
+                                                   int k_target, double &dvl, const Done &done,
+                                                   const T *rgoal = nullptr, int8_t *pit = nullptr,
+                                                   long long pit_stride = 0) {
     const int c = threadIdx.x;
     const int cc = c < geo.HW ? c : 0;  // idle threads shadow cell 0 and never write
     const bool own_cell = c < geo.HW;
     const int HW = geo.HW;
     const int k_start = k;
-    const XydTopo<T> tp = xyd_topo_soa<T>(cl, geo, cc);
+    const XydTopo<T> tp = xyd_topo_soa<T, ND>(cl, geo, cc);
     V4<T> own;
     if (k == 0) {
         own = V4<T>{{(T)0, (T)0, (T)0, (T)0}};
@@ -682,7 +704,13 @@ __device__ __forceinline__ void fused_fast_xyd_soa(const Geo &geo, const Coef<T>
             return false;
         }
         uint32_t pk;
-        diff = xyd_step<T, SLIP, false>(tp, cf, in, nbv, out, pk);
+        const T rg = HMODE ? rgoal[k_target - 1 - k] : (T)1;
+        if (HMODE == 2) {
+            diff = xyd_step<T, SLIP, true, ND, true>(tp, cf, in, nbv, out, pk, rg);
+            if (own_cell) *reinterpret_cast<uint32_t *>(pit + (long long)(k_target - 1 - k) * pit_stride + c * 4) = pk;
+        } else {
+            diff = xyd_step<T, SLIP, false, ND, HMODE != 0>(tp, cf, in, nbv, out, pk, rg);
+        }
         if (own_cell) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) Vout[q * HW + c] = out.v[q];
@@ -710,7 +738,7 @@ __device__ __forceinline__ void fused_fast_xyd_soa(const Geo &geo, const Coef<T>
         xyd_load_nb(tp, Vp, nbv);
         V4<T> tmp;
         uint32_t pk;
-        xyd_step<T, SLIP, true>(tp, cf, op, nbv, tmp, pk);
+        xyd_step<T, SLIP, true, ND, HMODE != 0>(tp, cf, op, nbv, tmp, pk, HMODE ? rgoal[k_target - k] : (T)1);
         *reinterpret_cast<uint32_t *>(pig + c * 4) = pk;
         *reinterpret_cast<V4<T> *>(Vg_out + c * 4) = own;
     }
@@ -726,11 +754,13 @@ __device__ __forceinline__ DkTopo dk_topo_soa(const uint8_t *cl, const Geo &geo,
     return tp;
 }
 
-template <typename T, bool LOCAL, typename Done>
+template <typename T, bool LOCAL, int HMODE = 0, typename Done>  // HMODE: see fused_fast_xyd_soa
 __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
                                                   T *V0, T *V1, T *slots, uint8_t *flags,
                                                   const T *Vg, T *Vg_out, int8_t *pig, int &k,
-                                                  int k_target, double &dvl, const Done &done) {
+                                                  int k_target, double &dvl, const Done &done,
+                                                  const T *rgoal = nullptr, int8_t *pit = nullptr,
+                                                  long long pit_stride = 0) {
     const int c = threadIdx.x;
     const int cc = c < geo.HW ? c : 0;
     const bool own_cell = c < geo.HW;
@@ -758,7 +788,15 @@ __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> 
             return false;
         }
         uint32_t pk[4];
-        diff = dk_step<T, false>(tp, cf, in, nbs, outv, pk);
+        const T rg = HMODE ? rgoal[k_target - 1 - k] : (T)1;
+        if (HMODE == 2) {
+            diff = dk_step<T, true, true>(tp, cf, in, nbs, outv, pk, rg);
+            if (own_cell)
+                *reinterpret_cast<uint4 *>(pit + (long long)(k_target - 1 - k) * pit_stride + c * 16) =
+                    make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        } else {
+            diff = dk_step<T, false, HMODE != 0>(tp, cf, in, nbs, outv, pk, rg);
+        }
         if (own_cell) {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
@@ -795,7 +833,7 @@ __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> 
         V4<T> nbs[4];
         dk_load_nb(tp, Vp, nbs);
         uint32_t pk[4];
-        dk_step<T, true>(tp, cf, op, nbs, tmp, pk);
+        dk_step<T, true, HMODE != 0>(tp, cf, op, nbs, tmp, pk, HMODE ? rgoal[k_target - k] : (T)1);
         *reinterpret_cast<uint4 *>(pig + c * 16) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -1232,6 +1270,73 @@ vi_serve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
     }
 }
 
+// The fused solve with the SURVEY 8(f) item-3 options (ND = NoDeath lava, HMODE = finite horizon
+// 1 / with pi_t 2): one workgroup per grid on the direction-major one-thread-per-cell path only
+// (the host enforces MGDP_MAP_CELL and no pair / quad steps when options are set).
+template <typename T, int MODEL, bool SLIP, bool ND, int HMODE>
+__global__ void __launch_bounds__(1024)
+vi_fused_opts_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
+                     int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
+                     unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
+                     unsigned long long *__restrict__ host_out, int k_target, int fresh, int in_kernel_reduce,
+                     unsigned int epoch, const T *__restrict__ rgoal, int8_t *__restrict__ pi_t) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T), geo.nbuf);
+    T *V0 = reinterpret_cast<T *>(smem);
+    T *V1 = reinterpret_cast<T *>(smem + L.v_bytes);
+    uint8_t *cl = reinterpret_cast<uint8_t *>(smem + L.cells_off());
+    T *slots = reinterpret_cast<T *>(smem + L.slots_off());
+    uint8_t *flags = reinterpret_cast<uint8_t *>(smem + L.flags_off());
+    const int e = blockIdx.x;
+    int k = fresh ? 0 : kenv[e];
+    double dvl = fresh ? 0.0 : dvenv[e];
+    const bool work = k_target < 0 ? (!(k > 0 && dvl < geo.tol) && k < geo.max_sweeps) : (k < k_target);
+    const bool lone = in_kernel_reduce && gridDim.x == 1;
+    if (work) {
+        const long long vb = (long long)e * geo.S;
+        copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
+        if (threadIdx.x < 64) flags[threadIdx.x] = 0;
+        __syncthreads();
+        auto done = [&](int kk, double dv) {
+            if (lone && threadIdx.x == 0)
+                publish(host_out, (unsigned long long)kk, (unsigned long long)__double_as_longlong(dv),
+                        (unsigned long long)kk, epoch);
+        };
+        int8_t *pit = HMODE == 2 ? pi_t + vb : nullptr;
+        const long long pstride = (long long)geo.B * geo.S;
+        if constexpr (MODEL == MGDP_MODEL_XYD) {
+            if constexpr (HMODE == 0) {
+                if (k_target < 0)
+                    fused_fast_xyd_soa<T, SLIP, true, ND, HMODE>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb,
+                                                                 k, k_target, dvl, done, rgoal, pit, pstride);
+                else
+                    fused_fast_xyd_soa<T, SLIP, false, ND, HMODE>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb,
+                                                                  k, k_target, dvl, done, rgoal, pit, pstride);
+            } else {  // finite horizon: exactly k_target = H sweeps
+                fused_fast_xyd_soa<T, SLIP, false, ND, HMODE>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb,
+                                                              k, k_target, dvl, done, rgoal, pit, pstride);
+            }
+        } else {
+            if constexpr (HMODE == 0) {
+                if (k_target < 0)
+                    fused_fast_dk_soa<T, true, HMODE>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k,
+                                                      k_target, dvl, done, rgoal, pit, pstride);
+                else
+                    fused_fast_dk_soa<T, false, HMODE>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k,
+                                                       k_target, dvl, done, rgoal, pit, pstride);
+            } else {
+                fused_fast_dk_soa<T, false, HMODE>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k,
+                                                   k_target, dvl, done, rgoal, pit, pstride);
+            }
+        }
+        if (threadIdx.x == 0) {
+            kenv[e] = k;
+            dvenv[e] = dvl;
+        }
+    }
+    if (in_kernel_reduce) fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16), epoch, work);
+}
+
 // Large batches: one workgroup reduces the per-grid (kenv, dvenv) into host-mapped memory (a
 // single arrival ticket shared by tens of thousands of workgroups would serialise on one address).
 __global__ void __launch_bounds__(1024)
@@ -1370,6 +1475,10 @@ struct mgdp_vi {
     int pair = 0;                 // fused XYD: two-sweep step
     int sweep_block = 256;
     int sweep_m = 1;              // grids staged per workgroup iteration (measured: m>1 no faster)
+    // SURVEY 8(f) item-3 options (NoDeath lava, finite horizon): vi_fused_opts_kernel
+    bool opts = false;
+    void *d_rgoal = nullptr;      // T[H]: the exact _reward() of step_count t+1, per t
+    int8_t *d_pi_t = nullptr;     // int8[H][B][S] with MGDP_KEEP_POLICY_T
     // persistent solver (lone grid, fused one-thread-per-cell path): see vi_serve_kernel
     bool persistent = true;       // MGDP_PERSISTENT=0 disables it
     bool serving = false;         // a vi_serve_kernel launch may be resident on `stream`
@@ -1412,6 +1521,7 @@ Coef<T> make_coef(const mgdp_vi *vi) {
     T t = (T)vi->d.tol;
     if ((double)t < vi->d.tol) t = std::nextafter(t, std::numeric_limits<T>::infinity());
     c.tol = t;
+    c.dc = (T)vi->d.death_cost;
     return c;
 }
 
@@ -1453,8 +1563,49 @@ int timed_collect(mgdp_vi *vi) {
     return 0;
 }
 
+template <typename T, int MODEL, bool SLIP, bool ND, int HMODE>
+int launch_opts_t(mgdp_vi *vi, int k_target) {
+    const Geo g = make_geo(vi);
+    const Smem L = smem_layout(vi->S, vi->HWp, sizeof(T), vi->nbuf);
+    auto kern = vi_fused_opts_kernel<T, MODEL, SLIP, ND, HMODE>;
+    if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
+    TimedPair tp;
+    if (int rc = timed_begin(vi, -1, &tp)) return rc;
+    hipExtLaunchKernelGGL(kern, dim3(vi->d.B), dim3(vi->fused_block), L.total(), vi->stream, tp.a, tp.b, 0, g,
+                          make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv, vi->d_dvenv,
+                          vi->d_red, vi->d_ticket, vi->d_hout, k_target, vi->fresh,
+                          vi->d.B <= kInKernelReduceMaxB ? 1 : 0, ++vi->epoch, (const T *)vi->d_rgoal, vi->d_pi_t);
+    MGDP_HIP(hipGetLastError());
+    vi->fresh = 0;
+    if (vi->d.B > kInKernelReduceMaxB) {
+        hipLaunchKernelGGL(vi_reduce_kernel, dim3(1), dim3(1024), 0, vi->stream, vi->d_kenv, vi->d_dvenv, vi->d.B,
+                           vi->d_hout, vi->epoch);
+        MGDP_HIP(hipGetLastError());
+    }
+    return 0;
+}
+
+// runtime options -> template instantiation of the options kernel
+template <typename T, int MODEL, bool SLIP, bool ND>
+int launch_opts_h(mgdp_vi *vi, int k_target) {
+    const int hm = vi->d.horizon > 0 ? ((vi->d.flags & MGDP_KEEP_POLICY_T) ? 2 : 1) : 0;
+    if (hm == 2) return launch_opts_t<T, MODEL, SLIP, ND, 2>(vi, k_target);
+    if (hm == 1) return launch_opts_t<T, MODEL, SLIP, ND, 1>(vi, k_target);
+    return launch_opts_t<T, MODEL, SLIP, ND, 0>(vi, k_target);
+}
+template <typename T>
+int launch_opts(mgdp_vi *vi, int k_target) {
+    if (vi->d.model == MGDP_MODEL_DOORKEY) return launch_opts_h<T, MGDP_MODEL_DOORKEY, false, false>(vi, k_target);
+    const bool slip = vi->d.slip_p >= 0.0, nd = vi->d.lava_mode == MGDP_LAVA_NODEATH;
+    if (slip) return nd ? launch_opts_h<T, MGDP_MODEL_XYD, true, true>(vi, k_target)
+                        : launch_opts_h<T, MGDP_MODEL_XYD, true, false>(vi, k_target);
+    return nd ? launch_opts_h<T, MGDP_MODEL_XYD, false, true>(vi, k_target)
+              : launch_opts_h<T, MGDP_MODEL_XYD, false, false>(vi, k_target);
+}
+
 template <typename T, int MODEL, bool SLIP, int MAP>
 int launch_fused_t(mgdp_vi *vi, int k_target) {
+    if (vi->opts) return launch_opts<T>(vi, k_target);
     const Geo g = make_geo(vi);
     const Smem L = smem_layout(vi->S, vi->HWp, sizeof(T), vi->nbuf);
     auto kern = vi_fused_kernel<T, MODEL, SLIP, MAP>;
@@ -1600,7 +1751,7 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
 
 // Persistent solver hand-off (lone grid on the one-thread-per-cell fused path).
 bool serve_eligible(const mgdp_vi *vi) {
-    return vi->persistent && vi->d.method == MGDP_METHOD_FUSED && vi->d.B == 1 && vi->d.mapping == MGDP_MAP_CELL &&
+    return vi->persistent && !vi->opts && vi->d.method == MGDP_METHOD_FUSED && vi->d.B == 1 && vi->d.mapping == MGDP_MAP_CELL &&
            vi->HW <= vi->fused_block && !vi->pair && !vi->quad;
 }
 // Ask a resident server to leave and drain the stream.  Every entry point that enqueues other
@@ -1690,7 +1841,8 @@ int validate_cells(const mgdp_vi_desc &d, const uint8_t *cells) {
                 }
                 MGDP_CHECK(ok, MGDP_E_UNSUPPORTED, "grid %d cell (%d,%d): type %d is outside the %s model", b, x, y, t,
                            d.model == MGDP_MODEL_XYD ? "XYD" : "DoorKey");
-                MGDP_CHECK(!(border && (t == T_EMPTY || t == T_FLOOR)), MGDP_E_UNSUPPORTED,
+                MGDP_CHECK(!(border && (t == T_EMPTY || t == T_FLOOR || (d.lava_mode == MGDP_LAVA_NODEATH && t == T_LAVA))),
+                           MGDP_E_UNSUPPORTED,
                            "grid %d border cell (%d,%d) is walkable; the model needs a closed border", b, x, y);
             }
         if (d.model == MGDP_MODEL_DOORKEY)
@@ -1719,11 +1871,22 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     MGDP_CHECK(d.mapping == MGDP_MAP_CELL || d.mapping == MGDP_MAP_SA, MGDP_E_INVALID, "unknown mapping %d", d.mapping);
     MGDP_CHECK(d.B > 0 && d.W >= 3 && d.H >= 3, MGDP_E_INVALID, "bad shape B=%d W=%d H=%d", d.B, d.W, d.H);
     MGDP_CHECK(d.max_sweeps > 0, MGDP_E_INVALID, "max_sweeps must be > 0");
-    MGDP_CHECK(d.gamma >= 0.0 && d.gamma < 1.0, MGDP_E_INVALID, "gamma must be in [0, 1)");
+    MGDP_CHECK(d.gamma >= 0.0 && (d.gamma < 1.0 || (d.horizon > 0 && d.gamma <= 1.0)), MGDP_E_INVALID,
+               "gamma must be in [0, 1) (or [0, 1] with a finite horizon)");
     MGDP_CHECK(d.tol > 0.0, MGDP_E_INVALID, "tol must be > 0");
     MGDP_CHECK(!(d.slip_p >= 0.0 && d.model != MGDP_MODEL_XYD), MGDP_E_UNSUPPORTED,
                "slip transitions are defined for the XYD model only");
     MGDP_CHECK(d.slip_p <= 1.0, MGDP_E_INVALID, "slip_p must be <= 1");
+    MGDP_CHECK(d.horizon >= 0, MGDP_E_INVALID, "horizon must be >= 0");
+    MGDP_CHECK(d.lava_mode == MGDP_LAVA_TERMINAL || d.lava_mode == MGDP_LAVA_NODEATH, MGDP_E_INVALID,
+               "unknown lava_mode %d", d.lava_mode);
+    MGDP_CHECK(!(d.lava_mode == MGDP_LAVA_NODEATH && d.model != MGDP_MODEL_XYD), MGDP_E_UNSUPPORTED,
+               "NoDeath lava is defined for the XYD model (DoorKey grids hold no lava)");
+    MGDP_CHECK(!((d.flags & MGDP_KEEP_POLICY_T) && d.horizon == 0), MGDP_E_INVALID,
+               "MGDP_KEEP_POLICY_T needs a finite horizon");
+    MGDP_CHECK(!((d.horizon > 0 || d.lava_mode) && (d.method != MGDP_METHOD_FUSED || d.mapping != MGDP_MAP_CELL)),
+               MGDP_E_UNSUPPORTED, "horizon / lava_mode options run on the fused MGDP_MAP_CELL path only");
+    MGDP_CHECK(!(d.horizon > 0 && (long long)d.W * d.H > 1024), MGDP_E_UNSUPPORTED, "horizon needs W*H <= 1024");
     int ndev = 0;
     MGDP_HIP(hipGetDeviceCount(&ndev));
     MGDP_CHECK(d.device >= 0 && d.device < ndev, MGDP_E_HIP, "device %d not available (%d visible)", d.device, ndev);
@@ -1749,6 +1912,8 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
         int quad = 0;  // measured slower than one thread per cell (LDS/barrier latency bound it)
         if (const char *ev = std::getenv("MGDP_QUAD")) quad = std::atoi(ev);
         vi->quad = eligible && !vi->pair && quad && 4 * vi->HW <= 1024 ? 1 : 0;
+        vi->opts = d.horizon > 0 || d.lava_mode != MGDP_LAVA_TERMINAL;
+        if (vi->opts) vi->pair = vi->quad = 0;  // the options kernel runs the direction-major path only
         vi->nbuf = vi->pair ? 3 : 2;
     }
     const Smem L = smem_layout(vi->S, vi->HWp, vi->tsize, vi->nbuf);
@@ -1778,6 +1943,19 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     al((void **)&vi->d_dvenv, sizeof(double) * d.B);
     al((void **)&vi->d_shards, sizeof(unsigned long long) * 8 * (size_t)(d.max_sweeps + 1));
     al((void **)&vi->d_red, sizeof(unsigned long long) * (kRedShards * 4 + 2));
+    if (d.horizon > 0) {
+        al(&vi->d_rgoal, (size_t)d.horizon * vi->tsize);
+        if (d.flags & MGDP_KEEP_POLICY_T) al((void **)&vi->d_pi_t, (size_t)d.horizon * BS);
+        if (e == hipSuccess) {  // goal reward of step_count t+1: _reward(), minigrid_env.py:235-240
+            std::vector<unsigned char> rg((size_t)d.horizon * vi->tsize);
+            for (int t = 0; t < d.horizon; ++t) {
+                const double r = 1.0 - 0.9 * ((double)(t + 1) / (double)d.horizon);
+                if (vi->tsize == 4) reinterpret_cast<float *>(rg.data())[t] = (float)r;
+                else reinterpret_cast<double *>(rg.data())[t] = r;
+            }
+            e = hipMemcpy(vi->d_rgoal, rg.data(), rg.size(), hipMemcpyHostToDevice);
+        }
+    }
     if (e == hipSuccess) e = hipHostMalloc((void **)&vi->h_out, 8 * sizeof(unsigned long long),
                                            hipHostMallocMapped | hipHostMallocCoherent);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&vi->d_hout, vi->h_out, 0);
@@ -1826,6 +2004,8 @@ int mgdp_vi_destroy(mgdp_vi *vi) {
     (void)hipFree(vi->d_dvenv);
     (void)hipFree(vi->d_shards);
     (void)hipFree(vi->d_red);
+    (void)hipFree(vi->d_rgoal);
+    (void)hipFree(vi->d_pi_t);
     if (vi->h_out) (void)hipHostFree(vi->h_out);
     if (vi->own_stream) (void)hipStreamDestroy(vi->stream);
     delete vi;
@@ -1899,7 +2079,9 @@ int mgdp_vi_run_local(mgdp_vi *vi, int32_t *k_local_max) {
             if (int rc = serve_request(vi)) return rc;
         } else {
             if (int rc = server_stop(vi)) return rc;
-            if (int rc = dispatch<FusedF>(vi, -1)) return rc;
+            // a finite horizon is exactly H backward sweeps from V_H = 0
+            if (vi->d.horizon > 0) MGDP_CHECK(vi->fresh, MGDP_E_INVALID, "finite horizon: call mgdp_vi_reset first");
+            if (int rc = dispatch<FusedF>(vi, vi->d.horizon > 0 ? vi->d.horizon : -1)) return rc;
         }
         int32_t km;
         if (int rc = reduce_env(vi, &km, nullptr)) return rc;
@@ -1922,6 +2104,8 @@ int mgdp_vi_run_to(mgdp_vi *vi, int32_t k_target, double *dv_out) {
             *dv_out = vi->dv_red;
             return 0;
         }
+        MGDP_CHECK(vi->d.horizon == 0, MGDP_E_INVALID,
+                   "finite horizon: the DP is exactly H sweeps (mgdp_vi_run_local / mgdp_vi_solve)");
         if (int rc = server_stop(vi)) return rc;
         if (int rc = dispatch<FusedF>(vi, k_target)) return rc;
         int32_t km;
@@ -1974,12 +2158,12 @@ int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *con
     if (int rc = mgdp_vi_run_local(vi, &k)) return rc;
     double dv = 0.0;
     if (int rc = mgdp_vi_run_to(vi, k, &dv)) return rc;
-    while (!(dv < vi->d.tol) && k < vi->d.max_sweeps) {  // contraction broken by rounding: global rule
+    while (vi->d.horizon == 0 && !(dv < vi->d.tol) && k < vi->d.max_sweeps) {  // contraction broken by rounding: global rule
         if (int rc = mgdp_vi_sweep(vi, &dv)) return rc;
         ++k;
     }
     if (int rc = mgdp_vi_finish(vi, k)) return rc;
-    vi->converged = dv < vi->d.tol;
+    vi->converged = vi->d.horizon > 0 ? 1 : dv < vi->d.tol;  // a finite horizon is exact after H sweeps
     if (sweeps_out) *sweeps_out = k;
     if (dv_out) *dv_out = dv;
     if (converged_out) *converged_out = vi->converged;
@@ -1998,6 +2182,15 @@ int mgdp_vi_get_values(mgdp_vi *vi, void *V) {
     if (int rc = server_stop(vi)) return rc;
     const void *src = vi->d.method == MGDP_METHOD_SWEEP ? vi->d_V[vi->cur] : vi->d_V[0];
     MGDP_HIP(hipMemcpyAsync(V, src, (size_t)vi->d.B * vi->S * vi->tsize, hipMemcpyDeviceToHost, vi->stream));
+    MGDP_HIP(hipStreamSynchronize(vi->stream));
+    return 0;
+}
+
+int mgdp_vi_get_policy_t(mgdp_vi *vi, int8_t *pi_t) {
+    MGDP_CHECK(vi && pi_t, MGDP_E_INVALID, "null argument");
+    MGDP_CHECK(vi->d_pi_t, MGDP_E_INVALID, "no per-step policy: create with horizon > 0 and MGDP_KEEP_POLICY_T");
+    DeviceGuard guard(vi->d.device);
+    MGDP_HIP(hipMemcpyAsync(pi_t, vi->d_pi_t, (size_t)vi->d.horizon * vi->d.B * vi->S, hipMemcpyDeviceToHost, vi->stream));
     MGDP_HIP(hipStreamSynchronize(vi->stream));
     return 0;
 }

@@ -136,7 +136,12 @@ class ValueIteration:
 
     def __init__(self, grids, model: str = "auto", gamma: float = 0.99, tol: float = 1e-6,
                  slip_p: float | None = None, max_sweeps: int = 10000, dtype: str = "f32",
-                 method: str = "fused", mapping: str = "cell", device: int = 0, stream=None):
+                 method: str = "fused", mapping: str = "cell", device: int = 0, stream=None,
+                 lava: str = "terminal", death_cost: float = -1.0, horizon: int = 0,
+                 keep_policy_t: bool = False):
+        """lava="nodeath": NoDeath(no_death_types=("lava",), death_cost) semantics
+        (wrappers.py:799-872).  horizon=H > 0: finite-horizon DP over step_count with the exact
+        _reward() (minigrid_env.py:235-240), H = the env's max_steps; keep_policy_t keeps pi_t."""
         cells, enc = to_cells(grids)
         if model == "auto":
             model = infer_model(cells)
@@ -164,6 +169,13 @@ class ValueIteration:
         d.gamma = float(gamma)
         d.tol = float(tol)
         d.slip_p = -1.0 if slip_p is None else float(slip_p)
+        if lava not in ("terminal", "nodeath"):
+            raise ValueError(f"lava must be 'terminal' or 'nodeath', got {lava!r}")
+        d.lava_mode = 1 if lava == "nodeath" else 0
+        d.death_cost = float(death_cost)
+        d.horizon = int(horizon)
+        d.flags = 1 if keep_policy_t else 0
+        self.horizon = int(horizon)
         self.desc = d
         self._solve_args = None
         h = ctypes.c_void_p()
@@ -243,6 +255,12 @@ class ValueIteration:
         self.converged = dv < self.tol
 
     # -- results
+    def policy_t(self) -> np.ndarray:
+        """Finite horizon with keep_policy_t: (H, B, S) int8, pi_t[t] = the greedy lane at step_count t."""
+        out = np.empty((self.horizon, self.B, self.S), np.int8)
+        _lib.check(self.L.mgdp_vi_get_policy_t(self.h, _lib.ptr(out)), "mgdp_vi_get_policy_t")
+        return out
+
     def values(self) -> np.ndarray:
         V = np.empty((self.B, self.S), self.np_dtype)
         _lib.check(self.L.mgdp_vi_get_values(self.h, _lib.ptr(V)), "mgdp_vi_get_values")

@@ -29,7 +29,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_version_and_error_string():
     L = _lib.load()
-    assert L.mgdp_abi_version() == 1
+    assert L.mgdp_abi_version() == 2
     n = ctypes.c_int32(-1)
     assert L.mgdp_device_count(ctypes.byref(n)) == 0
     assert n.value >= 0
@@ -44,9 +44,10 @@ def test_code_object_targets_gfx950():
 
 
 def test_desc_struct_layout_matches_header():
-    # int32 x 10 then 3 doubles
-    assert ctypes.sizeof(_lib.ViDesc) == 10 * 4 + 3 * 8
+    # int32 x 10, 3 doubles, int32 x 4, 1 double
+    assert ctypes.sizeof(_lib.ViDesc) == 10 * 4 + 3 * 8 + 4 * 4 + 8
     assert _lib.ViDesc.gamma.offset == 40
+    assert _lib.ViDesc.horizon.offset == 64 and _lib.ViDesc.death_cost.offset == 80
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="GPU present: the no-GPU error path is not reachable")

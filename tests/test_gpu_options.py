@@ -1,0 +1,167 @@
+"""SURVEY 8(f) item 3 on the GPU: NoDeath lava (wrappers.py:799-872) and the finite-horizon DP
+with the exact _reward() (minigrid_env.py:235-240), through the C ABI.
+
+Against the reference-derived fixtures of tests/golden/make_golden_f3.py (tables driven through
+the reference NoDeath wrapper and reference step() at every step_count, numpy VI / backward
+induction over them) and bit-exact against the oracle's orc_vi_ex at every size.  The finite
+horizon is also checked end to end: its per-step policy, executed by the GPU step kernel from
+reset(seed), collects exactly V_0[start] in real env reward.
+"""
+import numpy as np
+import pytest
+
+import minigrid_dynamicprogramming_amd as mg
+from minigrid_dynamicprogramming_amd.core import OBJECT_TO_IDX
+from oracle import oracle
+from tests.golden_util import cells_from_enc, load
+from tests.test_oracle_golden import _f3
+
+pytestmark = pytest.mark.gpu
+
+
+def _solve(cells, **kw):
+    vi = mg.ValueIteration(cells, **kw)
+    vi.solve()
+    out = {"V": vi.values(), "pi": vi.policy(), "sweeps": vi.sweeps, "converged": vi.converged}
+    if kw.get("keep_policy_t"):
+        out["pi_t"] = vi.policy_t()
+    vi.close()
+    return out
+
+
+@pytest.mark.parametrize("name", _f3("nodeath"))
+def test_nodeath_vs_reference_fixture_and_oracle(name):
+    t = load(f"{name}.npz")
+    cells = cells_from_enc(t["enc"])[None]
+    dc = float(t["death_cost"])
+    r = _solve(cells, model="xyd", dtype="f64", lava="nodeath", death_cost=dc)
+    assert r["sweeps"] == int(t["sweeps"]) and r["converged"]
+    np.testing.assert_array_equal(r["pi"][0], t["pi"])
+    np.testing.assert_allclose(r["V"][0], t["V"], rtol=0, atol=1e-12)
+    for dtype in ("f32", "f64"):
+        for slip in (None, 0.9):
+            r = _solve(cells, model="xyd", dtype=dtype, lava="nodeath", death_cost=dc, slip_p=slip)
+            o = oracle.value_iteration_ex(0, cells, dtype=dtype, slip_p=slip, lava_mode=1, death_cost=dc)
+            assert r["sweeps"] == o["sweeps"]
+            np.testing.assert_array_equal(r["V"], o["V"])
+            np.testing.assert_array_equal(r["pi"], o["pi"])
+
+
+@pytest.mark.parametrize("dc", [-1.0, -0.05, 0.5])
+def test_nodeath_batched_vs_oracle(dc):
+    g = load("grids_lava11n5.npz")
+    cells = np.stack([cells_from_enc(e) for e in g["enc"]])
+    for dtype in ("f32", "f64"):
+        r = _solve(cells, model="xyd", dtype=dtype, lava="nodeath", death_cost=dc)
+        o = oracle.value_iteration_ex(0, cells, dtype=dtype, lava_mode=1, death_cost=dc)
+        assert r["sweeps"] == o["sweeps"]
+        np.testing.assert_array_equal(r["V"], o["V"])
+        np.testing.assert_array_equal(r["pi"], o["pi"])
+
+
+@pytest.mark.parametrize("name", _f3("horizon"))
+def test_finite_horizon_vs_reference_fixture_and_oracle(name):
+    t = load(f"{name}.npz")
+    model = "xyd" if int(t["model"]) == 0 else "doorkey"
+    cells = cells_from_enc(t["enc"])[None]
+    Hh = int(t["max_steps"])
+    for tag, g in (("g1", 1.0), ("g099", 0.99)):
+        r = _solve(cells, model=model, dtype="f64", gamma=g, horizon=Hh, keep_policy_t=True)
+        assert r["sweeps"] == Hh and r["converged"]
+        np.testing.assert_array_equal(r["V"][0], t[f"V_{tag}"])
+        np.testing.assert_array_equal(r["pi"][0], t[f"pi0_{tag}"])
+        np.testing.assert_array_equal(r["pi_t"][:, 0], t[f"pi_{tag}"])
+        r32 = _solve(cells, model=model, dtype="f32", gamma=g, horizon=Hh)
+        o32 = oracle.value_iteration_ex(int(t["model"]), cells, gamma=g, dtype="f32", horizon=Hh)
+        np.testing.assert_array_equal(r32["V"], o32["V"])
+        np.testing.assert_array_equal(r32["pi"], o32["pi"])
+
+
+def test_finite_horizon_batched_nodeath_slip_vs_oracle():
+    g = load("grids_lava11n5.npz")
+    cells = np.stack([cells_from_enc(e) for e in g["enc"][:16]])
+    for kw in ({}, {"slip_p": 0.9}, {"lava": "nodeath", "death_cost": -0.5}):
+        r = _solve(cells, model="xyd", dtype="f64", gamma=1.0, horizon=484, keep_policy_t=True, **kw)
+        o = oracle.value_iteration_ex(0, cells, gamma=1.0, dtype="f64", horizon=484, keep_policy_t=True,
+                                      slip_p=kw.get("slip_p"), lava_mode=1 if kw.get("lava") else 0,
+                                      death_cost=kw.get("death_cost", -1.0))
+        np.testing.assert_array_equal(r["V"], o["V"])
+        np.testing.assert_array_equal(r["pi_t"], o["pi_t"])
+
+
+@pytest.mark.parametrize("env_id,B", [
+    ("MiniGrid-Empty-5x5-v0", 1),
+    ("MiniGrid-FourRooms-v0", 16),
+    ("MiniGrid-LavaCrossingS9N1-v0", 16),
+    ("MiniGrid-LavaGapS6-v0", 16),
+    ("MiniGrid-DistShift1-v0", 1),
+    ("MiniGrid-DoorKey-5x5-v0", 16),
+])
+def test_finite_horizon_policy_collects_exactly_v0(env_id, B):
+    """Undiscounted finite-horizon DP = the expected env return: executing pi_t (t = step_count)
+    in the step kernel returns exactly V_0[start] in the env's own reward (fp64)."""
+    venv = mg.MiniGridVecEnv(env_id, B)
+    venv.reset(seed=0)
+    st = venv.get_state()
+    enc = st["enc"]
+    model = "doorkey" if "DoorKey" in env_id else "xyd"
+    Hh = venv.max_steps
+    vi = mg.ValueIteration(enc, model=model, gamma=1.0, dtype="f64", horizon=Hh, keep_policy_t=True)
+    vi.solve()
+    res = vi.result()
+    pit = vi.policy_t()
+    vi.close()
+    door = None
+    if model == "doorkey":
+        door = [tuple(np.argwhere(enc[b, :, :, 0] == OBJECT_TO_IDX["door"])[0]) for b in range(B)]
+
+    def state(st, b):
+        x, y, d = (int(v) for v in st["agent"][b])
+        hk = dop = 0
+        if model == "doorkey":
+            hk = int(st["carry"][b, 0] == OBJECT_TO_IDX["key"])
+            dop = int(st["enc"][b, door[b][0], door[b][1], 2] == 0)
+        return mg.dp.state_index(model, venv.W, x, y, d, hk, dop)
+
+    v0 = np.array([res.V[b, state(st, b)] for b in range(B)])
+    ret = np.zeros(B)
+    done = np.zeros(B, bool)
+    for t in range(Hh):
+        acts = []
+        for b in range(B):
+            lane = int(pit[t, b, state(st, b)]) if not done[b] else 6
+            acts.append(mg.dp.DOORKEY_ACTIONS[lane] if (model == "doorkey" and not done[b]) else lane)
+        _, rew, term, trunc, _ = venv.step(np.array(acts))
+        ret[~done] += rew[~done]
+        done |= term | trunc
+        st = venv.get_state()
+        if done.all():
+            break
+    venv.close()
+    assert done.all()
+    np.testing.assert_array_equal(ret, v0)
+    assert (v0 > 0).any()
+
+
+def test_nodeath_wrapper_doctest():
+    """wrappers.py:806-820: LavaCrossingS9N1 seed 2, right then forward into lava: (0, True)
+    unwrapped, (-1.0, False) under NoDeath(("lava",), -1.0); the agent then stands on the lava."""
+    from minigrid_dynamicprogramming_amd.wrappers import NoDeath
+
+    env = mg.make("MiniGrid-LavaCrossingS9N1-v0")
+    env.reset(seed=2)
+    env.step(1)
+    _, reward, term, *_ = env.step(2)
+    assert (reward, term) == (0, True)
+    env = NoDeath(mg.make("MiniGrid-LavaCrossingS9N1-v0"), no_death_types=("lava",), death_cost=-1.0)
+    env.reset(seed=2)
+    env.step(1)
+    _, reward, term, *_ = env.step(2)
+    assert (reward, term) == (-1.0, False)
+    assert env.grid.get(*env.agent_pos).type == "lava"
+    # the NoDeath DP agrees with the wrapper on this transition: entering the lava is worth
+    # death_cost + gamma * V[lava state] (bit-exact with the oracle's table)
+    enc = env.grid.encode()[None]
+    r = _solve(enc, model="xyd", dtype="f64", lava="nodeath", death_cost=-1.0)
+    o = oracle.value_iteration_ex(0, enc[..., 0].transpose(0, 2, 1), dtype="f64", lava_mode=1, death_cost=-1.0)
+    np.testing.assert_array_equal(r["V"], o["V"])
