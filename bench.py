@@ -68,10 +68,11 @@ def make_cells(spec, rank, world):
         enc, _ = env.generate(seed=0)
         one = np.ascontiguousarray(enc[..., 0].T)
         return np.broadcast_to(one, (hi - lo,) + one.shape).copy(), (lo, hi)
-    cells = np.empty((hi - lo, env.height, env.width), np.uint8)
-    for i, s in enumerate(range(lo, hi)):
-        enc, _ = env.generate(seed=s)
-        cells[i] = enc[..., 0].T
+    # reset(seed) for every seed of this rank's shard, generated on the GPU (csrc/gen.hip; pinned
+    # to the reference's grid digests by tests/test_gpu_gen.py); not part of the timed region
+    from minigrid_dynamicprogramming_amd import gen
+
+    cells = gen.generate(env, lo, hi - lo, enc=False, cells=True, agent=False)["cells"]
     return cells, (lo, hi)
 
 

@@ -190,6 +190,36 @@ int mgdp_envs_get_state(mgdp_envs *envs, uint8_t *enc, int32_t *agent, int32_t *
 int mgdp_envs_set_state(mgdp_envs *envs, const int32_t *agent, const int32_t *carry,
                         const int32_t *step_count, const uint8_t *mask);
 
+/* ---------------------------------------------------------------------------------------------- */
+/* Batched reset(seed) grid generation on the GPU.  Env b gets seed seed0 + b */
+/* and the grid/agent reference reset(seed) produces: np_random(seed) = numpy                     */
+/* Generator(PCG64(SeedSequence(seed))) drawn in each family's _gen_grid order (empty.py:97-114,   */
+/* fourrooms.py:79-128, crossing.py:122-184, doorkey.py:75-100, lavagap.py:101-136,               */
+/* distshift.py:99-121; helpers minigrid_env.py:242-390).                                          */
+/* ---------------------------------------------------------------------------------------------- */
+enum {
+    MGDP_GEN_EMPTY = 0, MGDP_GEN_FOURROOMS = 1, MGDP_GEN_CROSSING = 2, MGDP_GEN_DOORKEY = 3,
+    MGDP_GEN_LAVAGAP = 4, MGDP_GEN_DISTSHIFT = 5,
+};
+typedef struct {
+    int32_t family;        /* MGDP_GEN_*                                                           */
+    int32_t W, H;          /* grid size (FourRooms 19; Crossing odd; 5..32)                         */
+    int32_t num_crossings; /* CROSSING                                                             */
+    int32_t obstacle;      /* CROSSING / LAVAGAP: OBJECT_TO_IDX of the obstacle (9 lava, 2 wall)    */
+    int32_t random_start;  /* EMPTY: agent_start_pos=None -> place_agent()                          */
+    int32_t strip2_row;    /* DISTSHIFT                                                            */
+    int32_t reserved;
+} mgdp_gen_desc;
+/* Device buffers (any may be NULL): enc B*W*H*3 uint8 (x-major Grid.encode(): type, colour,
+ * state -- what mgdp_envs_load takes), cells B*H*W uint8 row-major type codes (what
+ * mgdp_vi_load_cells_device takes), agent B*3 int32 (x, y, dir; dir -1 if rejection sampling hit
+ * its cap).  Asynchronous on `stream` (a hipStream_t; NULL = the default stream). */
+int mgdp_gen_grids(const mgdp_gen_desc *desc, int32_t device, void *hip_stream, int64_t seed0, int32_t B,
+                   uint8_t *enc, uint8_t *cells, int32_t *agent);
+/* Same into host buffers (synchronous). */
+int mgdp_gen_grids_host(const mgdp_gen_desc *desc, int32_t device, int64_t seed0, int32_t B, uint8_t *enc,
+                        uint8_t *cells, int32_t *agent);
+
 #ifdef __cplusplus
 }
 #endif

@@ -54,6 +54,11 @@ class ViDesc(ctypes.Structure):
     ]
 
 
+class GenDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in
+                ("family", "W", "H", "num_crossings", "obstacle", "random_start", "strip2_row", "reserved")]
+
+
 # name -> (restype, argtypes); the full export list of include/mgdp.h
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
@@ -84,6 +89,8 @@ SIGNATURES = {
     "mgdp_vi_kernel_time": (ctypes.c_int, [_P, _DP, _I64P]),
     "mgdp_vi_persistent": (ctypes.c_int, [_P, _I32P]),
     "mgdp_vi_get_policy_t": (ctypes.c_int, [_P, _P]),
+    "mgdp_gen_grids": (ctypes.c_int, [ctypes.POINTER(GenDesc), _I32, _P, ctypes.c_int64, _I32, _P, _P, _P]),
+    "mgdp_gen_grids_host": (ctypes.c_int, [ctypes.POINTER(GenDesc), _I32, ctypes.c_int64, _I32, _P, _P, _P]),
     "mgdp_envs_create": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, ctypes.POINTER(_P)]),
     "mgdp_envs_destroy": (ctypes.c_int, [_P]),
     "mgdp_envs_set_stream": (ctypes.c_int, [_P, _P]),

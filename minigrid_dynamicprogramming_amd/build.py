@@ -8,7 +8,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmgdp.so")
-SOURCES = ["lib.cpp", "vi.hip", "envs.hip"]
+SOURCES = ["lib.cpp", "vi.hip", "envs.hip", "gen.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MGDP_ARCH", "gfx950")
 

@@ -11,7 +11,7 @@ import ctypes
 
 import numpy as np
 
-from . import _lib
+from . import _lib, gen
 from .registry import make
 
 
@@ -29,6 +29,8 @@ class MiniGridVecEnv:
         self.num_envs = int(num_envs)
         self.autoreset = autoreset
         self._gen = make(env_id, **kwargs)  # host-side generator (one instance reused per seed)
+        self._gpu_gen = gen.supported(self._gen)  # reset(seed) batches generated on the GPU
+        self.device = device
         self.W, self.H = self._gen.width, self._gen.height
         self.view = self._gen.agent_view_size
         self.max_steps = self._gen.max_steps
@@ -79,6 +81,11 @@ class MiniGridVecEnv:
                                          _lib.ptr(m)), "mgdp_envs_load")
 
     def _generate(self, seeds):
+        seeds = np.asarray(seeds, np.int64)
+        if self._gpu_gen and len(seeds) and (np.diff(seeds) == 1).all():
+            # consecutive seeds: one generator launch (csrc/gen.hip) instead of a host loop
+            out = gen.generate(self._gen, int(seeds[0]), len(seeds), device=self.device)
+            return out["enc"], out["agent"]
         encs, agents = [], []
         for s in seeds:
             e, a = self._gen.generate(seed=int(s))
