@@ -138,12 +138,20 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    # Rehearsal knobs for a 1-GPU box (never set by the driver): MGDP_BENCH_DEVICE pins every rank
+    # to one device, MGDP_BENCH_BACKEND=gloo replaces RCCL (which refuses two ranks per GPU).
+    local = int(os.environ.get("MGDP_BENCH_DEVICE", local))
+    backend = os.environ.get("MGDP_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    red_dev = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
 
     import minigrid_dynamicprogramming_amd as mg
     from minigrid_dynamicprogramming_amd.distributed import solve_sharded
@@ -183,7 +191,7 @@ def main():
     A = 7 if vi.model == "xyd" else 5
     upd_rank = float(vi.updates_per_sweep) * float(sum(sweeps))
     if dist is not None:
-        t = torch.tensor([elapsed, upd_rank], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, upd_rank], dtype=torch.float64, device=red_dev)
         tmax = t[0:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         usum = t[1:2].clone()
