@@ -42,6 +42,7 @@ namespace mgdp {
 
 struct Geo {
     int B, W, H, HW, HWp, S;
+    int HWs, Ss;  // direction-major LDS tiles: cell stride HWs = round_up(HW, 64) (one slot per thread), Ss = S/HW*HWs
     int off[4];  // cell offset of the front cell for dir 0..3 (+x, +y, -x, -y)
     int max_sweeps;
     int nbuf;    // LDS V buffers of the fused kernel: 2, or 3 for the two-sweep XYD step
@@ -657,7 +658,7 @@ __device__ __forceinline__ XydTopo<T> xyd_topo_soa(const uint8_t *cl, const Geo 
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
         const int cell = tp.nbi[d] >> 2;  // cell-major index (cell*4 + d) -> direction-major
-        tp.nbi[d] = d * geo.HW + cell;
+        tp.nbi[d] = d * geo.HWs + cell;
     }
     return tp;
 }
@@ -675,7 +676,7 @@ __device__ __forceinline__ void fused_fast_xyd_soa(const Geo &geo, const Coef<T>
     const int c = threadIdx.x;
     const int cc = c < geo.HW ? c : 0;  // idle threads shadow cell 0 and never write
     const bool own_cell = c < geo.HW;
-    const int HW = geo.HW;
+    const int HW = geo.HWs;  // LDS stride: every thread (idle ones too) owns a slot, so LDS writes need no mask
     const int k_start = k;
     const XydTopo<T> tp = xyd_topo_soa<T, ND>(cl, geo, cc);
     V4<T> own;
@@ -684,10 +685,8 @@ __device__ __forceinline__ void fused_fast_xyd_soa(const Geo &geo, const Coef<T>
     } else {
         own = *reinterpret_cast<const V4<T> *>(Vg + cc * 4);
     }
-    if (own_cell) {
 #pragma unroll
-        for (int d = 0; d < 4; ++d) V0[d * HW + c] = own.v[d];
-    }
+    for (int d = 0; d < 4; ++d) V0[d * HW + c] = own.v[d];
     __syncthreads();
     int cur = 0, parity = 0;
     T diff = (T)0;
@@ -711,10 +710,8 @@ __device__ __forceinline__ void fused_fast_xyd_soa(const Geo &geo, const Coef<T>
         } else {
             diff = xyd_step<T, SLIP, false, ND, HMODE != 0>(tp, cf, in, nbv, out, pk, rg);
         }
-        if (own_cell) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) Vout[q * HW + c] = out.v[q];
-        }
+        for (int q = 0; q < 4; ++q) Vout[q * HW + c] = out.v[q];
         if (LOCAL) flag_write(diff >= cf.tol, flags, parity);
         __syncthreads();
         parity ^= 1;
@@ -750,7 +747,7 @@ __device__ __forceinline__ void fused_fast_xyd_soa(const Geo &geo, const Coef<T>
 __device__ __forceinline__ DkTopo dk_topo_soa(const uint8_t *cl, const Geo &geo, int c) {
     DkTopo tp = dk_topo(cl, geo, c);
 #pragma unroll
-    for (int d = 0; d < 4; ++d) tp.nb[d] = (d * geo.HW + (tp.nb[d] >> 4)) * 4;
+    for (int d = 0; d < 4; ++d) tp.nb[d] = (d * geo.HWs + (tp.nb[d] >> 4)) * 4;
     return tp;
 }
 
@@ -764,7 +761,7 @@ __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> 
     const int c = threadIdx.x;
     const int cc = c < geo.HW ? c : 0;
     const bool own_cell = c < geo.HW;
-    const int HW = geo.HW;
+    const int HW = geo.HWs;  // LDS stride: every thread (idle ones too) owns a slot, so LDS writes need no mask
     const int k_start = k;
     const DkTopo tp = dk_topo_soa(cl, geo, cc);
     T own[16];
@@ -773,7 +770,7 @@ __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> 
         const V4<T> x = k == 0 ? V4<T>{{(T)0, (T)0, (T)0, (T)0}} : *reinterpret_cast<const V4<T> *>(Vg + cc * 16 + 4 * q);
 #pragma unroll
         for (int j = 0; j < 4; ++j) own[4 * q + j] = x.v[j];
-        if (own_cell) *reinterpret_cast<V4<T> *>(V0 + (q * HW + c) * 4) = x;
+        *reinterpret_cast<V4<T> *>(V0 + (q * HW + c) * 4) = x;
     }
     __syncthreads();
     int cur = 0, parity = 0;
@@ -797,12 +794,10 @@ __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> 
         } else {
             diff = dk_step<T, false, HMODE != 0>(tp, cf, in, nbs, outv, pk, rg);
         }
-        if (own_cell) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                *reinterpret_cast<V4<T> *>(Vout + (q * HW + c) * 4) =
-                    V4<T>{{outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]}};
-        }
+        for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<V4<T> *>(Vout + (q * HW + c) * 4) =
+                V4<T>{{outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]}};
         if (LOCAL) flag_write(diff >= cf.tol, flags, parity);
         __syncthreads();
         parity ^= 1;
@@ -1106,7 +1101,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
                                            int k_target, int fresh, bool lone, unsigned int epoch, int e,
                                            int &k, double &dvl) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T), geo.nbuf);
+    const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
     T *V0 = reinterpret_cast<T *>(smem);
     T *V1 = reinterpret_cast<T *>(smem + L.v_bytes);
     int8_t *pis = reinterpret_cast<int8_t *>(smem + L.pi_off());
@@ -1123,8 +1118,9 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     const bool soa = fast && !geo.pair && !geo.quad;
     if (!SERVED) copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
     if (!soa) {
-        if (k == 0) zero16(V0, L.v_bytes);
-        else copy16(V0, V + vb, L.v_bytes);
+        // cell-major paths use the first S entries of each (Ss-sized) tile
+        if (k == 0) zero16(V0, geo.S * (int)sizeof(T));
+        else copy16(V0, V + vb, geo.S * (int)sizeof(T));
     }
     if (threadIdx.x < 64) flags[threadIdx.x] = 0;
     __syncthreads();
@@ -1184,7 +1180,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
             __syncthreads();
         }
     }
-    copy16(V + vb, Vfinal ? Vfinal : (cur ? V1 : V0), L.v_bytes);
+    copy16(V + vb, Vfinal ? Vfinal : (cur ? V1 : V0), geo.S * (int)sizeof(T));
     copy_pi(pi + vb, pis, geo.S);
     if (threadIdx.x == 0) {
         kenv[e] = k;
@@ -1201,7 +1197,7 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
                 unsigned long long *__restrict__ host_out, int k_target, int fresh, int in_kernel_reduce,
                 unsigned int epoch) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T), geo.nbuf);
+    const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
     T *slots = reinterpret_cast<T *>(smem + L.slots_off());
     int k;
     double dvl;
@@ -1230,7 +1226,7 @@ vi_serve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
                 unsigned long long served, unsigned long long idle_ticks, unsigned long long life_ticks) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ unsigned long long s_cmd;
-    const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T), geo.nbuf);
+    const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
     copy16(smem + L.cells_off(), cells, geo.HWp);
     if (threadIdx.x == 0) s_cmd = served;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1281,7 +1277,7 @@ vi_fused_opts_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *
                      unsigned long long *__restrict__ host_out, int k_target, int fresh, int in_kernel_reduce,
                      unsigned int epoch, const T *__restrict__ rgoal, int8_t *__restrict__ pi_t) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const Smem L = smem_layout(geo.S, geo.HWp, (int)sizeof(T), geo.nbuf);
+    const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
     T *V0 = reinterpret_cast<T *>(smem);
     T *V1 = reinterpret_cast<T *>(smem + L.v_bytes);
     uint8_t *cl = reinterpret_cast<uint8_t *>(smem + L.cells_off());
@@ -1440,6 +1436,7 @@ using namespace mgdp;
 struct mgdp_vi {
     mgdp_vi_desc d;
     int S = 0, HW = 0, HWp = 0, A = 0, tsize = 0;
+    int HWs = 0, Ss = 0;  // see Geo
     hipStream_t stream = nullptr;
     bool own_stream = false;
     uint8_t *d_cells = nullptr;
@@ -1498,6 +1495,8 @@ Geo make_geo(const mgdp_vi *vi) {
     g.H = vi->d.H;
     g.HW = vi->HW;
     g.HWp = vi->HWp;
+    g.HWs = vi->HWs;
+    g.Ss = vi->Ss;
     g.S = vi->S;
     g.off[0] = 1;
     g.off[1] = vi->d.W;
@@ -1566,7 +1565,7 @@ int timed_collect(mgdp_vi *vi) {
 template <typename T, int MODEL, bool SLIP, bool ND, int HMODE>
 int launch_opts_t(mgdp_vi *vi, int k_target) {
     const Geo g = make_geo(vi);
-    const Smem L = smem_layout(vi->S, vi->HWp, sizeof(T), vi->nbuf);
+    const Smem L = smem_layout(vi->Ss, vi->HWp, sizeof(T), vi->nbuf);
     auto kern = vi_fused_opts_kernel<T, MODEL, SLIP, ND, HMODE>;
     if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
     TimedPair tp;
@@ -1607,7 +1606,7 @@ template <typename T, int MODEL, bool SLIP, int MAP>
 int launch_fused_t(mgdp_vi *vi, int k_target) {
     if (vi->opts) return launch_opts<T>(vi, k_target);
     const Geo g = make_geo(vi);
-    const Smem L = smem_layout(vi->S, vi->HWp, sizeof(T), vi->nbuf);
+    const Smem L = smem_layout(vi->Ss, vi->HWp, sizeof(T), vi->nbuf);
     auto kern = vi_fused_kernel<T, MODEL, SLIP, MAP>;
     if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
     TimedPair tp;
@@ -1629,7 +1628,7 @@ int launch_fused_t(mgdp_vi *vi, int k_target) {
 template <typename T, int MODEL, bool SLIP, int MAP>
 int launch_serve_t(mgdp_vi *vi, unsigned int served) {
     const Geo g = make_geo(vi);
-    const Smem L = smem_layout(vi->S, vi->HWp, sizeof(T), vi->nbuf);
+    const Smem L = smem_layout(vi->Ss, vi->HWp, sizeof(T), vi->nbuf);
     auto kern = vi_serve_kernel<T, MODEL, SLIP, MAP>;
     if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
     TimedPair tp;
@@ -1898,6 +1897,8 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     vi->HW = d.W * d.H;
     vi->HWp = (int)round_up(vi->HW, 16);
     vi->S = vi->HW * (d.model == MGDP_MODEL_XYD ? 4 : 16);
+    vi->HWs = vi->HW <= 1024 ? (int)round_up(vi->HW, 64) : vi->HW;
+    vi->Ss = vi->S / vi->HW * vi->HWs;
     vi->A = d.model == MGDP_MODEL_XYD ? 7 : 5;
     vi->tsize = d.dtype == MGDP_F32 ? 4 : 8;
     // Two-sweep XYD step (3 LDS buffers): halves the barriers of the fused loop at 1.5x the VALU
@@ -1916,7 +1917,7 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
         if (vi->opts) vi->pair = vi->quad = 0;  // the options kernel runs the direction-major path only
         vi->nbuf = vi->pair ? 3 : 2;
     }
-    const Smem L = smem_layout(vi->S, vi->HWp, vi->tsize, vi->nbuf);
+    const Smem L = smem_layout(vi->Ss, vi->HWp, vi->tsize, vi->nbuf);
     if (L.total() > 160 * 1024) {
         delete vi;
         set_error("grid too large for the LDS-resident kernels (%d B > 160 KiB)", L.total());
