@@ -165,3 +165,30 @@ def test_nodeath_wrapper_doctest():
     r = _solve(enc, model="xyd", dtype="f64", lava="nodeath", death_cost=-1.0)
     o = oracle.value_iteration_ex(0, enc[..., 0].transpose(0, 2, 1), dtype="f64", lava_mode=1, death_cost=-1.0)
     np.testing.assert_array_equal(r["V"], o["V"])
+
+
+def test_option_validation_errors():
+    g = load("grids_lava11n5.npz")
+    cells = np.stack([cells_from_enc(e) for e in g["enc"][:2]])
+    dk = np.stack([cells_from_enc(e) for e in load("grids_doorkey8.npz")["enc"][:2]])
+    bad = [
+        dict(grids=dk, model="doorkey", lava="nodeath"),              # no lava in the DoorKey model
+        dict(grids=cells, model="xyd", horizon=10, method="sweep"),  # options run on the fused path
+        dict(grids=cells, model="xyd", lava="nodeath", mapping="sa"),
+        dict(grids=cells, model="xyd", keep_policy_t=True),          # needs a finite horizon
+        dict(grids=cells, model="xyd", gamma=1.0),                   # gamma = 1 needs a finite horizon
+        dict(grids=cells, model="xyd", horizon=-1),
+        dict(grids=cells, model="xyd", lava="sometimes"),
+    ]
+    for kw in bad:
+        grids = kw.pop("grids")
+        with pytest.raises(ValueError):
+            mg.ValueIteration(grids, **kw)
+    # the multi-device pieces refuse to cut a finite horizon short
+    vi = mg.ValueIteration(cells, model="xyd", horizon=50, gamma=1.0)
+    vi.reset()
+    assert vi.run_local() == 50
+    assert vi.run_to(50) < 1.0
+    with pytest.raises(ValueError):
+        vi.sweep()
+    vi.close()
