@@ -167,6 +167,9 @@ int mgdp_envs_create(int32_t device, int32_t B, int32_t W, int32_t H, int32_t vi
                      mgdp_envs **out);
 int mgdp_envs_destroy(mgdp_envs *envs);
 int mgdp_envs_set_stream(mgdp_envs *envs, void *hip_stream);
+/* NoDeath(env, no_death_types, death_cost) (wrappers.py:799-872) applied inside the step: bit t of
+ * type_mask = OBJECT_TO_IDX type t is a no-death type (goal is refused); 0 = off. */
+int mgdp_envs_set_nodeath(mgdp_envs *envs, uint32_t type_mask, double death_cost);
 /* reset(): upload grids + agent of the envs whose mask byte is 1 (mask NULL = all).
  * enc: B*W*H*3 x-major (Grid.encode()), agent: B*3 (x, y, dir), max_steps: B,
  * see_through: B (see_through_walls, minigrid_env.py:41,103).  step_count and carrying reset to 0. */

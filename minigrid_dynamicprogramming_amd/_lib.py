@@ -94,6 +94,7 @@ SIGNATURES = {
     "mgdp_envs_create": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, ctypes.POINTER(_P)]),
     "mgdp_envs_destroy": (ctypes.c_int, [_P]),
     "mgdp_envs_set_stream": (ctypes.c_int, [_P, _P]),
+    "mgdp_envs_set_nodeath": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.c_double]),
     "mgdp_envs_load": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
     "mgdp_envs_observe": (ctypes.c_int, [_P, _P, _P]),
     "mgdp_envs_step": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P]),

@@ -27,6 +27,8 @@ __constant__ int kDY[4] = {0, 1, 0, -1};
 
 struct EnvGeo {
     int B, W, H, HWp, vs;
+    uint32_t nd_mask;   // NoDeath (wrappers.py:799-872): bit t = OBJECT_TO_IDX type t is a no-death type
+    double death_cost;
 };
 
 constexpr int kStepBlock = 64;  // envs per workgroup; obs staging = 64 * 147 B (16-B multiple)
@@ -185,6 +187,15 @@ envs_step_kernel(EnvGeo g, uint8_t *__restrict__ TY, uint8_t *__restrict__ CO, u
                     }
                 }
                 if (sc >= max_steps[e]) trunc = 1;
+                if (g.nd_mask) {  // NoDeath.step: front cell before, agent's cell after the step
+                    const bool going = a == 2 && !fnone && ((g.nd_mask >> ft) & 1u);
+                    const int ct_now = ty[y * g.W + x];
+                    const bool in_death = ct_now != T_EMPTY && ((g.nd_mask >> ct_now) & 1u);
+                    if (term && (going || in_death)) {
+                        term = 0;
+                        r += g.death_cost;
+                    }
+                }
             }
             agent[e * 4 + 0] = x; agent[e * 4 + 1] = y; agent[e * 4 + 2] = d; agent[e * 4 + 3] = sc;
             carry[e * 2 + 0] = ct; carry[e * 2 + 1] = cc;
@@ -215,11 +226,13 @@ struct mgdp_envs {
             *d_status = nullptr;
     uint8_t *d_obs = nullptr, *d_term = nullptr, *d_trunc = nullptr;
     double *d_rew = nullptr;
+    uint32_t nd_mask = 0;
+    double death_cost = -1.0;
 };
 
 namespace {
 
-EnvGeo env_geo(const mgdp_envs *E) { return EnvGeo{E->B, E->W, E->H, E->HWp, E->vs}; }
+EnvGeo env_geo(const mgdp_envs *E) { return EnvGeo{E->B, E->W, E->H, E->HWp, E->vs, E->nd_mask, E->death_cost}; }
 
 int launch_step(mgdp_envs *E, const int32_t *d_act, uint8_t *d_obs, int32_t *d_dir, double *d_rew,
                 uint8_t *d_term, uint8_t *d_trunc, int32_t *d_status, int observe_only) {
@@ -285,6 +298,15 @@ int mgdp_envs_destroy(mgdp_envs *E) {
     for (void *p : ps) (void)hipFree(p);
     if (E->own_stream) (void)hipStreamDestroy(E->stream);
     delete E;
+    return 0;
+}
+
+int mgdp_envs_set_nodeath(mgdp_envs *E, uint32_t type_mask, double death_cost) {
+    MGDP_CHECK(E, MGDP_E_INVALID, "null handle");
+    MGDP_CHECK(!(type_mask & (1u << T_GOAL)), MGDP_E_INVALID, "goal cannot be a death cell (wrappers.py:845)");
+    MGDP_CHECK(!(type_mask & (1u << T_EMPTY)), MGDP_E_INVALID, "an empty cell is no object");
+    E->nd_mask = type_mask;
+    E->death_cost = death_cost;
     return 0;
 }
 

@@ -24,7 +24,10 @@ class MiniGridVecEnv:
     observation is in info["final_obs_image"]).
     """
 
-    def __init__(self, env_id: str, num_envs: int, device: int = 0, autoreset: bool = False, **kwargs):
+    def __init__(self, env_id: str, num_envs: int, device: int = 0, autoreset: bool = False,
+                 no_death_types: tuple = (), death_cost: float = -1.0, **kwargs):
+        """no_death_types / death_cost: NoDeath(env, no_death_types, death_cost) applied inside the
+        step kernel (wrappers.py:799-872)."""
         self.env_id = env_id
         self.num_envs = int(num_envs)
         self.autoreset = autoreset
@@ -42,6 +45,14 @@ class MiniGridVecEnv:
         _lib.check(self.L.mgdp_envs_create(device, self.num_envs, self.W, self.H, self.view, ctypes.byref(h)),
                    "mgdp_envs_create")
         self.h = h
+        if no_death_types:
+            assert "goal" not in no_death_types, "goal cannot be a death cell"
+            from .core import OBJECT_TO_IDX
+
+            mask = 0
+            for t in no_death_types:
+                mask |= 1 << OBJECT_TO_IDX[t]
+            _lib.check(self.L.mgdp_envs_set_nodeath(h, mask, float(death_cost)), "mgdp_envs_set_nodeath")
         B, V = self.num_envs, self.view
         self._obs = np.zeros((B, V, V, 3), np.uint8)
         self._dir = np.zeros(B, np.int32)

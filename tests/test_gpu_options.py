@@ -192,3 +192,42 @@ def test_option_validation_errors():
     with pytest.raises(ValueError):
         vi.sweep()
     vi.close()
+
+
+def test_nodeath_in_the_batched_step_kernel():
+    """NoDeath applied inside envs_step_kernel == the reference wrapper's logic (front cell before
+    the step, agent cell after it) on top of the oracle's step, over random trajectories; and the
+    wrapper's own doctest (wrappers.py:806-820)."""
+    from oracle.oracle import OracleEnv
+
+    v = mg.MiniGridVecEnv("MiniGrid-LavaCrossingS9N1-v0", 1, no_death_types=("lava",), death_cost=-1.0)
+    v.reset(seed=2)
+    v.step([1])
+    _, rew, term, _, _ = v.step([2])
+    assert (float(rew[0]), bool(term[0])) == (-1.0, False)
+    v.close()
+
+    B, steps, dc = 64, 200, -0.75
+    venv = mg.MiniGridVecEnv("MiniGrid-LavaCrossingS11N5-v0", B, no_death_types=("lava",), death_cost=dc)
+    venv.reset(seed=100)
+    st = venv.get_state()
+    orcs = [OracleEnv(st["enc"][b], st["agent"][b], venv.max_steps, venv.see_through) for b in range(B)]
+    rng = np.random.default_rng(7)
+    LAVA = 9
+    for _ in range(steps):
+        acts = rng.integers(0, 7, B)
+        # bias towards forward so lava gets entered and walked over
+        acts = np.where(rng.random(B) < 0.5, 2, acts)
+        obs, rew, term, trunc, _ = venv.step(acts)
+        for b in range(B):
+            o = orcs[b]
+            x, y, d = (int(t) for t in o.state[:3])
+            fx, fy = x + (1, 0, -1, 0)[d], y + (0, 1, 0, -1)[d]
+            going = acts[b] == 2 and o.ty[fy, fx] == LAVA
+            img, r, te, tr = o.step(int(acts[b]))
+            in_death = o.ty[o.state[1], o.state[0]] == LAVA
+            if te and (going or in_death):
+                te, r = False, r + dc
+            assert (float(rew[b]), bool(term[b]), bool(trunc[b])) == (r, te, tr), b
+            np.testing.assert_array_equal(obs["image"][b], img)
+    venv.close()
