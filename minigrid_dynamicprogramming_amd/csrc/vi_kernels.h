@@ -1,0 +1,340 @@
+// vi_kernels.h -- the value-iteration kernels: fused solve, persistent lone-grid server,
+// options kernel, reduce kernel, per-sweep HBM kernel.
+// Part of the single translation unit vi.hip (included in order: vi_model.h, vi_loops.h,
+// vi_kernels.h); see vi.hip for the DP semantics and the data layout.
+#pragma once
+
+namespace mgdp {
+template <typename T, int MODEL, bool SLIP, int MAP, bool SERVED = false>
+__device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, const uint8_t *__restrict__ cells,
+                                           T *__restrict__ V, int8_t *__restrict__ pi, int32_t *__restrict__ kenv,
+                                           double *__restrict__ dvenv, unsigned long long *__restrict__ host_out,
+                                           int k_target, int fresh, bool lone, unsigned int epoch, int e,
+                                           int &k, double &dvl) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
+    T *V0 = reinterpret_cast<T *>(smem);
+    T *V1 = reinterpret_cast<T *>(smem + L.v_bytes);
+    int8_t *pis = reinterpret_cast<int8_t *>(smem + L.pi_off());
+    uint8_t *cl = reinterpret_cast<uint8_t *>(smem + L.cells_off());
+    T *slots = reinterpret_cast<T *>(smem + L.slots_off());
+    uint8_t *flags = reinterpret_cast<uint8_t *>(smem + L.flags_off());
+
+    k = fresh ? 0 : kenv[e];
+    dvl = fresh ? 0.0 : dvenv[e];
+    const bool work = k_target < 0 ? (!(k > 0 && dvl < geo.tol) && k < geo.max_sweeps) : (k < k_target);
+    if (!work) return false;
+    const long long vb = (long long)e * geo.S;
+    const bool fast = MAP == MGDP_MAP_CELL && geo.HW <= (int)blockDim.x;
+    const bool soa = fast && !geo.pair && !geo.quad;
+    if (!SERVED) copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
+    if (!soa) {
+        // cell-major paths use the first S entries of each (Ss-sized) tile
+        if (k == 0) zero16(V0, geo.S * (int)sizeof(T));
+        else copy16(V0, V + vb, geo.S * (int)sizeof(T));
+    }
+    if (threadIdx.x < 64) flags[threadIdx.x] = 0;
+    __syncthreads();
+
+    int cur = 0, parity = 0;
+    T diff = (T)0;
+    auto done = [&](int kk, double dv) {
+        if (SERVED) {
+            if (threadIdx.x == 0) publish_tagged(host_out, kk, dv, epoch);
+        } else if (lone && threadIdx.x == 0) {
+            publish(host_out, (unsigned long long)kk, (unsigned long long)__double_as_longlong(dv),
+                    (unsigned long long)kk, epoch);
+        }
+    };
+    const T *Vfinal = nullptr;
+    if (soa) {
+        if (MODEL == MGDP_MODEL_XYD) {
+            if (k_target < 0) fused_fast_xyd_soa<T, SLIP, true>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+            else fused_fast_xyd_soa<T, SLIP, false>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+        } else {
+            if (k_target < 0) fused_fast_dk_soa<T, true>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+            else fused_fast_dk_soa<T, false>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+        }
+        if (threadIdx.x == 0) {
+            kenv[e] = k;
+            dvenv[e] = dvl;
+        }
+        return true;  // V and pi were written by their owner threads
+    } else if (fast && MODEL == MGDP_MODEL_XYD && geo.pair) {
+        int vf = 0;
+        if (k_target < 0) fused_fast_xyd2<T, SLIP, true>(geo, cf, cl, V0, pis, slots, flags, k, k_target, vf, dvl, done);
+        else fused_fast_xyd2<T, SLIP, false>(geo, cf, cl, V0, pis, slots, flags, k, k_target, vf, dvl, done);
+        Vfinal = V0 + vf * geo.S;
+    } else if (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL && geo.quad && 4 * geo.HW <= (int)blockDim.x) {
+        if (k_target < 0) fused_quad_xyd<T, SLIP, true>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
+        else fused_quad_xyd<T, SLIP, false>(geo, cf, cl, V0, V1, pis, slots, flags, k, k_target, cur, dvl, done);
+    } else {
+        while (true) {
+            const T *Vin = cur ? V1 : V0;
+            T *Vout = cur ? V0 : V1;
+            diff = sweep_lds<T, MODEL, SLIP, MAP, true, MAP == MGDP_MAP_SA>(geo, cf, cl, Vin, Vout, pis);
+            cur ^= 1;
+            ++k;
+            if (k_target < 0) {
+                const bool more = block_any(diff >= cf.tol, flags, parity);
+                parity ^= 1;
+                if (!more || k >= geo.max_sweeps) break;
+            } else {
+                __syncthreads();
+                if (k >= k_target) break;
+            }
+        }
+        dvl = (double)block_max(diff, slots, 0);
+        done(k, dvl);
+        if (MAP == MGDP_MAP_CELL) {  // pi of the last sweep = argmax on V_{k-1}
+            sweep_lds<T, MODEL, SLIP, MAP, false, true>(geo, cf, cl, cur ? V0 : V1, nullptr, pis);
+            __syncthreads();
+        }
+    }
+    copy16(V + vb, Vfinal ? Vfinal : (cur ? V1 : V0), geo.S * (int)sizeof(T));
+    copy_pi(pi + vb, pis, geo.S);
+    if (threadIdx.x == 0) {
+        kenv[e] = k;
+        dvenv[e] = dvl;
+    }
+    return true;
+}
+
+template <typename T, int MODEL, bool SLIP, int MAP>
+__global__ void __launch_bounds__(1024)
+vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
+                int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
+                unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
+                unsigned long long *__restrict__ host_out, int k_target, int fresh, int in_kernel_reduce,
+                unsigned int epoch) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
+    T *slots = reinterpret_cast<T *>(smem + L.slots_off());
+    int k;
+    double dvl;
+    const bool lone = in_kernel_reduce && gridDim.x == 1;
+    const bool work = fused_grid<T, MODEL, SLIP, MAP>(geo, cf, cells, V, pi, kenv, dvenv, host_out, k_target, fresh,
+                                                      lone, epoch, blockIdx.x, k, dvl);
+    if (in_kernel_reduce) fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16), epoch, work);
+}
+
+// Persistent solver for a lone grid: one workgroup stays resident and serves solve requests posted
+// in host-mapped memory, removing the launch and dispatch latency from every solve.  The cells
+// cannot change while it is resident (every other entry point stops it first), so they are staged
+// in LDS once.  Lane 0 of every wave polls the request word (relaxed system-scope loads, the waves
+// staggered by s_sleep so a new request is seen a fraction of a round trip after it lands) and
+// also watches the LDS word another wave may already have set.  Request r (!= the last served)
+// runs a fresh fused solve whose {k, dV} is published tagged with r.  Every wave leaves on the quit
+// word, after `idle_ticks` without a request or after `life_ticks` in total (s_memrealtime,
+// 100 MHz); the host relaunches the server if a request finds it gone.
+constexpr unsigned long long kServeQuit = ~0ull;
+
+template <typename T, int MODEL, bool SLIP, int MAP>
+__global__ void __launch_bounds__(1024)
+vi_serve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
+                int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
+                unsigned long long *__restrict__ host_out, const unsigned long long *__restrict__ host_cmd,
+                unsigned long long served, unsigned long long idle_ticks, unsigned long long life_ticks) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ unsigned long long s_cmd;
+    const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
+    copy16(smem + L.cells_off(), cells, geo.HWp);
+    if (threadIdx.x == 0) s_cmd = served;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t_last = t_start;
+    __syncthreads();
+    while (true) {
+        if (lane == 0) {
+            for (int i = 0; i < wave; ++i) __builtin_amdgcn_s_sleep(8);  // stagger the pollers
+            while (true) {
+                const unsigned long long cmd = __hip_atomic_load(host_cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (cmd != served) {
+                    __hip_atomic_store(&s_cmd, cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    break;
+                }
+                if (__hip_atomic_load(&s_cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != served) break;
+                const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+                if (now - t_last > idle_ticks || now - t_start > life_ticks) {
+                    __hip_atomic_store(&s_cmd, kServeQuit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        __syncthreads();
+        const unsigned long long cmd = s_cmd;
+        if (cmd == kServeQuit) break;
+        int k;
+        double dvl;
+        if (!fused_grid<T, MODEL, SLIP, MAP, true>(geo, cf, cells, V, pi, kenv, dvenv, host_out, -1, 1, true,
+                                                   (unsigned int)cmd, 0, k, dvl) &&
+            threadIdx.x == 0)
+            publish_tagged(host_out, k, dvl, (unsigned int)cmd);
+        served = cmd;
+        t_last = __builtin_amdgcn_s_memrealtime();
+        __syncthreads();  // every wave is past s_cmd and the LDS tiles before the next request
+    }
+}
+
+// The fused solve with the SURVEY 8(f) item-3 options (ND = NoDeath lava, HMODE = finite horizon
+// 1 / with pi_t 2): one workgroup per grid on the direction-major one-thread-per-cell path only
+// (the host enforces MGDP_MAP_CELL and no pair / quad steps when options are set).
+template <typename T, int MODEL, bool SLIP, bool ND, int HMODE>
+__global__ void __launch_bounds__(1024)
+vi_fused_opts_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
+                     int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
+                     unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
+                     unsigned long long *__restrict__ host_out, int k_target, int fresh, int in_kernel_reduce,
+                     unsigned int epoch, const T *__restrict__ rgoal, int8_t *__restrict__ pi_t) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
+    T *V0 = reinterpret_cast<T *>(smem);
+    T *V1 = reinterpret_cast<T *>(smem + L.v_bytes);
+    uint8_t *cl = reinterpret_cast<uint8_t *>(smem + L.cells_off());
+    T *slots = reinterpret_cast<T *>(smem + L.slots_off());
+    uint8_t *flags = reinterpret_cast<uint8_t *>(smem + L.flags_off());
+    const int e = blockIdx.x;
+    int k = fresh ? 0 : kenv[e];
+    double dvl = fresh ? 0.0 : dvenv[e];
+    const bool work = k_target < 0 ? (!(k > 0 && dvl < geo.tol) && k < geo.max_sweeps) : (k < k_target);
+    const bool lone = in_kernel_reduce && gridDim.x == 1;
+    if (work) {
+        const long long vb = (long long)e * geo.S;
+        copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
+        if (threadIdx.x < 64) flags[threadIdx.x] = 0;
+        __syncthreads();
+        auto done = [&](int kk, double dv) {
+            if (lone && threadIdx.x == 0)
+                publish(host_out, (unsigned long long)kk, (unsigned long long)__double_as_longlong(dv),
+                        (unsigned long long)kk, epoch);
+        };
+        int8_t *pit = HMODE == 2 ? pi_t + vb : nullptr;
+        const long long pstride = (long long)geo.B * geo.S;
+        if constexpr (MODEL == MGDP_MODEL_XYD) {
+            if constexpr (HMODE == 0) {
+                if (k_target < 0)
+                    fused_fast_xyd_soa<T, SLIP, true, ND, HMODE>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb,
+                                                                 k, k_target, dvl, done, rgoal, pit, pstride);
+                else
+                    fused_fast_xyd_soa<T, SLIP, false, ND, HMODE>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb,
+                                                                  k, k_target, dvl, done, rgoal, pit, pstride);
+            } else {  // finite horizon: exactly k_target = H sweeps
+                fused_fast_xyd_soa<T, SLIP, false, ND, HMODE>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb,
+                                                              k, k_target, dvl, done, rgoal, pit, pstride);
+            }
+        } else {
+            if constexpr (HMODE == 0) {
+                if (k_target < 0)
+                    fused_fast_dk_soa<T, true, HMODE>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k,
+                                                      k_target, dvl, done, rgoal, pit, pstride);
+                else
+                    fused_fast_dk_soa<T, false, HMODE>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k,
+                                                       k_target, dvl, done, rgoal, pit, pstride);
+            } else {
+                fused_fast_dk_soa<T, false, HMODE>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k,
+                                                   k_target, dvl, done, rgoal, pit, pstride);
+            }
+        }
+        if (threadIdx.x == 0) {
+            kenv[e] = k;
+            dvenv[e] = dvl;
+        }
+    }
+    if (in_kernel_reduce) fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16), epoch, work);
+}
+
+// Large batches: one workgroup reduces the per-grid (kenv, dvenv) into host-mapped memory (a
+// single arrival ticket shared by tens of thousands of workgroups would serialise on one address).
+__global__ void __launch_bounds__(1024)
+vi_reduce_kernel(const int32_t *__restrict__ kenv, const double *__restrict__ dvenv, int B,
+                 unsigned long long *__restrict__ host_out, unsigned int epoch) {
+    __shared__ unsigned long long sk[16], sd[16], sn[16];
+    unsigned long long km = 0, dm = 0, kn = 0x7fffffffull;
+    for (int i = threadIdx.x; i < B; i += blockDim.x) {
+        const unsigned long long k = (unsigned long long)kenv[i];
+        km = max(km, k);
+        kn = min(kn, k);
+        dm = max(dm, (unsigned long long)__double_as_longlong(dvenv[i]));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        km = max(km, (unsigned long long)__shfl_xor(km, o));
+        dm = max(dm, (unsigned long long)__shfl_xor(dm, o));
+        kn = min(kn, (unsigned long long)__shfl_xor(kn, o));
+    }
+    if ((threadIdx.x & 63) == 0) { sk[threadIdx.x >> 6] = km; sd[threadIdx.x >> 6] = dm; sn[threadIdx.x >> 6] = kn; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < (int)(blockDim.x >> 6); ++i) { km = max(km, sk[i]); dm = max(dm, sd[i]); kn = min(kn, sn[i]); }
+        publish(host_out, km, dm, kn, epoch);
+    }
+}
+
+// Early exit of a speculatively enqueued sweep: the previous sweep already met the rule.
+__device__ __forceinline__ bool prev_sweep_converged(const unsigned long long *shards, int k, double tol) {
+    if (k <= 1) return false;
+    const unsigned long long *prev = shards + (long long)(k - 2) * 8;
+    double m = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m = fmax(m, __longlong_as_double((long long)prev[i]));
+    return m < tol;
+}
+
+// ------------------------------------------------------------------------------------------------
+// One Jacobi sweep (index k, 1-based) of every grid, V double-buffered in HBM.  A workgroup
+// stages a group of `m` consecutive grids (their V rows and cells are contiguous in HBM) into LDS
+// with 16-B loads -- the LDS tile of the neighbourhood --, updates them from LDS and writes the
+// new rows back with 16-B stores; m > 1 keeps more bytes in flight per load phase and amortises
+// the barriers.  check_prev: skip when the previous sweep's global max|dV| was already < tol.
+// POLICY: evaluate only, write pi.
+// ------------------------------------------------------------------------------------------------
+constexpr int kSweepBlock = 256;
+
+__host__ __device__ inline int sweep_smem_bytes(int S, int HWp, int tsize, int m) {
+    return 2 * m * S * tsize + m * ((S + 15) / 16 * 16) + m * HWp + 256;
+}
+
+template <typename T, int MODEL, bool SLIP, int MAP, bool POLICY>
+__global__ void __launch_bounds__(kSweepBlock)
+vi_sweep_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, const T *__restrict__ Vin,
+                T *__restrict__ Vout, int8_t *__restrict__ pi, unsigned long long *__restrict__ shards,
+                int k, int check_prev, int m) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    if (check_prev && prev_sweep_converged(shards, k, geo.tol)) return;
+    const int vbytes = geo.S * (int)sizeof(T), pib = (geo.S + 15) / 16 * 16;
+    T *Vi = reinterpret_cast<T *>(smem);
+    T *Vo = reinterpret_cast<T *>(smem + m * vbytes);
+    int8_t *pis = reinterpret_cast<int8_t *>(smem + 2 * m * vbytes);
+    uint8_t *cl = reinterpret_cast<uint8_t *>(smem + 2 * m * vbytes + m * pib);
+    T *slots = reinterpret_cast<T *>(smem + 2 * m * vbytes + m * pib + m * geo.HWp);
+    const int ngroups = (geo.B + m - 1) / m;
+
+    T acc = (T)0;
+    for (int gidx = blockIdx.x; gidx < ngroups; gidx += gridDim.x) {
+        const int e0 = gidx * m;
+        const int me = min(m, geo.B - e0);
+        const long long vb = (long long)e0 * geo.S;
+        __syncthreads();  // the previous group's LDS tile is no longer read
+        copy16(cl, cells + (long long)e0 * geo.HWp, me * geo.HWp);
+        copy16(Vi, Vin + vb, me * vbytes);
+        __syncthreads();
+        for (int j = 0; j < me; ++j)
+            acc = vmax(acc, sweep_lds<T, MODEL, SLIP, MAP, !POLICY, POLICY || MAP == MGDP_MAP_SA>(
+                                geo, cf, cl + j * geo.HWp, Vi + j * geo.S, Vo + j * geo.S, pis + j * pib));
+        __syncthreads();
+        if (!POLICY) {
+            copy16(Vout + vb, Vo, me * vbytes);
+        } else {
+            for (int j = 0; j < me; ++j) copy_pi(pi + vb + (long long)j * geo.S, pis + j * pib, geo.S);
+        }
+    }
+    if (!POLICY) {
+        const T bdv = block_max(acc, slots, 0);
+        if (threadIdx.x == 0 && shards)
+            atomicMax(shards + (long long)(k - 1) * 8 + (blockIdx.x & 7),
+                      (unsigned long long)__double_as_longlong((double)bdv));
+    }
+}
+
+}  // namespace mgdp

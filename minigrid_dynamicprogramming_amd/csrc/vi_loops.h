@@ -1,0 +1,669 @@
+// vi_loops.h -- the sweep loops of one workgroup: (state, action) lanes, LDS staging,
+// the fused direction-major loops, the two-sweep and four-threads-per-cell XYD loops, the launch
+// reduction and host publication.
+// Part of the single translation unit vi.hip (included in order: vi_model.h, vi_loops.h,
+// vi_kernels.h); see vi.hip for the DP semantics and the data layout.
+#pragma once
+
+namespace mgdp {
+// ------------------------------------------------------------------------------------------------
+// (state, action) lane mapping: 8 lanes per state, lane a evaluates action a, a wave shuffle
+// max-reduce over the 8 lanes keeps the lowest index among exact maxima (numpy argmax rule).
+// ------------------------------------------------------------------------------------------------
+template <typename T, int MODEL, bool SLIP, bool WRITE_V>
+__device__ __forceinline__ T sa_sweep(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
+                                      const T *Vin, T *Vout, int8_t *pis) {
+    const int a = threadIdx.x & 7;
+    const int groups = blockDim.x >> 3;
+    const int S = geo.S;
+    const int bound = (S + groups - 1) / groups * groups;
+    const int A = MODEL == MGDP_MODEL_XYD ? 7 : 5;
+    const T NEG = -INFINITY;
+    T dv = (T)0;
+    for (int s = threadIdx.x >> 3; s < bound; s += groups) {
+        const bool inr = s < S;
+        const int ss = inr ? s : 0;
+        bool valid;
+        T q = NEG;
+        if (MODEL == MGDP_MODEL_XYD) {
+            const int c = ss >> 2, d = ss & 3;
+            valid = inr && xyd_free(cl[c]);
+            if (valid && a < A) {
+                if (a == 0) q = cf.g * Vin[c * 4 + ((d + 3) & 3)];
+                else if (a == 1) q = cf.g * Vin[c * 4 + ((d + 1) & 3)];
+                else if (a == 2) {
+                    const int cfr = c + geo.off[d];
+                    const int tf = cl[cfr];
+                    if (tf == T_GOAL) q = (T)1;
+                    else if (tf == T_LAVA) q = (T)0;
+                    else if (xyd_free(tf)) q = cf.g * Vin[cfr * 4 + d];
+                    else q = cf.g * Vin[ss];
+                } else q = cf.g * Vin[ss];
+            }
+            if (SLIP) {
+                const int base = (threadIdx.x & 63) & ~7;
+                const T q0 = __shfl(q, base + 0), q1 = __shfl(q, base + 1), q2 = __shfl(q, base + 2),
+                        q3 = __shfl(q, base + 3), q4 = __shfl(q, base + 4), q5 = __shfl(q, base + 5);
+                T s6 = q0 + q1;
+                s6 = s6 + q2;
+                s6 = s6 + q3;
+                s6 = s6 + q4;
+                s6 = s6 + q5;
+                if (valid && a < A) q = cf.p * q + cf.c * s6;
+            }
+        } else {
+            const int c = ss >> 4, l = ss & 15, d = l >> 2, hk = (l >> 1) & 1, dop = l & 1;
+            valid = inr && dk_walk(cl[c], hk, dop);
+            if (valid && a < A) {
+                const T *vc = Vin + c * 16;
+                if (a == 0) q = cf.g * vc[(((d + 3) & 3) * 2 + hk) * 2 + dop];
+                else if (a == 1) q = cf.g * vc[(((d + 1) & 3) * 2 + hk) * 2 + dop];
+                else {
+                    const int cfr = c + geo.off[d];
+                    const int tf = cl[cfr];
+                    int tgt = l;  // self loop unless the action changes the state
+                    if (a == 2) {
+                        if (tf == T_GOAL) tgt = -2;
+                        else if (tf == T_LAVA) tgt = -3;
+                        else if (dk_walk(tf, hk, dop)) tgt = -1;
+                    } else if (a == 3) {
+                        if (tf == T_KEY && !hk) tgt = (d * 2 + 1) * 2 + dop;
+                    } else {
+                        if (tf == T_DOOR) {
+                            if (dop) tgt = (d * 2 + hk) * 2 + 0;
+                            else if (hk) tgt = (d * 2 + hk) * 2 + 1;
+                        }
+                    }
+                    if (tgt == -2) q = (T)1;
+                    else if (tgt == -3) q = (T)0;
+                    else if (tgt == -1) q = cf.g * Vin[cfr * 16 + l];
+                    else q = cf.g * vc[tgt];
+                }
+            }
+        }
+        int arg = a;
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+            const T qo = __shfl_xor(q, o);
+            const int ao = __shfl_xor(arg, o);
+            if (qo > q || (qo == q && ao < arg)) { q = qo; arg = ao; }
+        }
+        if (a == 0 && inr) {
+            const T old = Vin[ss];
+            const T nv = valid ? q : (T)0;
+            if (WRITE_V) Vout[ss] = nv;
+            pis[ss] = valid ? (int8_t)arg : (int8_t)-1;
+            dv = vmax(dv, vabs(nv - old));
+        }
+    }
+    return dv;
+}
+
+// Generic LDS sweep over all cells of one grid (topology re-read from LDS each time).
+template <typename T, int MODEL, bool SLIP, int MAP, bool WRITE_V, bool WRITE_PI>
+__device__ __forceinline__ T sweep_lds(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
+                                       const T *Vin, T *Vout, int8_t *pis) {
+    if (MAP == MGDP_MAP_SA) return sa_sweep<T, MODEL, SLIP, WRITE_V>(geo, cf, cl, Vin, Vout, pis);
+    T dv = (T)0;
+    for (int c = threadIdx.x; c < geo.HW; c += blockDim.x) {
+        if (MODEL == MGDP_MODEL_XYD)
+            dv = vmax(dv, xyd_update<T, SLIP, WRITE_V, WRITE_PI>(xyd_topo<T>(cl, geo, c), cf, Vin, Vout, pis, c));
+        else
+            dv = vmax(dv, dk_update<T, WRITE_V, WRITE_PI>(dk_topo(cl, geo, c), cf, Vin, Vout, pis, c));
+    }
+    return dv;
+}
+
+// 16-byte cooperative copies between HBM and LDS (bytes is a multiple of 16).
+__device__ __forceinline__ void copy16(void *dst, const void *src, int bytes) {
+    const uint4 *s = reinterpret_cast<const uint4 *>(src);
+    uint4 *d = reinterpret_cast<uint4 *>(dst);
+    for (int i = threadIdx.x; i < (bytes >> 4); i += blockDim.x) d[i] = s[i];
+}
+__device__ __forceinline__ void zero16(void *dst, int bytes) {
+    uint4 *d = reinterpret_cast<uint4 *>(dst);
+    for (int i = threadIdx.x; i < (bytes >> 4); i += blockDim.x) d[i] = make_uint4(0, 0, 0, 0);
+}
+__device__ __forceinline__ void copy_pi(int8_t *dst, const int8_t *src, int S) {
+    // S is a multiple of 4, so pi rows are 4-byte aligned
+    const uint32_t *s = reinterpret_cast<const uint32_t *>(src);
+    uint32_t *d = reinterpret_cast<uint32_t *>(dst);
+    for (int i = threadIdx.x; i < (S >> 2); i += blockDim.x) d[i] = s[i];
+}
+
+struct Smem {
+    int nbuf, v_bytes, pi_bytes, cells_bytes, slot_bytes;
+    __host__ __device__ int total() const { return nbuf * v_bytes + pi_bytes + cells_bytes + slot_bytes; }
+    __host__ __device__ int pi_off() const { return nbuf * v_bytes; }
+    __host__ __device__ int cells_off() const { return nbuf * v_bytes + pi_bytes; }
+    __host__ __device__ int slots_off() const { return nbuf * v_bytes + pi_bytes + cells_bytes; }
+    __host__ __device__ int flags_off() const { return slots_off() + 256; }
+};
+
+__host__ __device__ inline Smem smem_layout(int S, int HWp, int tsize, int nbuf = 2) {
+    Smem m;
+    m.nbuf = nbuf;
+    m.v_bytes = S * tsize;  // S is a multiple of 4 -> 16-B multiple for f32, f64
+    m.pi_bytes = (S + 15) / 16 * 16;
+    m.cells_bytes = HWp;
+    m.slot_bytes = 256 + 64;  // block_max slots [2][16] x 8 B + convergence flags [2][2][16] B
+    return m;
+}
+
+constexpr int kRedShards = 64;  // fused-launch reduction shards: [64][kmax, dV bits, kmin, -]
+constexpr int kInKernelReduceMaxB = 512;  // above this, a separate one-workgroup reduce kernel
+
+// Fold this block's (k, dV) into the launch reduction.  Every access to the shards and the ticket
+// is an atomic read-modify-write (performed at the device coherence point, never served from a
+// possibly stale per-XCD L2 line), so no cache fences are needed: each block's shard updates
+// return before its ticket add is issued, hence the block that draws the last ticket observes all
+// of them; it combines the shards with exchanges that also re-arm them for the next launch, and
+// publishes {kmax, dV bits, kmin} to host-mapped memory.
+__device__ __forceinline__ void publish(unsigned long long *host_out, unsigned long long km,
+                                        unsigned long long dv, unsigned long long kn, unsigned int epoch) {
+    // The host polls host_out[3]; the three values are acknowledged (vmcnt drained) before the
+    // epoch word is stored, so the host sees them first.  No L2 write-back (release) is needed:
+    // V and pi are consumed only by later stream-ordered operations.
+    __hip_atomic_store(host_out + 0, km, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host_out + 1, dv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host_out + 2, kn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(host_out + 3, (unsigned long long)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Persistent-server result: three 8-byte words, each tagged with the request epoch in its high half
+// ({k}, {dV bits 63..32}, {dV bits 31..0}), so they may land in any order and need no drain between
+// them; the host waits until all three carry its epoch.
+__device__ __forceinline__ void publish_tagged(unsigned long long *host_out, int k, double dv, unsigned int epoch) {
+    const unsigned long long tag = (unsigned long long)epoch << 32;
+    const unsigned long long b = (unsigned long long)__double_as_longlong(dv);
+    __hip_atomic_store(host_out + 5, tag | (unsigned int)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host_out + 6, tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host_out + 7, tag | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void fused_reduce(unsigned long long *red, unsigned int *ticket,
+                                             unsigned long long *host_out, int k, double dvl,
+                                             unsigned int *lds_flag, unsigned int epoch, bool published) {
+    if (gridDim.x == 1) {  // a lone grid publishes directly (early, if it swept: see `done`)
+        if (threadIdx.x == 0 && !published)
+            publish(host_out, (unsigned long long)k, (unsigned long long)__double_as_longlong(dvl),
+                    (unsigned long long)k, epoch);
+        return;
+    }
+    if (threadIdx.x == 0) {
+        unsigned long long *r = red + (blockIdx.x & (kRedShards - 1)) * 4;
+        const unsigned long long a = __hip_atomic_fetch_max(r + 0, (unsigned long long)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long b = __hip_atomic_fetch_max(r + 1, (unsigned long long)__double_as_longlong(dvl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long c = __hip_atomic_fetch_min(r + 2, (unsigned long long)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" :: "v"(a), "v"(b), "v"(c) : "memory");
+        const unsigned int t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *lds_flag = t == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (*lds_flag && threadIdx.x < 64) {
+        unsigned long long *r = red + threadIdx.x * 4;
+        unsigned long long km = __hip_atomic_exchange(r + 0, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long dv = __hip_atomic_exchange(r + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long kn = __hip_atomic_exchange(r + 2, 0x7fffffffull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            km = max(km, (unsigned long long)__shfl_xor(km, o));
+            dv = max(dv, (unsigned long long)__shfl_xor(dv, o));
+            kn = min(kn, (unsigned long long)__shfl_xor(kn, o));
+        }
+        if (threadIdx.x == 0) {
+            __hip_atomic_exchange(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            publish(host_out, km, dv, kn, epoch);
+        }
+    }
+}
+
+// XYD fast path with the LDS V tiles in direction-major (SoA) order, V_d[c] at d*HW + c: the four
+// front-cell reads of a wave are then four unit-stride ds_read_b32 (no bank conflicts; the cell-
+// major order made every read a 4-way conflict), and the cell's own update is four unit-stride
+// writes.  The HBM rows stay in the ABI's cell-major order: each thread loads / stores its own cell's
+// 16 B (V4) directly, and writes its 4 pi lanes directly, so no LDS transposition pass is needed.
+template <typename T, bool ND = false>
+__device__ __forceinline__ XydTopo<T> xyd_topo_soa(const uint8_t *cl, const Geo &geo, int c) {
+    XydTopo<T> tp = xyd_topo<T, ND>(cl, geo, c);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const int cell = tp.nbi[d] >> 2;  // cell-major index (cell*4 + d) -> direction-major
+        tp.nbi[d] = d * geo.HWs + cell;
+    }
+    return tp;
+}
+
+// Options: ND = NoDeath lava; HMODE 1 = finite horizon (k_target = H sweeps,
+// sweep k+1 computes V_{H-k-1} with goal reward rgoal[H-k-1]), 2 = the same keeping pi_t (per-action
+// form every sweep, 4 lanes per cell stored to pit + t*pit_stride).
+template <typename T, bool SLIP, bool LOCAL, bool ND = false, int HMODE = 0, typename Done>
+__device__ __forceinline__ void fused_fast_xyd_soa(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
+                                                   T *V0, T *V1, T *slots, uint8_t *flags,
+                                                   const T *Vg, T *Vg_out, int8_t *pig, int &k,
+                                                   int k_target, double &dvl, const Done &done,
+                                                   const T *rgoal = nullptr, int8_t *pit = nullptr,
+                                                   long long pit_stride = 0) {
+    const int c = threadIdx.x;
+    const int cc = c < geo.HW ? c : 0;  // idle threads shadow cell 0 and never write
+    const bool own_cell = c < geo.HW;
+    const int HW = geo.HWs;  // LDS stride: every thread (idle ones too) owns a slot, so LDS writes need no mask
+    const int k_start = k;
+    const XydTopo<T> tp = xyd_topo_soa<T, ND>(cl, geo, cc);
+    V4<T> own;
+    if (k == 0) {
+        own = V4<T>{{(T)0, (T)0, (T)0, (T)0}};
+    } else {
+        own = *reinterpret_cast<const V4<T> *>(Vg + cc * 4);
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) V0[d * HW + c] = own.v[d];
+    __syncthreads();
+    int cur = 0, parity = 0;
+    T diff = (T)0;
+    // One sweep from Vin to Vout; false = the rule stopped before it.  The ping-pong is unrolled
+    // by two below, so each copy has fixed LDS addresses and a fixed flag parity.  Idle threads
+    // shadow cell 0, so their |dV| equals cell 0's and needs no masking.
+    auto sweep = [&](const T *Vin, T *Vout, const V4<T> &in, V4<T> &out) -> bool {
+        T nbv[4];
+        xyd_load_nb(tp, Vin, nbv);
+        if (LOCAL) {
+            if (k >= geo.max_sweeps) return false;
+            if (k > k_start && !flags_any(flags, parity ^ 1)) return false;
+        } else if (k >= k_target) {
+            return false;
+        }
+        uint32_t pk;
+        const T rg = HMODE ? rgoal[k_target - 1 - k] : (T)1;
+        if (HMODE == 2) {
+            diff = xyd_step<T, SLIP, true, ND, true>(tp, cf, in, nbv, out, pk, rg);
+            if (own_cell) *reinterpret_cast<uint32_t *>(pit + (long long)(k_target - 1 - k) * pit_stride + c * 4) = pk;
+        } else {
+            diff = xyd_step<T, SLIP, false, ND, HMODE != 0>(tp, cf, in, nbv, out, pk, rg);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Vout[q * HW + c] = out.v[q];
+        if (LOCAL) flag_write(diff >= cf.tol, flags, parity);
+        __syncthreads();
+        parity ^= 1;
+        ++k;
+        return true;
+    };
+    V4<T> alt;  // the two register sets alternate with the LDS buffers: no copies between sweeps
+    while (true) {
+        if (!sweep(V0, V1, own, alt)) { cur = 0; break; }
+        if (!sweep(V1, V0, alt, own)) { cur = 1; own = alt; break; }
+    }
+    dvl = (double)block_max(diff, slots, 0);
+    done(k, dvl);
+    if (own_cell) {
+        // pi of the last sweep = argmax on V_{k-1} (buffer cur ^ 1, intact); V_k is `own`
+        const T *Vp = cur ? V0 : V1;
+        V4<T> op;
+        T nbv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) op.v[q] = Vp[q * HW + c];
+        xyd_load_nb(tp, Vp, nbv);
+        V4<T> tmp;
+        uint32_t pk;
+        xyd_step<T, SLIP, true, ND, HMODE != 0>(tp, cf, op, nbv, tmp, pk, HMODE ? rgoal[k_target - k] : (T)1);
+        *reinterpret_cast<uint32_t *>(pig + c * 4) = pk;
+        *reinterpret_cast<V4<T> *>(Vg_out + c * 4) = own;
+    }
+}
+
+// DoorKey fast path with the LDS tiles direction-major: the 4 (has_key, door_open) values of
+// state group (c, d) are the V4 at (d*HW + c)*4, so a wave's front-cell reads and own writes are
+// unit-stride 16-B accesses.  HBM rows stay cell-major (c*16 + d*4 + hk*2 + door_open).
+__device__ __forceinline__ DkTopo dk_topo_soa(const uint8_t *cl, const Geo &geo, int c) {
+    DkTopo tp = dk_topo(cl, geo, c);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) tp.nb[d] = (d * geo.HWs + (tp.nb[d] >> 4)) * 4;
+    return tp;
+}
+
+template <typename T, bool LOCAL, int HMODE = 0, typename Done>  // HMODE: see fused_fast_xyd_soa
+__device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
+                                                  T *V0, T *V1, T *slots, uint8_t *flags,
+                                                  const T *Vg, T *Vg_out, int8_t *pig, int &k,
+                                                  int k_target, double &dvl, const Done &done,
+                                                  const T *rgoal = nullptr, int8_t *pit = nullptr,
+                                                  long long pit_stride = 0) {
+    const int c = threadIdx.x;
+    const int cc = c < geo.HW ? c : 0;
+    const bool own_cell = c < geo.HW;
+    const int HW = geo.HWs;  // LDS stride: every thread (idle ones too) owns a slot, so LDS writes need no mask
+    const int k_start = k;
+    const DkTopo tp = dk_topo_soa(cl, geo, cc);
+    T own[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const V4<T> x = k == 0 ? V4<T>{{(T)0, (T)0, (T)0, (T)0}} : *reinterpret_cast<const V4<T> *>(Vg + cc * 16 + 4 * q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) own[4 * q + j] = x.v[j];
+        *reinterpret_cast<V4<T> *>(V0 + (q * HW + c) * 4) = x;
+    }
+    __syncthreads();
+    int cur = 0, parity = 0;
+    T diff = (T)0;
+    auto sweep = [&](const T *Vin, T *Vout, const T (&in)[16], T (&outv)[16]) -> bool {  // see fused_fast_xyd_soa
+        V4<T> nbs[4];
+        dk_load_nb(tp, Vin, nbs);
+        if (LOCAL) {
+            if (k >= geo.max_sweeps) return false;
+            if (k > k_start && !flags_any(flags, parity ^ 1)) return false;
+        } else if (k >= k_target) {
+            return false;
+        }
+        uint32_t pk[4];
+        const T rg = HMODE ? rgoal[k_target - 1 - k] : (T)1;
+        if (HMODE == 2) {
+            diff = dk_step<T, true, true>(tp, cf, in, nbs, outv, pk, rg);
+            if (own_cell)
+                *reinterpret_cast<uint4 *>(pit + (long long)(k_target - 1 - k) * pit_stride + c * 16) =
+                    make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        } else {
+            diff = dk_step<T, false, HMODE != 0>(tp, cf, in, nbs, outv, pk, rg);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<V4<T> *>(Vout + (q * HW + c) * 4) =
+                V4<T>{{outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]}};
+        if (LOCAL) flag_write(diff >= cf.tol, flags, parity);
+        __syncthreads();
+        parity ^= 1;
+        ++k;
+        return true;
+    };
+    T alt[16];
+    while (true) {
+        if (!sweep(V0, V1, own, alt)) { cur = 0; break; }
+        if (!sweep(V1, V0, alt, own)) {
+            cur = 1;
+#pragma unroll
+            for (int l = 0; l < 16; ++l) own[l] = alt[l];
+            break;
+        }
+    }
+    dvl = (double)block_max(diff, slots, 0);
+    done(k, dvl);
+    if (own_cell) {  // pi on V_{k-1} (buffer cur ^ 1); V_k is `own`
+        const T *Vp = cur ? V0 : V1;
+        T op[16], tmp[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const V4<T> x = *reinterpret_cast<const V4<T> *>(Vp + (q * HW + c) * 4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) op[4 * q + j] = x.v[j];
+        }
+        V4<T> nbs[4];
+        dk_load_nb(tp, Vp, nbs);
+        uint32_t pk[4];
+        dk_step<T, true, HMODE != 0>(tp, cf, op, nbs, tmp, pk, HMODE ? rgoal[k_target - k] : (T)1);
+        *reinterpret_cast<uint4 *>(pig + c * 16) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<V4<T> *>(Vg_out + c * 16 + 4 * q) = V4<T>{{own[4 * q], own[4 * q + 1], own[4 * q + 2], own[4 * q + 3]}};
+    }
+}
+
+// Two-sweep step for the XYD fast path (geo.pair, three LDS buffers).  V_{k+2}[c, d] needs V_{k+1} only at
+// the cell itself and at state (front(c, d), d); the thread recomputes that neighbour state with
+// exactly the neighbour's own operations (bit-identical), so two Jacobi sweeps cost one barrier.
+// Buffers rotate: input X = V_k, outputs Y = V_{k+1}, Z = V_{k+2}; the convergence flags of both
+// sweeps are tested after the barrier, so the stopping sweep (and V_{K-1} for pi) is exact.
+template <typename T>
+struct Xyd2Topo {
+    XydTopo<T> b;
+    uint32_t nfree;   // bit d: the front cell n_d = c + off[d] is free (forward moves there)
+    uint32_t n2term;  // bit d: forward from state (n_d, d) is terminal
+    int nbase[4];     // V index of n_d's 4-state block (own block when not free)
+    int n2i[4];       // V index read by forward from (n_d, d)
+    T n2tq[4];
+};
+
+template <typename T>
+__device__ __forceinline__ Xyd2Topo<T> xyd2_topo(const uint8_t *cl, const Geo &geo, int c) {
+    Xyd2Topo<T> t;
+    t.b = xyd_topo<T>(cl, geo, c);
+    t.nfree = 0;
+    t.n2term = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const int n = c + geo.off[d];
+        const bool nf = t.b.valid && xyd_free(cl[n]);
+        t.nbase[d] = (nf ? n : c) * 4;
+        t.n2i[d] = c * 4 + d;
+        t.n2tq[d] = (T)0;
+        if (nf) {
+            t.nfree |= 1u << d;
+            const int n2 = n + geo.off[d];  // n is free, hence interior
+            const int tf = cl[n2];
+            t.n2i[d] = n * 4 + d;
+            if (tf == T_GOAL) { t.n2term |= 1u << d; t.n2tq[d] = (T)1; }
+            else if (tf == T_LAVA) { t.n2term |= 1u << d; }
+            else if (xyd_free(tf)) t.n2i[d] = n2 * 4 + d;
+        }
+    }
+    return t;
+}
+
+// Value of one XYD state from its four distinct action values (the WRITE_PI = false branch of
+// xyd_step, operation for operation).
+template <typename T, bool SLIP>
+__device__ __forceinline__ T xyd_value(const Coef<T> &cf, T qL, T qR, T qF, T qS) {
+    T a0 = qL, a1 = qR, a2 = qF, a3 = qS;
+    if (SLIP) {
+        T s6 = qL + qR;
+        s6 = s6 + qF;
+        s6 = s6 + qS;
+        s6 = s6 + qS;
+        s6 = s6 + qS;
+        const T tail = cf.c * s6;
+        a0 = cf.p * qL + tail;
+        a1 = cf.p * qR + tail;
+        a2 = cf.p * qF + tail;
+        a3 = cf.p * qS + tail;
+    }
+    return vmax(vmax(a0, a1), vmax(a2, a3));
+}
+
+template <typename T, bool SLIP, bool LOCAL, typename Done>
+__device__ __forceinline__ void fused_fast_xyd2(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
+                                                T *vbase, int8_t *pis, T *slots, uint8_t *flags,
+                                                int &k, int k_target, int &vfinal, double &dvl,
+                                                const Done &done) {
+    // buffer i = vbase + i*S: offsets from the LDS base keep every access a ds_* instruction (a
+    // pointer picked from an array of buffers would degrade to flat loads/stores)
+    auto buf = [&](int i) -> T * { return vbase + i * geo.S; };
+    const int c = threadIdx.x;
+    const int cc = c < geo.HW ? c : 0;
+    const bool own_cell = c < geo.HW;
+    const Xyd2Topo<T> tp = xyd2_topo<T>(cl, geo, cc);
+    const int limit = LOCAL ? geo.max_sweeps : k_target;
+    V4<T> own = *reinterpret_cast<const V4<T> *>(buf(0) + cc * 4);
+    int bx = 0, by = 1, bz = 2, last_n = 0, par = 0;
+    T dA = (T)0, dB = (T)0, dfin = (T)0;
+    int bfin = 0, bprev = 0, kfin = k;
+    while (true) {
+        // speculative loads from the buffer the next step would read
+        const T *X = buf(last_n == 2 ? bz : (last_n == 1 ? by : bx));
+        V4<T> nb4[4];
+        T n2v[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            nb4[d] = *reinterpret_cast<const V4<T> *>(X + tp.nbase[d]);
+            n2v[d] = X[tp.n2i[d]];
+        }
+        if (last_n > 0) {
+            bool stop = false;
+            if (LOCAL && !flags_any(flags + (par ^ 1) * 32, 0)) {  // first sweep of the last step converged
+                stop = true; kfin = k - last_n + 1; bfin = by; bprev = bx; dfin = dA;
+            } else if (LOCAL && last_n == 2 && !flags_any(flags + (par ^ 1) * 32 + 16, 0)) {
+                stop = true; kfin = k; bfin = bz; bprev = by; dfin = dB;
+            } else if (k >= limit) {
+                stop = true; kfin = k;
+                bfin = last_n == 2 ? bz : by;
+                bprev = last_n == 2 ? by : bx;
+                dfin = last_n == 2 ? dB : dA;
+            }
+            if (stop) break;
+            if (last_n == 2) { const int t = bx; bx = bz; bz = by; by = t; }
+            else { const int t = bx; bx = by; by = bz; bz = t; }
+        }
+        const int n = k + 2 <= limit ? 2 : 1;
+        T nbv[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) nbv[d] = ((tp.nfree >> d) & 1u) ? nb4[d].v[d] : own.v[d];
+        V4<T> out1;
+        uint32_t pk;
+        dA = xyd_step<T, SLIP, false>(tp.b, cf, own, nbv, out1, pk);
+        if (own_cell) *reinterpret_cast<V4<T> *>(buf(by) + cc * 4) = out1;
+        else dA = (T)0;
+        if (n == 2) {
+            T nbv2[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const V4<T> &nv = nb4[d];
+                const T qL = cf.g * nv.v[(d + 3) & 3], qR = cf.g * nv.v[(d + 1) & 3], qS = cf.g * nv.v[d];
+                const T qF = ((tp.n2term >> d) & 1u) ? tp.n2tq[d] : cf.g * n2v[d];
+                const T vn = xyd_value<T, SLIP>(cf, qL, qR, qF, qS);  // V_{k+1}[n_d, d]
+                nbv2[d] = ((tp.nfree >> d) & 1u) ? vn : out1.v[d];
+            }
+            V4<T> out2;
+            dB = xyd_step<T, SLIP, false>(tp.b, cf, out1, nbv2, out2, pk);
+            if (own_cell) *reinterpret_cast<V4<T> *>(buf(bz) + cc * 4) = out2;
+            else dB = (T)0;
+            own = out2;
+        } else {
+            own = out1;
+            dB = (T)0;
+        }
+        if (LOCAL) {
+            flag_write(dA >= cf.tol, flags + par * 32, 0);
+            if (n == 2) flag_write(dB >= cf.tol, flags + par * 32 + 16, 0);
+        }
+        __syncthreads();
+        par ^= 1;
+        k += n;
+        last_n = n;
+    }
+    k = kfin;
+    vfinal = bfin;
+    dvl = (double)block_max(dfin, slots, 0);
+    done(k, dvl);
+    if (own_cell) xyd_update<T, SLIP, false, true>(tp.b, cf, buf(bprev), nullptr, pis, cc);  // pi on V_{K-1}
+    __syncthreads();
+}
+
+// DPP quad permutation (lane i of each group of 4 reads lane CTRL[i]); all lanes must be active.
+template <int CTRL>
+__device__ __forceinline__ float quad_perm(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double quad_perm(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+constexpr int kQuadLeft = 0x93;   // lane d reads lane (d+3)&3: the state after turning left
+constexpr int kQuadRight = 0x39;  // lane d reads lane (d+1)&3: the state after turning right
+
+// XYD fused fast path with 4 threads per cell, one per direction (geo.quad): each lane holds its
+// state's V in a register, gets the left/right-turn values from its quad by DPP (no LDS), reads
+// only the forward value from LDS and writes one word.  Shorter dependency chain per sweep than
+// one thread per cell; needs 4*HW <= blockDim.
+template <typename T, bool SLIP, bool LOCAL, typename Done>
+__device__ __forceinline__ void fused_quad_xyd(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *V0,
+                                               T *V1, int8_t *pis, T *slots, uint8_t *flags, int &k,
+                                               int k_target, int &cur, double &dvl, const Done &done) {
+    const int c = threadIdx.x >> 2, d = threadIdx.x & 3;
+    const bool own_cell = c < geo.HW;
+    const int cc = own_cell ? c : 0;
+    const int s = cc * 4 + d;
+    const bool valid = own_cell && xyd_free(cl[cc]);
+    bool term = false;
+    T tq = (T)0;
+    int nbi = s;
+    if (valid) {
+        const int cfr = cc + geo.off[d];
+        const int tf = cl[cfr];
+        if (tf == T_GOAL) { term = true; tq = (T)1; }
+        else if (tf == T_LAVA) { term = true; }
+        else if (xyd_free(tf)) nbi = cfr * 4 + d;
+    }
+    const int k_start = k;
+    int parity = 0;
+    T v = (cur ? V1 : V0)[s];
+    T vprev = v;
+    T diff = (T)0;
+    while (true) {
+        const T *Vin = cur ? V1 : V0;
+        T *Vout = cur ? V0 : V1;
+        const T nb = Vin[nbi];
+        const T vl = quad_perm<kQuadLeft>(v), vr = quad_perm<kQuadRight>(v);
+        const bool stop = LOCAL ? (k >= geo.max_sweeps || (k > k_start && !flags_any(flags, parity ^ 1)))
+                                : k >= k_target;
+        if (stop) break;
+        const T qF = term ? tq : cf.g * nb;
+        T best = xyd_value<T, SLIP>(cf, cf.g * vl, cf.g * vr, qF, cf.g * v);
+        best = valid ? best : (T)0;
+        diff = vabs(best - v);
+        if (own_cell) Vout[s] = best;
+        vprev = v;
+        v = best;
+        if (LOCAL) flag_write(diff >= cf.tol, flags, parity);
+        __syncthreads();
+        parity ^= 1;
+        cur ^= 1;
+        ++k;
+    }
+    dvl = (double)block_max(diff, slots, 0);
+    done(k, dvl);
+    {   // pi of the last sweep: argmax on V_{k-1} (vprev in registers, forward from buffer cur ^ 1)
+        const T *Vp = cur ? V0 : V1;
+        const T nb = Vp[nbi];
+        const T vl = quad_perm<kQuadLeft>(vprev), vr = quad_perm<kQuadRight>(vprev);
+        const T qL = cf.g * vl, qR = cf.g * vr, qS = cf.g * vprev, qF = term ? tq : cf.g * nb;
+        T a0 = qL, a1 = qR, a2 = qF, a3 = qS;
+        if (SLIP) {
+            T s6 = qL + qR;
+            s6 = s6 + qF;
+            s6 = s6 + qS;
+            s6 = s6 + qS;
+            s6 = s6 + qS;
+            const T tail = cf.c * s6;
+            a0 = cf.p * qL + tail;
+            a1 = cf.p * qR + tail;
+            a2 = cf.p * qF + tail;
+            a3 = cf.p * qS + tail;
+        }
+        int arg = 0;
+        T best = a0;
+        if (a1 > best) { best = a1; arg = 1; }
+        if (a2 > best) { best = a2; arg = 2; }
+        if (a3 > best) { best = a3; arg = 3; }
+        if (own_cell) pis[s] = valid ? (int8_t)arg : (int8_t)-1;
+    }
+    __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fused solve: blockIdx.x = grid index; the grid's cells, both V buffers and pi stay in LDS for
+// every sweep of the launch.  k_target < 0: sweep until this grid's own max|dV| < tol (or
+// max_sweeps); k_target >= 0: sweep until exactly k_target sweeps are done.  fresh: start from
+// V_0 = 0 regardless of kenv/dvenv.  MAP_CELL with HW <= blockDim keeps each thread's cell
+// topology in registers for the whole launch (no LDS cell reads inside the sweep loop).
+// Sweeps are value-only (max, no argmax); the per-sweep convergence test is a block OR of
+// (|dV| >= tol) (ballot + one byte per wave, one barrier); after the loop the exact max |dV| is
+// reduced once and pi is extracted once from V_{k-1} (exactly what sweep k's argmax would give).
+// ------------------------------------------------------------------------------------------------
+// The whole fused solve of grid e by one workgroup: stage cells (and V unless fresh) in LDS, sweep
+// to the local stopping rule (k_target < 0) or to k_target, extract pi, write V / pi / (k, dV) back.
+// `lone`: this workgroup is the only one of the solve and publishes {k, dV} to the host as soon as
+// they are known (pi extraction and the write-back then overlap the host's reaction); `served`:
+// it does so in the persistent server's tagged form, and the cells are already staged in LDS.
+}  // namespace mgdp
