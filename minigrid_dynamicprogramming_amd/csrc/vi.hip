@@ -88,6 +88,7 @@ struct mgdp_vi {
     int nbuf = 2;                 // fused LDS V buffers (3 = two-sweep XYD step)
     int quad = 0;                 // fused XYD: 4 threads per cell
     int pair = 0;                 // fused XYD: two-sweep step
+    int wave_p = 0;               // lone XYD grid on one wave: cells per lane (fused_wave_xyd)
     int sweep_block = 256;
     int sweep_m = 1;              // grids staged per workgroup iteration (measured: m>1 no faster)
     // SURVEY 8(f) item-3 options (NoDeath lava, finite horizon): vi_fused_opts_kernel
@@ -220,12 +221,31 @@ int launch_opts(mgdp_vi *vi, int k_target) {
               : launch_opts_h<T, MGDP_MODEL_XYD, false, false>(vi, k_target);
 }
 
+// Kernel variant: the one-wave lone-grid instantiation when vi->wave_p is set (XYD, cell mapping).
+template <template <typename, int, bool, int, int> class K, typename T, int MODEL, bool SLIP, int MAP>
+auto pick_wave(const mgdp_vi *vi) -> decltype(K<T, MODEL, SLIP, MAP, 0>::fn) {
+    if constexpr (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL) {
+        switch (vi->wave_p) {
+        case 1: return K<T, MODEL, SLIP, MAP, 1>::fn;
+        case 2: return K<T, MODEL, SLIP, MAP, 2>::fn;
+        case 4: return K<T, MODEL, SLIP, MAP, 4>::fn;
+        case 8: return K<T, MODEL, SLIP, MAP, 8>::fn;
+        default: break;
+        }
+    }
+    return K<T, MODEL, SLIP, MAP, 0>::fn;
+}
+template <typename T, int MODEL, bool SLIP, int MAP, int WP>
+struct FusedK { static constexpr auto fn = vi_fused_kernel<T, MODEL, SLIP, MAP, WP>; };
+template <typename T, int MODEL, bool SLIP, int MAP, int WP>
+struct ServeK { static constexpr auto fn = vi_serve_kernel<T, MODEL, SLIP, MAP, WP>; };
+
 template <typename T, int MODEL, bool SLIP, int MAP>
 int launch_fused_t(mgdp_vi *vi, int k_target) {
     if (vi->opts) return launch_opts<T>(vi, k_target);
     const Geo g = make_geo(vi);
     const Smem L = smem_layout(vi->Ss, vi->HWp, sizeof(T), vi->nbuf);
-    auto kern = vi_fused_kernel<T, MODEL, SLIP, MAP>;
+    auto kern = pick_wave<FusedK, T, MODEL, SLIP, MAP>(vi);
     if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
     TimedPair tp;
     if (int rc = timed_begin(vi, -1, &tp)) return rc;
@@ -247,7 +267,7 @@ template <typename T, int MODEL, bool SLIP, int MAP>
 int launch_serve_t(mgdp_vi *vi, unsigned int served) {
     const Geo g = make_geo(vi);
     const Smem L = smem_layout(vi->Ss, vi->HWp, sizeof(T), vi->nbuf);
-    auto kern = vi_serve_kernel<T, MODEL, SLIP, MAP>;
+    auto kern = pick_wave<ServeK, T, MODEL, SLIP, MAP>(vi);
     if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
     TimedPair tp;
     if (int rc = timed_begin(vi, -1, &tp)) return rc;
@@ -369,7 +389,7 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
 // Persistent solver hand-off (lone grid on the one-thread-per-cell fused path).
 bool serve_eligible(const mgdp_vi *vi) {
     return vi->persistent && !vi->opts && vi->d.method == MGDP_METHOD_FUSED && vi->d.B == 1 && vi->d.mapping == MGDP_MAP_CELL &&
-           vi->HW <= vi->fused_block && !vi->pair && !vi->quad;
+           (vi->HW <= vi->fused_block || vi->wave_p) && !vi->pair && !vi->quad;
 }
 // Ask a resident server to leave and drain the stream.  Every entry point that enqueues other
 // work on the stream, or reads results, calls this first.
@@ -545,6 +565,22 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     // grid has <= 1024 cells; MAP_SA: 8 lanes per state, a lone grid gets the widest workgroup.
     if (d.mapping == MGDP_MAP_CELL) {
         vi->fused_block = (int)std::min<int64_t>(1024, round_up(vi->HW * (vi->quad ? 4 : 1), 64));
+        // A lone XYD grid of <= 64*MGDP_WAVE cells runs on ONE wave, P = 1, 2, 4 or 8 cells per
+        // lane: no workgroup barrier per sweep, the stopping rule is a wave ballot.  Measured per
+        // sweep against the multi-wave loop: P = 1 faster (0.10 vs 0.12 us), P = 2 even, P = 4 and 8
+        // slower (0.27 vs 0.17, 0.55 vs 0.18 us: one SIMD issues every cell's VALU work), so the
+        // default is P = 1 (grids of <= 64 cells); MGDP_WAVE=8 enables the rest (tests cover them).
+        int wave_max = 1;
+        if (const char *ev = std::getenv("MGDP_WAVE")) wave_max = std::atoi(ev);
+        if (d.B == 1 && d.model == MGDP_MODEL_XYD && d.method == MGDP_METHOD_FUSED && !vi->pair && !vi->quad &&
+            !vi->opts && vi->HW <= 64 * std::min(wave_max, 8)) {
+            int P = 1;
+            while (64 * P < vi->HW) P *= 2;
+            vi->wave_p = P;
+            vi->HWs = 64 * P;
+            vi->Ss = vi->S / vi->HW * vi->HWs;
+            vi->fused_block = 64;
+        }
     } else {
         int blk = d.B == 1 ? 1024 : 256;
         while (blk > 64 && blk / 2 >= vi->S * 8) blk /= 2;

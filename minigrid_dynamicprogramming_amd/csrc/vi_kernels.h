@@ -5,7 +5,7 @@
 #pragma once
 
 namespace mgdp {
-template <typename T, int MODEL, bool SLIP, int MAP, bool SERVED = false>
+template <typename T, int MODEL, bool SLIP, int MAP, bool SERVED = false, int WP = 0>
 __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, const uint8_t *__restrict__ cells,
                                            T *__restrict__ V, int8_t *__restrict__ pi, int32_t *__restrict__ kenv,
                                            double *__restrict__ dvenv, unsigned long long *__restrict__ host_out,
@@ -47,6 +47,18 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
         }
     };
     const T *Vfinal = nullptr;
+    if constexpr (WP > 0) {  // lone XYD grid on one wave, WP cells per lane (host: B == 1, blockDim 64)
+        static_assert(MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL, "one-wave path is XYD, cell mapping");
+        if (SERVED || k_target < 0)
+            fused_wave_xyd<T, SLIP, true, WP>(geo, cf, cl, V0, V1, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+        else
+            fused_wave_xyd<T, SLIP, false, WP>(geo, cf, cl, V0, V1, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+        if (threadIdx.x == 0) {
+            kenv[e] = k;
+            dvenv[e] = dvl;
+        }
+        return true;
+    }
     if (soa) {
         if (MODEL == MGDP_MODEL_XYD) {
             if (k_target < 0) fused_fast_xyd_soa<T, SLIP, true>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
@@ -100,8 +112,10 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     return true;
 }
 
-template <typename T, int MODEL, bool SLIP, int MAP>
-__global__ void __launch_bounds__(1024)
+// WP > 0: the one-wave lone-grid variant (fused_wave_xyd), 64 threads, so its WP cells per lane
+// may use the whole register file.
+template <typename T, int MODEL, bool SLIP, int MAP, int WP = 0>
+__global__ void __launch_bounds__(WP ? 64 : 1024)
 vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
@@ -113,8 +127,8 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
     int k;
     double dvl;
     const bool lone = in_kernel_reduce && gridDim.x == 1;
-    const bool work = fused_grid<T, MODEL, SLIP, MAP>(geo, cf, cells, V, pi, kenv, dvenv, host_out, k_target, fresh,
-                                                      lone, epoch, blockIdx.x, k, dvl);
+    const bool work = fused_grid<T, MODEL, SLIP, MAP, false, WP>(geo, cf, cells, V, pi, kenv, dvenv, host_out, k_target,
+                                                                 fresh, lone, epoch, blockIdx.x, k, dvl);
     if (in_kernel_reduce) fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16), epoch, work);
 }
 
@@ -129,8 +143,8 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
 // 100 MHz); the host relaunches the server if a request finds it gone.
 constexpr unsigned long long kServeQuit = ~0ull;
 
-template <typename T, int MODEL, bool SLIP, int MAP>
-__global__ void __launch_bounds__(1024)
+template <typename T, int MODEL, bool SLIP, int MAP, int WP = 0>
+__global__ void __launch_bounds__(WP ? 64 : 1024)
 vi_serve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ host_out, const unsigned long long *__restrict__ host_cmd,
@@ -167,7 +181,7 @@ vi_serve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
         if (cmd == kServeQuit) break;
         int k;
         double dvl;
-        if (!fused_grid<T, MODEL, SLIP, MAP, true>(geo, cf, cells, V, pi, kenv, dvenv, host_out, -1, 1, true,
+        if (!fused_grid<T, MODEL, SLIP, MAP, true, WP>(geo, cf, cells, V, pi, kenv, dvenv, host_out, -1, 1, true,
                                                    (unsigned int)cmd, 0, k, dvl) &&
             threadIdx.x == 0)
             publish_tagged(host_out, k, dvl, (unsigned int)cmd);

@@ -313,6 +313,88 @@ __device__ __forceinline__ void fused_fast_xyd_soa(const Geo &geo, const Coef<T>
     }
 }
 
+// Lone XYD grid on ONE wave, P cells per lane (cell j*64 + lane, same direction-major tiles with
+// HWs = 64*P).  A wave's LDS instructions execute in issue order, so the writes of sweep k are
+// seen by the reads of sweep k+1 without a workgroup barrier, and the stopping rule is the wave's
+// ballot -- no flag round trip through LDS.  The compiler fence keeps the program order of the
+// two sweeps' LDS accesses (cross-lane dependencies it cannot see).  Same arithmetic, same rule
+// and same final pi pass as fused_fast_xyd_soa.
+template <typename T, bool SLIP, bool LOCAL, int P, typename Done>
+__device__ __forceinline__ void fused_wave_xyd(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *V0, T *V1,
+                                               const T *Vg, T *Vg_out, int8_t *pig, int &k, int k_target,
+                                               double &dvl, const Done &done) {
+    const int lane = threadIdx.x;
+    const int HW = geo.HWs;
+    const int k_start = k;
+    XydTopo<T> tp[P];
+    V4<T> own[P], alt[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const int c = j * 64 + lane;
+        const int cc = c < geo.HW ? c : 0;  // idle slots shadow cell 0 and never write HBM
+        tp[j] = xyd_topo_soa<T>(cl, geo, cc);
+        if (k == 0) own[j] = V4<T>{{(T)0, (T)0, (T)0, (T)0}};
+        else own[j] = *reinterpret_cast<const V4<T> *>(Vg + cc * 4);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) V0[d * HW + c] = own[j].v[d];
+    }
+    asm volatile("" ::: "memory");
+    bool more = true;
+    T diff = (T)0;
+    auto sweep = [&](const T *Vin, T *Vout, const V4<T> (&in)[P], V4<T> (&out)[P]) -> bool {
+        T nbv[P][4];
+#pragma unroll
+        for (int j = 0; j < P; ++j) xyd_load_nb(tp[j], Vin, nbv[j]);
+        if (LOCAL) {
+            if (k >= geo.max_sweeps) return false;
+            if (k > k_start && !more) return false;
+        } else if (k >= k_target) {
+            return false;
+        }
+        T dm = (T)0;
+        uint32_t pk;
+#pragma unroll
+        for (int j = 0; j < P; ++j) dm = vmax(dm, xyd_step<T, SLIP, false>(tp[j], cf, in[j], nbv[j], out[j], pk));
+#pragma unroll
+        for (int j = 0; j < P; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) Vout[q * HW + j * 64 + lane] = out[j].v[q];
+        asm volatile("" ::: "memory");
+        diff = dm;
+        if (LOCAL) more = __ballot(dm >= cf.tol) != 0ull;
+        ++k;
+        return true;
+    };
+    int cur;
+    while (true) {
+        if (!sweep(V0, V1, own, alt)) { cur = 0; break; }
+        if (!sweep(V1, V0, alt, own)) {
+            cur = 1;
+#pragma unroll
+            for (int j = 0; j < P; ++j) own[j] = alt[j];
+            break;
+        }
+    }
+    dvl = (double)wave_max(diff);
+    done(k, dvl);
+    const T *Vp = cur ? V0 : V1;  // V_{k-1}: pi of the last sweep is the argmax on it
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const int c = j * 64 + lane;
+        if (c < geo.HW) {
+            V4<T> op, tmp;
+            T nbv[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) op.v[q] = Vp[q * HW + c];
+            xyd_load_nb(tp[j], Vp, nbv);
+            uint32_t pk;
+            xyd_step<T, SLIP, true>(tp[j], cf, op, nbv, tmp, pk);
+            *reinterpret_cast<uint32_t *>(pig + c * 4) = pk;
+            *reinterpret_cast<V4<T> *>(Vg_out + c * 4) = own[j];
+        }
+    }
+}
+
 // DoorKey fast path with the LDS tiles direction-major: the 4 (has_key, door_open) values of
 // state group (c, d) are the V4 at (d*HW + c)*4, so a wave's front-cell reads and own writes are
 // unit-stride 16-B accesses.  HBM rows stay cell-major (c*16 + d*4 + hk*2 + door_open).

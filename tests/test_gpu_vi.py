@@ -309,3 +309,54 @@ def test_tolerance_threshold_edges(dtype):
                 o = oracle.value_iteration(0, sub, slip_p=0.9, dtype=dtype, tol=tol)
                 assert r.sweeps == o["sweeps"]
                 np.testing.assert_array_equal(r.V, o["V"])
+
+
+def _random_xyd_grid(rng, W, H):
+    """Closed-border grid with random walls / lava / floor and one goal (XYD cell types)."""
+    c = rng.choice(np.array([1, 1, 1, 1, 1, 2, 3, 9], np.uint8), size=(H, W))
+    c[0, :] = c[-1, :] = 2
+    c[:, 0] = c[:, -1] = 2
+    c[rng.integers(1, H - 1), rng.integers(1, W - 1)] = 8
+    return c
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_one_wave_lone_grid_sizes(dtype, monkeypatch):
+    """Lone XYD grids of <= 512 cells run on one wave with P = 1, 2, 4, 8 cells per lane
+    (fused_wave_xyd): bit-exact vs the oracle and vs the multi-wave loop (MGDP_WAVE=0) at sizes
+    on both sides of every P boundary, with slip, max_sweeps caps, one-sweep-at-a-time
+    continuation (k > 0 restarts from V in HBM) and the persistent server."""
+    rng = np.random.default_rng(7)
+    sizes = [(5, 5), (8, 8), (9, 8), (11, 11), (16, 8), (16, 16), (17, 16), (19, 19), (22, 22), (23, 23)]
+    for W, H in sizes:
+        cells = _random_xyd_grid(rng, W, H)[None]
+        for slip in (None, 0.9):
+            o = oracle.value_iteration(0, cells, slip_p=slip, dtype=dtype)
+            got = {}
+            for wave, pers in (("8", "1"), ("8", "0"), ("0", "1"), ("1", "1")):
+                monkeypatch.setenv("MGDP_WAVE", wave)
+                monkeypatch.setenv("MGDP_PERSISTENT", pers)
+                r = gpu_vi(cells, "xyd", dtype, "fused", "cell", slip=slip)
+                assert r.sweeps == o["sweeps"], (W, H, slip, wave, pers)
+                np.testing.assert_array_equal(r.V, o["V"])
+                np.testing.assert_array_equal(r.pi, o["pi"])
+                got[(wave, pers)] = r
+        monkeypatch.setenv("MGDP_WAVE", "8")
+        for pers in ("0", "1"):
+            monkeypatch.setenv("MGDP_PERSISTENT", pers)
+            for ms in (1, 2, 5):
+                r = gpu_vi(cells, "xyd", dtype, "fused", "cell", max_sweeps=ms)
+                o = oracle.value_iteration(0, cells, dtype=dtype, max_sweeps=ms)
+                assert r.sweeps == o["sweeps"]
+                np.testing.assert_array_equal(r.V, o["V"])
+                np.testing.assert_array_equal(r.pi, o["pi"])
+        vi = mg.ValueIteration(cells, dtype=dtype)
+        vi.reset()
+        vi.run_to(1)  # fresh, non-local loop to k = 1
+        vi.sweep()    # continuations: k = 1 -> 2 -> 3 from V in HBM
+        vi.sweep()
+        vi.finish(3, 0.0)
+        o = oracle.value_iteration(0, cells, dtype=dtype, max_sweeps=3)
+        np.testing.assert_array_equal(vi.values(), o["V"])
+        np.testing.assert_array_equal(vi.policy(), o["pi"])
+        vi.close()
