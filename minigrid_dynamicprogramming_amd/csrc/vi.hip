@@ -91,6 +91,8 @@ struct mgdp_vi {
     int wave_p = 0;               // lone XYD grid on one wave: cells per lane (fused_wave_xyd)
     int sweep_block = 256;
     int sweep_m = 1;              // grids staged per workgroup iteration (measured: m>1 no faster)
+    int sweep_pipe = 2;           // register-pipelined sweep kernel: grids fetched ahead (0 = staged kernel)
+    int pipe_grid = 0;            // its grid: resident workgroups (set at the first launch)
     // SURVEY 8(f) item-3 options (NoDeath lava, finite horizon): vi_fused_opts_kernel
     bool opts = false;
     void *d_rgoal = nullptr;      // T[H]: the exact _reward() of step_count t+1, per t
@@ -293,6 +295,25 @@ int launch_sweep_kernel(mgdp_vi *vi, const T *Vin, T *Vout, int k, int check_pre
     return 0;
 }
 
+template <typename T, int MODEL, bool SLIP, int DEPTH>
+int launch_sweep_pipe(mgdp_vi *vi, const T *Vin, T *Vout, int k, int check_prev, TimedPair tp) {
+    const int smem = sweep_pipe_smem_bytes(vi->S, vi->HW, vi->HWs, vi->HWp, sizeof(T));
+    auto kern = vi_sweep_pipe_kernel<T, MODEL, SLIP, DEPTH>;
+    if (smem > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
+    if (vi->pipe_grid == 0) {  // every workgroup resident at once: grid = resident blocks per CU x CUs
+        int per_cu = 0, cus = 0;
+        MGDP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)kern, vi->HWs, smem));
+        MGDP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, vi->d.device));
+        vi->pipe_grid = std::max(1, per_cu) * std::max(1, cus);
+        if (const char *ev = std::getenv("MGDP_SWEEP_GRID")) vi->pipe_grid = std::max(1, std::atoi(ev));
+    }
+    const int grid = std::min(vi->d.B, vi->pipe_grid);
+    hipExtLaunchKernelGGL(kern, dim3(grid), dim3(vi->HWs), smem, vi->stream, tp.a, tp.b, 0, make_geo(vi), make_coef<T>(vi),
+                          vi->d_cells, Vin, Vout, vi->d_shards, k, check_prev);
+    MGDP_HIP(hipGetLastError());
+    return 0;
+}
+
 template <typename T, int MODEL, bool SLIP, int MAP>
 int launch_sweep_t(mgdp_vi *vi, int k, int check_prev, bool policy) {
     const T *Vin = (const T *)vi->d_V[(k - 1) & 1];
@@ -300,6 +321,10 @@ int launch_sweep_t(mgdp_vi *vi, int k, int check_prev, bool policy) {
     if (policy) return launch_sweep_kernel<T, MODEL, SLIP, MAP, true>(vi, Vin, Vout, k, 0);
     TimedPair tp;
     if (int rc = timed_begin(vi, k, &tp)) return rc;
+    if constexpr (MAP == MGDP_MAP_CELL) {
+        if (vi->sweep_pipe == 1) return launch_sweep_pipe<T, MODEL, SLIP, 1>(vi, Vin, Vout, k, check_prev, tp);
+        if (vi->sweep_pipe == 2) return launch_sweep_pipe<T, MODEL, SLIP, 2>(vi, Vin, Vout, k, check_prev, tp);
+    }
     return launch_sweep_kernel<T, MODEL, SLIP, MAP, false>(vi, Vin, Vout, k, check_prev, tp);
 }
 
@@ -625,6 +650,14 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     if (const char *ev = std::getenv("MGDP_SWEEP_GRID")) vi->sweep_grid = std::max(1, std::atoi(ev));
     if (const char *ev = std::getenv("MGDP_SWEEP_BLOCK")) vi->sweep_block = std::min(256, std::max(64, std::atoi(ev) / 64 * 64));
     if (const char *ev = std::getenv("MGDP_PERSISTENT")) vi->persistent = std::atoi(ev) != 0;
+    // DoorKey (64-128 B of V per thread) measured slower on the register pipeline (5.38 -> 3.3 TB/s
+    // compulsory: the prefetch registers collide with the 16-state backup's), so it keeps the
+    // staged kernel unless MGDP_SWEEP_PIPE asks otherwise.
+    if (d.model == MGDP_MODEL_DOORKEY) vi->sweep_pipe = 0;
+    if (const char *ev = std::getenv("MGDP_SWEEP_PIPE")) vi->sweep_pipe = std::min(2, std::max(0, std::atoi(ev)));
+    if (vi->HW > 1024 || d.mapping != MGDP_MAP_CELL ||
+        sweep_pipe_smem_bytes(vi->S, vi->HW, vi->HWs, vi->HWp, vi->tsize) > 160 * 1024)
+        vi->sweep_pipe = 0;  // one thread per cell: grids of <= 1024 cells
     if (const char *ev = std::getenv("MGDP_SERVE_IDLE_US"))  // s_memrealtime ticks at 100 MHz
         vi->serve_idle_ticks = (unsigned long long)std::max(1LL, std::atoll(ev)) * 100ull;
     if (const char *ev = std::getenv("MGDP_SERVE_LIFE_US"))

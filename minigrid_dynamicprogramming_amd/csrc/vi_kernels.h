@@ -351,4 +351,129 @@ vi_sweep_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, const T 
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Register-pipelined HBM sweep (one thread per cell, HW <= blockDim = HWs): a workgroup walks its
+// grids e = blockIdx.x + i*gridDim.x.  Each thread loads its own cell's V row (16 B XYD, 64 B
+// DoorKey fp32, coalesced) and a dword of cell bytes DEPTH grids ahead into registers, so the HBM
+// reads of the next grids are in flight while the current one is computed and stored; at the top
+// of an iteration the registers are written to the direction-major LDS tile (the neighbourhood
+// the front-cell reads need, bank-conflict free), the thread keeps its own values in registers and
+// stores its new row straight to HBM.  LDS is only the neighbour exchange: no output staging.
+// Same backups and |dV| as vi_sweep_kernel (bit-identical); pi stays with vi_sweep_kernel<POLICY>.
+// ------------------------------------------------------------------------------------------------
+template <typename T, int MODEL>
+struct PipeRow {
+    static constexpr int NV = MODEL == MGDP_MODEL_XYD ? 1 : 4;  // V4 per cell
+    V4<T> v[NV];
+    uint32_t cw;  // cell bytes 4c .. 4c+3 (threads c < HWp/4)
+};
+
+__host__ __device__ inline int sweep_pipe_smem_bytes(int S, int HW, int HWs, int HWp, int tsize) {
+    return S / HW * HWs * tsize + HWp + 256;
+}
+
+template <typename T, int MODEL, bool SLIP, int DEPTH>
+__global__ void __launch_bounds__(1024)
+vi_sweep_pipe_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, const T *__restrict__ Vin,
+                     T *__restrict__ Vout, unsigned long long *__restrict__ shards, int k, int check_prev) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    if (check_prev && prev_sweep_converged(shards, k, geo.tol)) return;
+    using Row = PipeRow<T, MODEL>;
+    constexpr int NV = Row::NV;
+    const int HWs = geo.HWs;
+    T *Vt = reinterpret_cast<T *>(smem);
+    uint8_t *cl = smem + (size_t)geo.Ss * sizeof(T);
+    T *slots = reinterpret_cast<T *>(smem + (size_t)geo.Ss * sizeof(T) + geo.HWp);
+    const int c = threadIdx.x;
+    const bool own_cell = c < geo.HW;
+    const bool cell_word = c < (geo.HWp >> 2);
+    const int cc = own_cell ? c : 0;
+    const int stride = gridDim.x;
+
+    // Unconditional loads (clamped addresses: past the last grid, idle threads re-read a valid row
+    // whose values are never used), so the loop body is straight-line and the compiler's vmcnt
+    // waits count the DEPTH-1 younger fetches instead of draining them.
+    const int cw_idx = cell_word ? c : 0;
+    auto fetch = [&](int e, Row &r) {
+        const long long ee = e < geo.B ? e : geo.B - 1;
+        const V4<T> *src = reinterpret_cast<const V4<T> *>(Vin + ee * geo.S + (long long)cc * 4 * NV);
+#pragma unroll
+        for (int q = 0; q < NV; ++q) r.v[q] = src[q];
+        r.cw = reinterpret_cast<const uint32_t *>(cells + ee * geo.HWp)[cw_idx];
+    };
+    Row rows[DEPTH];
+#pragma unroll
+    for (int s = 0; s < DEPTH; ++s) fetch(blockIdx.x + s * stride, rows[s]);
+    T acc = (T)0;
+    auto step = [&](int e, Row &r) {
+        // stage this grid's rows; every thread is past the previous grid's LDS reads (barrier below)
+        if (MODEL == MGDP_MODEL_XYD) {
+#pragma unroll
+            for (int d = 0; d < 4; ++d) Vt[d * HWs + c] = r.v[0].v[d];
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) *reinterpret_cast<V4<T> *>(Vt + (q * HWs + c) * 4) = r.v[q];
+        }
+        if (cell_word) reinterpret_cast<uint32_t *>(cl)[c] = r.cw;
+        __syncthreads();
+        // refill in place, DEPTH grids ahead: r is dead once staged (the thread's own values are read
+        // back from the tile), so the loads need no register copies and stay in flight during this
+        // grid's work
+        fetch(e + DEPTH * stride, r);
+        Row own;
+        if (MODEL == MGDP_MODEL_XYD) {
+#pragma unroll
+            for (int d = 0; d < 4; ++d) own.v[0].v[d] = Vt[d * HWs + c];
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) own.v[q] = *reinterpret_cast<const V4<T> *>(Vt + (q * HWs + c) * 4);
+        }
+        T *dst = Vout + (long long)e * geo.S + (long long)c * 4 * NV;
+        if (MODEL == MGDP_MODEL_XYD) {
+            const XydTopo<T> tp = xyd_topo_soa<T>(cl, geo, cc);
+            T nbv[4];
+            xyd_load_nb(tp, Vt, nbv);
+            V4<T> out;
+            uint32_t pk;
+            const T dv = xyd_step<T, SLIP, false>(tp, cf, own.v[0], nbv, out, pk);
+            if (own_cell) {
+                *reinterpret_cast<V4<T> *>(dst) = out;
+                acc = vmax(acc, dv);
+            }
+        } else {
+            const DkTopo tp = dk_topo_soa(cl, geo, cc);
+            V4<T> nbs[4];
+            dk_load_nb(tp, Vt, nbs);
+            T in[16], outv[16];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) in[4 * q + j] = own.v[q].v[j];
+            uint32_t pk[4];
+            const T dv = dk_step<T, false>(tp, cf, in, nbs, outv, pk);
+            if (own_cell) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    reinterpret_cast<V4<T> *>(dst)[q] = V4<T>{{outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]}};
+                acc = vmax(acc, dv);
+            }
+        }
+        __syncthreads();  // the tile is rewritten by the next grid
+    };
+    int e = blockIdx.x;
+    while (true) {
+        if (e >= geo.B) break;
+        step(e, rows[0]);
+        e += stride;
+        if (DEPTH > 1) {
+            if (e >= geo.B) break;
+            step(e, rows[DEPTH - 1]);
+            e += stride;
+        }
+    }
+    const T bdv = block_max(acc, slots, 0);
+    if (threadIdx.x == 0 && shards)
+        atomicMax(shards + (long long)(k - 1) * 8 + (blockIdx.x & 7), (unsigned long long)__double_as_longlong((double)bdv));
+}
+
 }  // namespace mgdp

@@ -132,18 +132,19 @@ __device__ __forceinline__ XydTopo<T> xyd_topo(const uint8_t *cl, const Geo &geo
     tp.valid = xyd_free(cl[c]) || (ND && cl[c] == T_LAVA);
     tp.term = 0;
     tp.lavaF = 0;
+    // Branch-free (selects only, every LDS byte read unconditional): it runs once per grid-sweep
+    // in the HBM sweep kernels.
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-        const int cfr = c + geo.off[d];
-        const int tf = tp.valid ? cl[cfr] : T_WALL;  // valid cells are interior (closed border)
-        tp.tq[d] = (T)0;
-        tp.nbi[d] = c * 4 + d;
-        if (tf == T_GOAL) { tp.term |= 1u << d; tp.tq[d] = (T)1; }
-        else if (tf == T_LAVA) {
-            if (ND) { tp.lavaF |= 1u << d; tp.nbi[d] = cfr * 4 + d; }
-            else tp.term |= 1u << d;
-        }
-        else if (xyd_free(tf)) tp.nbi[d] = cfr * 4 + d;
+        const int cfr = tp.valid ? c + geo.off[d] : c;  // valid cells are interior (closed border)
+        const int tf0 = cl[cfr];
+        const int tf = tp.valid ? tf0 : T_WALL;
+        const bool goal = tf == T_GOAL, lava = tf == T_LAVA;
+        const bool enter = xyd_free(tf) || (ND && lava);  // forward reads the front cell's state
+        tp.term |= (uint32_t)(goal || (!ND && lava)) << d;
+        tp.lavaF |= (uint32_t)(ND && lava) << d;
+        tp.tq[d] = goal ? (T)1 : (T)0;
+        tp.nbi[d] = (enter ? cfr : c) * 4 + d;
     }
     return tp;
 }
@@ -257,7 +258,8 @@ __device__ __forceinline__ DkTopo dk_topo(const uint8_t *cl, const Geo &geo, int
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
         const int cfr = inner ? c + geo.off[d] : c;
-        const int tf = inner ? cl[cfr] : T_WALL;
+        const int tf0 = cl[cfr];  // unconditional read, select below (branch-free)
+        const int tf = inner ? tf0 : T_WALL;
         tp.f[d] = dk_walk_mask(tf) | (tf == T_GOAL ? 16u : 0u) | (tf == T_LAVA ? 32u : 0u) |
                   (tf == T_KEY ? 64u : 0u) | (tf == T_DOOR ? 128u : 0u);
         tp.nb[d] = cfr * 16 + d * 4;
