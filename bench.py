@@ -13,6 +13,12 @@ Workloads; default = BASELINE configs[1]:
   lava65536      MiniGrid-LavaCrossingS11N5-v0, 65536 seeds sharded over N GPUs (RCCL dV all-reduce)
   doorkey65536   MiniGrid-DoorKey-16x16-v0 (pos, dir, has_key, door_open), 65536 seeds sharded
 
+Side paths (measured to the same bar; their own metric, not the headline):
+  step_doorkey16x65536 / step_fourrooms65536 / step_lava65536
+                 batched MiniGridEnv.step + gen_obs (csrc/envs.hip), 65536 envs per GPU, env-steps/s
+  gen_lava65536 / gen_fourrooms65536 / gen_doorkey16x65536
+                 batched reset(seed) grid generation (csrc/gen.hip), 65536 seeds per GPU, grids/s
+
 Run:  python bench.py [--gpus N --steps K --warmup W --workload NAME --method fused|sweep ...]
       N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
@@ -41,8 +47,29 @@ WORKLOADS = {
 }
 
 
+STEP_WORKLOADS = {
+    "step_doorkey16x65536": dict(env_id="MiniGrid-DoorKey-16x16-v0", per_gpu=65536),
+    "step_fourrooms65536": dict(env_id="MiniGrid-FourRooms-v0", per_gpu=65536),
+    "step_lava65536": dict(env_id="MiniGrid-LavaCrossingS11N5-v0", per_gpu=65536),
+}
+GEN_WORKLOADS = {
+    "gen_lava65536": dict(env_id="MiniGrid-LavaCrossingS11N5-v0", per_gpu=65536),
+    "gen_fourrooms65536": dict(env_id="MiniGrid-FourRooms-v0", per_gpu=65536),
+    "gen_doorkey16x65536": dict(env_id="MiniGrid-DoorKey-16x16-v0", per_gpu=65536),
+}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def step_bytes_per_env_step(view: int) -> int:
+    """Algorithmic HBM bytes of one env step (csrc/envs.hip layout): reads action 4, agent
+    (x, y, dir, step_count) 16, carry 8, max_steps 4, see_through 1 and the view window's
+    view*view cells x 3 planes; writes the obs view*view*3, direction 4, reward 8, terminated 1,
+    truncated 1, status 4, agent 16, carry 8 (pickup/drop/toggle cell writes are rare, not counted)."""
+    vv3 = view * view * 3
+    return (4 + 16 + 8 + 4 + 1 + vv3) + (vv3 + 4 + 8 + 1 + 1 + 4 + 16 + 8)
 
 
 def algorithmic_bytes_per_update(tsize: int, A: int) -> float:
@@ -120,7 +147,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="empty16", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="empty16", choices=sorted(WORKLOADS) + sorted(STEP_WORKLOADS) + sorted(GEN_WORKLOADS))
     ap.add_argument("--method", default="fused", choices=["fused", "sweep"])
     ap.add_argument("--mapping", default="cell", choices=["cell", "sa"])
     ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
@@ -152,6 +179,16 @@ def main():
         else:
             dist.init_process_group(backend)
     red_dev = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
+
+    if args.workload in STEP_WORKLOADS or args.workload in GEN_WORKLOADS:
+        side = step_bench if args.workload in STEP_WORKLOADS else gen_bench
+        out = side(args, rank, world, local, dist, red_dev)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     import minigrid_dynamicprogramming_amd as mg
     from minigrid_dynamicprogramming_amd.distributed import solve_sharded
@@ -273,6 +310,183 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _max_over_ranks(dist, red_dev, elapsed, units):
+    import torch
+
+    if dist is None:
+        return elapsed, units
+    t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
+    u = torch.tensor([units], dtype=torch.float64, device=red_dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(u, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(u.item())
+
+
+def _timed_launches(args, launch, dist):
+    """W untimed launches, then K launches bracketed by barrier + synchronize, each launch between
+    a pair of events on the current stream (the stream the library launches on)."""
+    import torch
+
+    for i in range(args.warmup):
+        launch(i)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record()
+        launch(args.warmup + i)
+        evs[i][1].record()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_s = sum(a.elapsed_time(b) for a, b in evs) / 1000.0
+    return elapsed, kern_s
+
+
+def step_bench(args, rank, world, local, dist, red_dev):
+    """K batched steps (MiniGridEnv.step + gen_obs, one envs_step_kernel launch
+    each) of B envs resident in HBM, actions pre-drawn on the device; env-steps/s."""
+    import torch
+
+    from minigrid_dynamicprogramming_amd.vector import MiniGridVecEnv
+
+    spec = STEP_WORKLOADS[args.workload]
+    B = spec["per_gpu"]
+    venv = MiniGridVecEnv(spec["env_id"], B, device=local)
+    venv.reset(seed=rank * B)  # reset(seed) for seeds [rank*B, (rank+1)*B), generated on the GPU
+    stream = torch.cuda.current_stream()
+    venv.set_stream(stream.cuda_stream)
+    dev = torch.device("cuda", local)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    acts = torch.randint(0, 7, (args.warmup + args.steps, B), generator=g, device=dev, dtype=torch.int32)
+    V = venv.view
+    obs = torch.empty((B, V, V, 3), dtype=torch.uint8, device=dev)
+    dirn = torch.empty(B, dtype=torch.int32, device=dev)
+    rew = torch.empty(B, dtype=torch.float64, device=dev)
+    term = torch.empty(B, dtype=torch.uint8, device=dev)
+    trunc = torch.empty(B, dtype=torch.uint8, device=dev)
+    status = torch.empty(B, dtype=torch.int32, device=dev)
+
+    def launch(i):
+        venv.step_device(acts[i], obs, dirn, rew, term, trunc, status)
+
+    elapsed, kern_s = _timed_launches(args, launch, dist)
+    assert int(status.max().item()) == 0, "step kernel reported an error status"
+    elapsed_max, steps_total = _max_over_ranks(dist, red_dev, elapsed, float(B) * args.steps)
+    out = None
+    if rank == 0:
+        bpe = step_bytes_per_env_step(V)
+        avg = kern_s / args.steps
+        ach = bpe * B / avg / 1e9
+        out = {
+            "metric": "batched env steps/sec (MiniGridEnv.step + gen_obs), " + spec["env_id"],
+            "value": steps_total / elapsed_max, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed_max * 1000.0 / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": f"synthetic: {spec['env_id']} reset(seed) grids for seeds [{rank * B}, ..) generated on the "
+                    "GPU, uniform random actions 0..6 drawn on the device (no resets inside the timed region)",
+            "config": {"workload": args.workload, "env_id": spec["env_id"], "envs_per_gpu": B,
+                       "global_envs": B * world, "view": V, "parallelism": f"independent env batches x{world}"},
+            "roofline": {"bound": "hbm", "kernel": "envs_step_kernel", "achieved": ach, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                         "traffic": load_traffic(f"{args.workload}/step", 1.0), "launches": args.steps,
+                         "avg_launch_us": avg * 1e6, "alg_bytes_per_launch": bpe * B,
+                         "alg_bytes_per_env_step": bpe},
+        }
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = step_cpu_baseline(venv, acts, args.cpu_budget)
+    venv.close()
+    return out
+
+
+def step_cpu_baseline(venv, acts, budget_s, n=4096):
+    """The oracle's step() restatement (oracle/mgdp_oracle.c orc_step_batch, 1 thread) over the first
+    n envs of the same batch with the same action stream, for about budget_s seconds."""
+    from oracle import oracle
+
+    st = venv.get_state()  # grids/agents as left by the timed run: same distribution of states
+    ob = oracle.OracleBatch(st["enc"][:n], st["agent"][:n], venv.max_steps, venv.see_through, venv.view)
+    A = acts[:, :n].cpu().numpy()
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        ob.step(A[steps % len(A)])
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": steps * n / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{steps} batched steps of {n} envs of the same workload (same action stream), "
+                      f"oracle/mgdp_oracle.c orc_step_batch, {el:.1f} s"}
+
+
+def gen_bench(args, rank, world, local, dist, red_dev):
+    """reset(seed) for B consecutive seeds generated on the GPU (one
+    gen_grids_kernel launch: seeding + the family's _gen_grid), written to device buffers; grids/s."""
+    import torch
+
+    from minigrid_dynamicprogramming_amd import gen, make
+
+    spec = GEN_WORKLOADS[args.workload]
+    B = spec["per_gpu"]
+    env = make(spec["env_id"])
+    W, H = env.width, env.height
+    dev = torch.device("cuda", local)
+    enc = torch.empty((B, W, H, 3), dtype=torch.uint8, device=dev)
+    cells = torch.empty((B, H, W), dtype=torch.uint8, device=dev)
+    agent = torch.empty((B, 3), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def launch(i):
+        gen.generate_device(env, rank * B, B, enc, cells, agent, device=local, stream=stream)
+
+    elapsed, kern_s = _timed_launches(args, launch, dist)
+    assert int(agent[:, 2].min().item()) >= 0, "generator reported a placement failure"
+    elapsed_max, total = _max_over_ranks(dist, red_dev, elapsed, float(B) * args.steps)
+    out = None
+    if rank == 0:
+        bpg = W * H * 3 + H * W + 12  # written per grid: encoding + type codes + agent
+        avg = kern_s / args.steps
+        ach = bpg * B / avg / 1e9
+        out = {
+            "metric": "batched reset(seed) grid generation, grids/sec, " + spec["env_id"],
+            "value": total / elapsed_max, "unit": "grids/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed_max * 1000.0 / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+            "data": f"seeds [{rank * B}, {rank * B + B}) per rank (numpy SeedSequence/PCG64 restated in HIP)",
+            "config": {"workload": args.workload, "env_id": spec["env_id"], "grids_per_gpu": B,
+                       "global_grids": B * world, "parallelism": f"seed ranges x{world}"},
+            "roofline": {"bound": "hbm", "kernel": "gen_grids_kernel", "achieved": ach, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                         "traffic": load_traffic(f"{args.workload}/gen", 1.0), "launches": args.steps,
+                         "avg_launch_us": avg * 1e6, "alg_bytes_per_launch": bpg * B, "alg_bytes_per_grid": bpg,
+                         "regime": "integer RNG / rejection-loop latency bound (one thread per seed); "
+                                   "HBM carries only the output"},
+        }
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = gen_cpu_baseline(env, args.cpu_budget)
+    return out
+
+
+def gen_cpu_baseline(env, budget_s):
+    """The host generator (minigrid_dynamicprogramming_amd/envs.py, the numpy restatement of the
+    reference's reset/_gen_grid with the same Generator calls), 1 thread, seeds 0.. for budget_s."""
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        env.generate(seed=n)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": n / el, "unit": "grids/s", "cores": 1, "kind": "port",
+            "sample": f"{n} host reset(seed) generations (numpy PCG64, envs.py), {el:.1f} s"}
 
 
 def hbm_side_measurement(args, n_solves=3):

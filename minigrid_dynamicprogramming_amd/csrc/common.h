@@ -38,12 +38,15 @@ inline int hip_fail(hipError_t e, const char *what, const char *file, int line) 
         if (!(cond)) { ::mgdp::set_error(__VA_ARGS__); return (code); }      \
     } while (0)
 
-// Sets the device for the calling thread and restores the previous one on scope exit.
+// Sets the device for the calling thread and restores the previous one on scope exit (no runtime
+// call beyond hipGetDevice when the thread is already on `dev`: the lone-grid solve path crosses
+// several guarded entry points per solve).
 struct DeviceGuard {
     int prev = -1;
     bool ok = false;
     explicit DeviceGuard(int dev) {
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev == dev) { prev = -1; ok = true; return; }
         ok = hipSetDevice(dev) == hipSuccess;
     }
     ~DeviceGuard() {
@@ -51,6 +54,6 @@ struct DeviceGuard {
     }
 };
 
-inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+__host__ __device__ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 }  // namespace mgdp

@@ -15,6 +15,7 @@
 // top_left - f*j + r*i (f = DIR_TO_VEC[dir], r = right_vec, minigrid_env.py:421-446), which equals
 // the reference's slice + (dir+1) x rotate_left; process_vis runs on a 64-bit visibility mask.
 // Observations are assembled in LDS and leave with 16-byte coalesced stores.
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -119,6 +120,179 @@ __device__ __forceinline__ double reward_fn(int sc, int ms) {
     return 1.0 - t;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Windowed gen_obs.  The view's vs x vs cells always cover an axis-aligned world box
+// [bx, bx+vs) x [by, by+vs) (rotation only permutes them), so the thread stages that box of the
+// three planes into its own LDS window with 3*vs*3 independent dword loads (all in flight at
+// once; byte-aligned with v_alignbyte so window cell (u, v) is byte u of row v) instead of ~5*vs*vs
+// dependent byte loads from HBM, and the visibility and encode passes read LDS.  Rows outside the
+// grid are loaded from a clamped address and never read (bounds are tested in world coordinates,
+// exactly as gen_obs_one does).  Bit-identical to gen_obs_one.
+// ------------------------------------------------------------------------------------------------
+constexpr int kWinRow = 8;                    // bytes per staged window row (vs <= 7)
+__host__ __device__ constexpr int win_stride(int vs) { return 3 * vs * kWinRow + 4; }  // odd dword count
+
+__device__ __forceinline__ void view_box(int ax, int ay, int d, int vs, int &tlx, int &tly, int &bx, int &by) {
+    const int hs = vs / 2;
+    const int fx = kDX[d], fy = kDY[d], rx = -fy, ry = fx;
+    tlx = ax + fx * (vs - 1) - rx * hs;
+    tly = ay + fy * (vs - 1) - ry * hs;
+    bx = tlx + min(0, -fx * (vs - 1)) + min(0, rx * (vs - 1));
+    by = tly + min(0, -fy * (vs - 1)) + min(0, ry * (vs - 1));
+}
+
+template <int VS>
+__device__ __forceinline__ void stage_window(const EnvGeo &g, const uint8_t *ty, const uint8_t *co, const uint8_t *st,
+                                             int bx, int by, uint32_t *win) {
+    const int nd = g.HWp >> 2;
+    const uint32_t *P[3] = {reinterpret_cast<const uint32_t *>(ty), reinterpret_cast<const uint32_t *>(co),
+                            reinterpret_cast<const uint32_t *>(st)};
+    uint32_t w[3][VS][3];
+#pragma unroll
+    for (int v = 0; v < VS; ++v) {
+        const int o = (by + v) * g.W + bx;
+        const int a = o >> 2;  // floor(o / 4): o may be negative left of / above the grid
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int idx = min(max(a + q, 0), nd - 1);  // only bytes of in-grid cells are ever read
+#pragma unroll
+            for (int p = 0; p < 3; ++p) w[p][v][q] = P[p][idx];
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < VS; ++v) {
+        const int sh = ((by + v) * g.W + bx) & 3;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            win[(p * VS + v) * 2 + 0] = __builtin_amdgcn_alignbyte(w[p][v][1], w[p][v][0], sh);
+            win[(p * VS + v) * 2 + 1] = __builtin_amdgcn_alignbyte(w[p][v][2], w[p][v][1], sh);
+        }
+    }
+}
+
+// gen_obs_one on the staged window `wb` (plane p, row v, column u at wb[(p*vs + v)*8 + u]).
+__device__ void gen_obs_win(const EnvGeo &g, const uint8_t *wb, int tlx, int tly, int bx, int by, int d, int ct,
+                            int cc, bool see_through, uint8_t *img) {
+    const int vs = g.vs, hs = vs / 2;
+    const int fx = kDX[d], fy = kDY[d];
+    const int rx = -fy, ry = fx;
+    const uint8_t *WT = wb, *WC = wb + vs * kWinRow, *WS = wb + 2 * vs * kWinRow;
+    unsigned long long sb = 0, mask = 0;
+    for (int j = 0; j < vs; ++j)
+        for (int i = 0; i < vs; ++i) {
+            const int wx = tlx - fx * j + rx * i, wy = tly - fy * j + ry * i;
+            bool s = false;  // out of bounds -> Wall (grid.py:136-139)
+            if (wx >= 0 && wy >= 0 && wx < g.W && wy < g.H) {
+                const int o = (wy - by) * kWinRow + (wx - bx);
+                s = see_behind(WT[o], WS[o]);
+            }
+            if (s) sb |= 1ull << (j * 8 + i);
+        }
+    if (see_through) {
+        mask = ~0ull;
+    } else {  // process_vis, grid.py:291-328, literal loop order
+        mask = 1ull << ((vs - 1) * 8 + hs);
+        for (int j = vs - 1; j >= 0; --j) {
+            for (int i = 0; i < vs - 1; ++i) {
+                const unsigned long long b = 1ull << (j * 8 + i);
+                if (!(mask & b) || !(sb & b)) continue;
+                mask |= b << 1;
+                if (j > 0) mask |= (b << 1 >> 8) | (b >> 8);
+            }
+            for (int i = vs - 1; i >= 1; --i) {
+                const unsigned long long b = 1ull << (j * 8 + i);
+                if (!(mask & b) || !(sb & b)) continue;
+                mask |= b >> 1;
+                if (j > 0) mask |= (b >> 1 >> 8) | (b >> 8);
+            }
+        }
+    }
+    for (int i = 0; i < vs; ++i)
+        for (int j = 0; j < vs; ++j) {
+            uint8_t *o = img + (i * vs + j) * 3;
+            int t = 0, c = 0, s = 0;
+            if (mask & (1ull << (j * 8 + i))) {
+                if (i == hs && j == vs - 1) {
+                    if (ct > 0) { t = ct; c = cc; } else { t = T_EMPTY; }
+                } else {
+                    const int wx = tlx - fx * j + rx * i, wy = tly - fy * j + ry * i;
+                    if (wx >= 0 && wy >= 0 && wx < g.W && wy < g.H) {
+                        const int w = (wy - by) * kWinRow + (wx - bx);
+                        t = WT[w];
+                        if (t != T_EMPTY) { c = WC[w]; s = WS[w]; }
+                    } else {
+                        t = T_WALL; c = C_GREY;
+                    }
+                }
+            }
+            o[0] = (uint8_t)t; o[1] = (uint8_t)c; o[2] = (uint8_t)s;
+        }
+}
+
+// One env step: MiniGridEnv.step (minigrid_env.py:520-590) on registers; the front-cell mutation
+// of pickup / drop / toggle is returned (mut, nt/nc/ns) instead of written, so the caller orders it
+// against the window staging.
+struct StepOut {
+    int x, y, d, sc, ct, cc, stat, term, trunc, mut, fi, nt, nc, ns;
+    double r;
+};
+
+__device__ __forceinline__ StepOut step_one(const EnvGeo &g, const uint8_t *ty, const uint8_t *co, const uint8_t *st,
+                                            int x, int y, int d, int sc, int ct, int cc, int a, int ms) {
+    StepOut o{x, y, d, sc + 1, ct, cc, MGDP_OK, 0, 0, 0, 0, 0, 0, 0, 0.0};  // step_count += 1 first (:523)
+    const int fx = x + kDX[d], fy = y + kDY[d];
+    // Grid.get asserts on the front cell (minigrid_env.py:533) before the action branch
+    if (fx < 0 || fy < 0 || fx >= g.W || fy >= g.H) { o.stat = MGDP_E_BOUNDS; return o; }
+    if (a < 0 || a > 6) { o.stat = MGDP_E_ACTION; return o; }
+    const int fi = fy * g.W + fx;
+    o.fi = fi;
+    const int ft = ty[fi];
+    const bool fnone = ft == T_EMPTY;
+    if (a == 0) {
+        o.d = (d + 3) & 3;
+    } else if (a == 1) {
+        o.d = (d + 1) & 3;
+    } else if (a == 2) {
+        const bool overlap = ft == T_GOAL || ft == T_FLOOR || ft == T_LAVA || (ft == T_DOOR && st[fi] == D_OPEN);
+        if (fnone || overlap) { o.x = fx; o.y = fy; }
+        if (ft == T_GOAL) { o.term = 1; o.r = reward_fn(o.sc, ms); }
+        if (ft == T_LAVA) o.term = 1;
+    } else if (a == 3) {
+        if ((ft == T_KEY || ft == T_BALL || ft == T_BOX) && ct == 0) {
+            o.ct = ft; o.cc = co[fi];
+            o.mut = 1; o.nt = T_EMPTY; o.nc = 0; o.ns = 0;
+        }
+    } else if (a == 4) {
+        if (fnone && ct != 0) {
+            o.mut = 1; o.nt = ct; o.nc = cc; o.ns = 0;
+            o.ct = 0; o.cc = 0;
+        }
+    } else if (a == 5) {
+        if (ft == T_DOOR) {
+            const int s = st[fi];
+            if (s == D_LOCKED) {
+                if (ct == T_KEY && cc == co[fi]) { o.mut = 1; o.nt = ft; o.nc = co[fi]; o.ns = D_OPEN; }
+            } else {
+                o.mut = 1; o.nt = ft; o.nc = co[fi]; o.ns = s == D_OPEN ? D_CLOSED : D_OPEN;
+            }
+        } else if (ft == T_BOX) {  // Box(contains=None).toggle -> empty cell
+            o.mut = 1; o.nt = T_EMPTY; o.nc = 0; o.ns = 0;
+        }
+    }
+    if (o.sc >= ms) o.trunc = 1;
+    if (g.nd_mask) {  // NoDeath.step: front cell before, agent's cell after the step (never mutated)
+        const bool going = a == 2 && !fnone && ((g.nd_mask >> ft) & 1u);
+        const int ct_now = ty[o.y * g.W + o.x];
+        const bool in_death = ct_now != T_EMPTY && ((g.nd_mask >> ct_now) & 1u);
+        if (o.term && (going || in_death)) {
+            o.term = 0;
+            o.r += g.death_cost;
+        }
+    }
+    return o;
+}
+
+template <bool WIN>
 __global__ void __launch_bounds__(kStepBlock)
 envs_step_kernel(EnvGeo g, uint8_t *__restrict__ TY, uint8_t *__restrict__ CO, uint8_t *__restrict__ ST,
                  int32_t *__restrict__ agent, int32_t *__restrict__ carry,
@@ -132,81 +306,46 @@ envs_step_kernel(EnvGeo g, uint8_t *__restrict__ TY, uint8_t *__restrict__ CO, u
     const int e0 = blockIdx.x * kStepBlock;
     const int e = e0 + threadIdx.x;
     uint8_t *img = smem + threadIdx.x * obs_bytes;
+    uint32_t *win = reinterpret_cast<uint32_t *>(smem + round_up(kStepBlock * obs_bytes, 16) +
+                                                 threadIdx.x * win_stride(g.vs));
     if (e < g.B) {
         uint8_t *ty = TY + (long long)e * g.HWp;
         uint8_t *co = CO + (long long)e * g.HWp;
         uint8_t *st = ST + (long long)e * g.HWp;
-        int x = agent[e * 4 + 0], y = agent[e * 4 + 1], d = agent[e * 4 + 2], sc = agent[e * 4 + 3];
-        int ct = carry[e * 2 + 0], cc = carry[e * 2 + 1];
-        int stat = MGDP_OK;
-        double r = 0.0;
-        int term = 0, trunc = 0;
-        if (!observe_only) {
-            const int a = actions[e];
-            sc += 1;  // minigrid_env.py:523, before the action is validated
-            const int fx = x + kDX[d], fy = y + kDY[d];
-            // Grid.get asserts on the front cell (minigrid_env.py:533) before the action branch
-            if (fx < 0 || fy < 0 || fx >= g.W || fy >= g.H) {
-                stat = MGDP_E_BOUNDS;
-            } else if (a < 0 || a > 6) {
-                stat = MGDP_E_ACTION;
+        const int4 ag = reinterpret_cast<const int4 *>(agent)[e];
+        const int2 cr = reinterpret_cast<const int2 *>(carry)[e];
+        StepOut o{ag.x, ag.y, ag.z, ag.w, cr.x, cr.y, MGDP_OK, 0, 0, 0, 0, 0, 0, 0, 0.0};
+        if (!observe_only) o = step_one(g, ty, co, st, ag.x, ag.y, ag.z, ag.w, cr.x, cr.y, actions[e], max_steps[e]);
+        if (!WIN && o.mut) { ty[o.fi] = (uint8_t)o.nt; co[o.fi] = (uint8_t)o.nc; st[o.fi] = (uint8_t)o.ns; }
+        if (o.stat == MGDP_OK) {
+            if (WIN) {
+                int tlx, tly, bx, by;
+                view_box(o.x, o.y, o.d, g.vs, tlx, tly, bx, by);
+                if (g.vs == 7) stage_window<7>(g, ty, co, st, bx, by, win);
+                else if (g.vs == 5) stage_window<5>(g, ty, co, st, bx, by, win);
+                else stage_window<3>(g, ty, co, st, bx, by, win);
+                uint8_t *wb = reinterpret_cast<uint8_t *>(win);
+                if (o.mut) {  // the front cell (in the view: the agent did not move) as the step left it
+                    const int w = (o.fi / g.W - by) * kWinRow + (o.fi % g.W - bx);
+                    wb[w] = (uint8_t)o.nt; wb[g.vs * kWinRow + w] = (uint8_t)o.nc; wb[2 * g.vs * kWinRow + w] = (uint8_t)o.ns;
+                    ty[o.fi] = (uint8_t)o.nt; co[o.fi] = (uint8_t)o.nc; st[o.fi] = (uint8_t)o.ns;
+                }
+                gen_obs_win(g, wb, tlx, tly, bx, by, o.d, o.ct, o.cc, see[e] != 0, img);
             } else {
-                const int fi = fy * g.W + fx;
-                const int ft = ty[fi];
-                const bool fnone = ft == T_EMPTY;
-                if (a == 0) {
-                    d = (d + 3) & 3;
-                } else if (a == 1) {
-                    d = (d + 1) & 3;
-                } else if (a == 2) {
-                    const bool overlap = ft == T_GOAL || ft == T_FLOOR || ft == T_LAVA ||
-                                         (ft == T_DOOR && st[fi] == D_OPEN);
-                    if (fnone || overlap) { x = fx; y = fy; }
-                    if (ft == T_GOAL) { term = 1; r = reward_fn(sc, max_steps[e]); }
-                    if (ft == T_LAVA) term = 1;
-                } else if (a == 3) {
-                    if ((ft == T_KEY || ft == T_BALL || ft == T_BOX) && ct == 0) {
-                        ct = ft; cc = co[fi];
-                        ty[fi] = T_EMPTY; co[fi] = 0; st[fi] = 0;
-                    }
-                } else if (a == 4) {
-                    if (fnone && ct != 0) {
-                        ty[fi] = (uint8_t)ct; co[fi] = (uint8_t)cc; st[fi] = 0;
-                        ct = 0; cc = 0;
-                    }
-                } else if (a == 5) {
-                    if (ft == T_DOOR) {
-                        const int s = st[fi];
-                        if (s == D_LOCKED) {
-                            if (ct == T_KEY && cc == co[fi]) st[fi] = D_OPEN;
-                        } else {
-                            st[fi] = s == D_OPEN ? D_CLOSED : D_OPEN;
-                        }
-                    } else if (ft == T_BOX) {  // Box(contains=None).toggle -> empty cell
-                        ty[fi] = T_EMPTY; co[fi] = 0; st[fi] = 0;
-                    }
-                }
-                if (sc >= max_steps[e]) trunc = 1;
-                if (g.nd_mask) {  // NoDeath.step: front cell before, agent's cell after the step
-                    const bool going = a == 2 && !fnone && ((g.nd_mask >> ft) & 1u);
-                    const int ct_now = ty[y * g.W + x];
-                    const bool in_death = ct_now != T_EMPTY && ((g.nd_mask >> ct_now) & 1u);
-                    if (term && (going || in_death)) {
-                        term = 0;
-                        r += g.death_cost;
-                    }
-                }
+                gen_obs_one(g, ty, co, st, o.x, o.y, o.d, o.ct, o.cc, see[e] != 0, img);
             }
-            agent[e * 4 + 0] = x; agent[e * 4 + 1] = y; agent[e * 4 + 2] = d; agent[e * 4 + 3] = sc;
-            carry[e * 2 + 0] = ct; carry[e * 2 + 1] = cc;
-            reward[e] = r;
-            terminated[e] = (uint8_t)term;
-            truncated[e] = (uint8_t)trunc;
-            status[e] = stat;
+        } else {
+            for (int i = 0; i < obs_bytes; ++i) img[i] = 0;
         }
-        if (stat == MGDP_OK) gen_obs_one(g, ty, co, st, x, y, d, ct, cc, see[e] != 0, img);
-        else for (int i = 0; i < obs_bytes; ++i) img[i] = 0;
-        direction[e] = d;
+        if (!observe_only) {
+            reinterpret_cast<int4 *>(agent)[e] = make_int4(o.x, o.y, o.d, o.sc);
+            reinterpret_cast<int2 *>(carry)[e] = make_int2(o.ct, o.cc);
+            reward[e] = o.r;
+            terminated[e] = (uint8_t)o.term;
+            truncated[e] = (uint8_t)o.trunc;
+            status[e] = o.stat;
+        }
+        direction[e] = o.d;
     }
     __syncthreads();
     const int n = min(kStepBlock, g.B - e0);
@@ -228,6 +367,7 @@ struct mgdp_envs {
     double *d_rew = nullptr;
     uint32_t nd_mask = 0;
     double death_cost = -1.0;
+    bool win = true;  // windowed gen_obs (MGDP_STEP_WIN=0: the per-cell HBM byte loads of gen_obs_one)
 };
 
 namespace {
@@ -237,8 +377,8 @@ EnvGeo env_geo(const mgdp_envs *E) { return EnvGeo{E->B, E->W, E->H, E->HWp, E->
 int launch_step(mgdp_envs *E, const int32_t *d_act, uint8_t *d_obs, int32_t *d_dir, double *d_rew,
                 uint8_t *d_term, uint8_t *d_trunc, int32_t *d_status, int observe_only) {
     const int grid = (E->B + kStepBlock - 1) / kStepBlock;
-    const int smem = kStepBlock * E->vs * E->vs * 3;
-    hipLaunchKernelGGL(envs_step_kernel, dim3(grid), dim3(kStepBlock), smem, E->stream, env_geo(E),
+    const int smem = (int)round_up(kStepBlock * E->vs * E->vs * 3, 16) + kStepBlock * win_stride(E->vs);
+    hipLaunchKernelGGL(E->win ? envs_step_kernel<true> : envs_step_kernel<false>, dim3(grid), dim3(kStepBlock), smem, E->stream, env_geo(E),
                        E->d_ty, E->d_co, E->d_st, E->d_agent, E->d_carry, E->d_max, E->d_see, d_act,
                        d_obs, d_dir, d_rew, d_term, d_trunc, d_status, observe_only);
     MGDP_HIP(hipGetLastError());
@@ -261,6 +401,7 @@ int mgdp_envs_create(int32_t device, int32_t B, int32_t W, int32_t H, int32_t vi
     mgdp_envs *E = new mgdp_envs();
     E->device = device; E->B = B; E->W = W; E->H = H; E->HW = W * H; E->HWp = (int)round_up(W * H, 16);
     E->vs = view_size;
+    if (const char *ev = std::getenv("MGDP_STEP_WIN")) E->win = std::atoi(ev) != 0;
     const size_t P = (size_t)B * E->HWp;
     hipError_t e = hipSuccess;
     auto al = [&](void **p, size_t n) { if (e == hipSuccess) e = hipMalloc(p, n); };

@@ -561,3 +561,23 @@ int orc_step(int W, int H, uint8_t *ty, uint8_t *co, uint8_t *st, int32_t *state
     orc_gen_obs(W, H, ty, co, st, state[0], state[1], state[2], carry[0], carry[1], see_through, vs, image);
     return 0;
 }
+
+/* B envs stepped once each (the CPU baseline of the batched step path; same per-env semantics as
+ * orc_step above, i.e. MiniGridEnv.step minigrid_env.py:520-590).  Planes are [B][HWp] row-major,
+ * state [B][4], carry [B][2], obs [B][vs*vs*3]; status[b] is orc_step's return code.
+ * nthreads > 1 splits the envs over OpenMP threads. */
+void orc_step_batch(int B, int W, int H, int HWp, uint8_t *ty, uint8_t *co, uint8_t *st, int32_t *state,
+                    int32_t *carry, const int32_t *max_steps, const uint8_t *see, int vs, const int32_t *actions,
+                    uint8_t *obs, double *reward, uint8_t *terminated, uint8_t *truncated, int32_t *status,
+                    int nthreads) {
+    const int ob = vs * vs * 3;
+#pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
+    for (int b = 0; b < B; ++b) {
+        int te = 0, tr = 0;
+        const size_t o = (size_t)b * HWp;
+        status[b] = orc_step(W, H, ty + o, co + o, st + o, state + 4 * b, carry + 2 * b, max_steps[b], see[b], vs,
+                             actions[b], obs + (size_t)b * ob, reward + b, &te, &tr);
+        terminated[b] = (uint8_t)te;
+        truncated[b] = (uint8_t)tr;
+    }
+}

@@ -41,6 +41,8 @@ def lib():
         L.orc_vi_ex.argtypes = [_I, _I, _I, _I, _I, _P, _D, _D, _D, _I, _I, _I, _D, _I, _P, _P, _P, _P, _P]
         L.orc_xyd_next_nodeath.argtypes = [_P, _I, _I, _I, _I, _D, _P, _P, _P]
         L.orc_reward.argtypes = [_I, _I]
+        L.orc_step_batch.argtypes = [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _I]
+        L.orc_step_batch.restype = None
         L.orc_reward.restype = _D
         _lib = L
     return _lib
@@ -133,6 +135,38 @@ def gen_obs(planes, agent, carry=(0, 0), see_through=False, view=7):
     lib().orc_gen_obs(W, H, _ptr(ty), _ptr(co), _ptr(st), int(agent[0]), int(agent[1]),
                       int(agent[2]), int(carry[0]), int(carry[1]), int(see_through), view, _ptr(img))
     return img
+
+
+class OracleBatch:
+    """B envs in the GPU engine's layout (row-major planes [B][HWp], agent [B][4]) stepped by the
+    oracle's MiniGridEnv.step restatement (orc_step_batch); the step path's CPU baseline."""
+
+    def __init__(self, enc: np.ndarray, agent: np.ndarray, max_steps, see_through, view=7):
+        enc = np.asarray(enc, np.uint8)  # (B, W, H, 3) x-major encodings
+        B, W, H, _ = enc.shape
+        self.B, self.W, self.H, self.view = B, W, H, view
+        self.HWp = (W * H + 15) // 16 * 16
+        planes = np.zeros((3, B, self.HWp), np.uint8)
+        for p in range(3):
+            planes[p, :, : W * H] = enc[..., p].transpose(0, 2, 1).reshape(B, W * H)
+        self.ty, self.co, self.st = (np.ascontiguousarray(planes[p]) for p in range(3))
+        self.state = np.zeros((B, 4), np.int32)
+        self.state[:, :3] = np.asarray(agent, np.int32)[:, :3]
+        self.carry = np.zeros((B, 2), np.int32)
+        self.max_steps = np.broadcast_to(np.asarray(max_steps, np.int32), (B,)).copy()
+        self.see = np.broadcast_to(np.asarray(see_through, np.uint8), (B,)).copy()
+        self.obs = np.zeros((B, view, view, 3), np.uint8)
+        self.reward = np.zeros(B, np.float64)
+        self.terminated = np.zeros(B, np.uint8)
+        self.truncated = np.zeros(B, np.uint8)
+        self.status = np.zeros(B, np.int32)
+
+    def step(self, actions: np.ndarray, nthreads: int = 1):
+        a = np.ascontiguousarray(actions, np.int32)
+        lib().orc_step_batch(self.B, self.W, self.H, self.HWp, _ptr(self.ty), _ptr(self.co), _ptr(self.st),
+                             _ptr(self.state), _ptr(self.carry), _ptr(self.max_steps), _ptr(self.see), self.view,
+                             _ptr(a), _ptr(self.obs), _ptr(self.reward), _ptr(self.terminated),
+                             _ptr(self.truncated), _ptr(self.status), int(nthreads))
 
 
 class OracleEnv:

@@ -129,3 +129,38 @@ def test_vector_autoreset():
     st = venv.get_state()
     assert (st["step_count"] == 0).all()
     venv.close()
+
+
+@pytest.mark.parametrize("env_id,view", [
+    ("MiniGrid-DoorKey-16x16-v0", 7), ("MiniGrid-FourRooms-v0", 7), ("MiniGrid-LavaCrossingS11N5-v0", 7),
+    ("MiniGrid-Empty-16x16-v0", 7), ("MiniGrid-DoorKey-5x5-v0", 7), ("MiniGrid-DoorKey-8x8-v0", 5),
+    ("MiniGrid-FourRooms-v0", 3), ("MiniGrid-LavaGapS7-v0", 5), ("MiniGrid-DistShift1-v0", 7),
+])
+def test_full_batch_random_actions_vs_batched_oracle(env_id, view):
+    """Every env of a 4096-env batch, every step: obs bytes, fp64 reward, flags, agent, carry and
+    step_count equal the oracle's step() restatement (orc_step_batch) on the same action stream;
+    the final grids too (pickup / drop / toggle mutations).  Covers agents at the grid border
+    (view windows outside the grid) and the 3 / 5 / 7 view sizes."""
+    B, steps = 4096, 96
+    venv = MiniGridVecEnv(env_id, B, agent_view_size=view)
+    venv.reset(seed=7)
+    st0 = venv.get_state()
+    ob = oracle.OracleBatch(st0["enc"], st0["agent"], venv.max_steps, venv.see_through, view)
+    rng = np.random.default_rng(3)
+    for t in range(steps):
+        a = rng.integers(0, 7, B).astype(np.int32)
+        obs, rew, term, trunc, _ = venv.step(a)
+        ob.step(a)
+        np.testing.assert_array_equal(obs["image"], ob.obs, err_msg=f"{env_id} step {t}")
+        np.testing.assert_array_equal(rew, ob.reward, err_msg=f"{env_id} step {t}")
+        np.testing.assert_array_equal(term, ob.terminated.astype(bool))
+        np.testing.assert_array_equal(trunc, ob.truncated.astype(bool))
+        np.testing.assert_array_equal(obs["direction"], ob.state[:, 2])
+    st = venv.get_state()
+    np.testing.assert_array_equal(st["agent"], ob.state[:, :3])
+    np.testing.assert_array_equal(st["carry"], ob.carry)
+    np.testing.assert_array_equal(st["step_count"], ob.state[:, 3])
+    W, H = ob.W, ob.H
+    enc = np.stack([p[:, : W * H].reshape(B, H, W).transpose(0, 2, 1) for p in (ob.ty, ob.co, ob.st)], axis=-1)
+    np.testing.assert_array_equal(st["enc"], enc)
+    venv.close()

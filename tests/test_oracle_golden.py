@@ -87,6 +87,28 @@ def test_step_trajectory_matches_reference(name):
         np.testing.assert_array_equal(env.encode(), t["final_enc"][k])
 
 
+@pytest.mark.parametrize("name", traj_names())
+def test_batched_oracle_step_matches_reference(name):
+    """orc_step_batch (the step path's CPU baseline) replays the reference trajectories, 4 envs at once."""
+    t = load(f"traj_{name}.npz")
+    n = t["actions"].shape[0]
+    ob = oracle.OracleBatch(t["init_enc"], t["init_agent"], t["max_steps"], SEE_THROUGH.get(name, False))
+    for i in range(t["actions"].shape[1]):
+        ob.step(t["actions"][:, i])
+        ctx = f"{name} step {i}"
+        assert (ob.status == 0).all(), ctx
+        np.testing.assert_array_equal(ob.obs, t["image"][:, i], err_msg=ctx)
+        np.testing.assert_array_equal(ob.reward, t["reward"][:, i], err_msg=ctx)
+        np.testing.assert_array_equal(ob.terminated, t["terminated"][:, i], err_msg=ctx)
+        np.testing.assert_array_equal(ob.truncated, t["truncated"][:, i], err_msg=ctx)
+        np.testing.assert_array_equal(ob.state[:, :3], t["agent"][:, i], err_msg=ctx)
+        np.testing.assert_array_equal(ob.carry, t["carry"][:, i], err_msg=ctx)
+    W, H = ob.W, ob.H
+    for k in range(n):
+        enc = np.stack([p[k, : W * H].reshape(H, W).T for p in (ob.ty, ob.co, ob.st)], axis=-1)
+        np.testing.assert_array_equal(enc, t["final_enc"][k])
+
+
 def test_unknown_action_raises():
     t = load("traj_empty5.npz")
     env = oracle.OracleEnv(t["init_enc"][0], t["init_agent"][0], 100, True)
