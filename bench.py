@@ -324,11 +324,16 @@ def _max_over_ranks(dist, red_dev, elapsed, units):
     return float(t.item()), float(u.item())
 
 
-def _timed_launches(args, launch, dist):
+def _timed_launches(args, launch, dist, stream=None):
     """W untimed launches, then K launches bracketed by barrier + synchronize, each launch between
-    a pair of events on the current stream (the stream the library launches on)."""
+    a pair of events on `stream`, the stream the library launches on (a torch Stream; None = the
+    current stream).  The events must be on the launch stream: events on another stream time
+    nothing (round-1 lesson: the legacy null stream handle 0 made the library create its own)."""
     import torch
 
+    if stream is not None:
+        with torch.cuda.stream(stream):
+            return _timed_launches(args, launch, dist)
     for i in range(args.warmup):
         launch(i)
     if dist is not None:
@@ -359,9 +364,9 @@ def step_bench(args, rank, world, local, dist, red_dev):
     B = spec["per_gpu"]
     venv = MiniGridVecEnv(spec["env_id"], B, device=local)
     venv.reset(seed=rank * B)  # reset(seed) for seeds [rank*B, (rank+1)*B), generated on the GPU
-    stream = torch.cuda.current_stream()
-    venv.set_stream(stream.cuda_stream)
     dev = torch.device("cuda", local)
+    stream = torch.cuda.Stream(device=dev)  # a real stream handle (0 would make the library use its own)
+    venv.set_stream(stream.cuda_stream)
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     acts = torch.randint(0, 7, (args.warmup + args.steps, B), generator=g, device=dev, dtype=torch.int32)
@@ -376,7 +381,8 @@ def step_bench(args, rank, world, local, dist, red_dev):
     def launch(i):
         venv.step_device(acts[i], obs, dirn, rew, term, trunc, status)
 
-    elapsed, kern_s = _timed_launches(args, launch, dist)
+    torch.cuda.synchronize()  # actions / outputs allocated on the default stream
+    elapsed, kern_s = _timed_launches(args, launch, dist, stream)
     assert int(status.max().item()) == 0, "step kernel reported an error status"
     elapsed_max, steps_total = _max_over_ranks(dist, red_dev, elapsed, float(B) * args.steps)
     out = None
@@ -441,12 +447,13 @@ def gen_bench(args, rank, world, local, dist, red_dev):
     enc = torch.empty((B, W, H, 3), dtype=torch.uint8, device=dev)
     cells = torch.empty((B, H, W), dtype=torch.uint8, device=dev)
     agent = torch.empty((B, 3), dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream().cuda_stream
+    stream = torch.cuda.Stream(device=dev)
 
     def launch(i):
-        gen.generate_device(env, rank * B, B, enc, cells, agent, device=local, stream=stream)
+        gen.generate_device(env, rank * B, B, enc, cells, agent, device=local, stream=stream.cuda_stream)
 
-    elapsed, kern_s = _timed_launches(args, launch, dist)
+    torch.cuda.synchronize()
+    elapsed, kern_s = _timed_launches(args, launch, dist, stream)
     assert int(agent[:, 2].min().item()) >= 0, "generator reported a placement failure"
     elapsed_max, total = _max_over_ranks(dist, red_dev, elapsed, float(B) * args.steps)
     out = None

@@ -239,46 +239,47 @@ struct StepOut {
 
 __device__ __forceinline__ StepOut step_one(const EnvGeo &g, const uint8_t *ty, const uint8_t *co, const uint8_t *st,
                                             int x, int y, int d, int sc, int ct, int cc, int a, int ms) {
-    StepOut o{x, y, d, sc + 1, ct, cc, MGDP_OK, 0, 0, 0, 0, 0, 0, 0, 0.0};  // step_count += 1 first (:523)
+    // Branch-free over the action (a wave steps envs with different actions): every effect is
+    // computed and selected.  step_count += 1 first (:523); an out-of-grid front cell fails before
+    // the action branch (Grid.get assert, :533), an unknown action after it (:579-580).
+    StepOut o{x, y, d, sc + 1, ct, cc, MGDP_OK, 0, 0, 0, 0, 0, 0, 0, 0.0};
     const int fx = x + kDX[d], fy = y + kDY[d];
-    // Grid.get asserts on the front cell (minigrid_env.py:533) before the action branch
-    if (fx < 0 || fy < 0 || fx >= g.W || fy >= g.H) { o.stat = MGDP_E_BOUNDS; return o; }
-    if (a < 0 || a > 6) { o.stat = MGDP_E_ACTION; return o; }
-    const int fi = fy * g.W + fx;
-    o.fi = fi;
-    const int ft = ty[fi];
+    const bool inb = (unsigned)fx < (unsigned)g.W && (unsigned)fy < (unsigned)g.H;
+    const bool act_ok = (unsigned)a <= 6u;
+    o.stat = !inb ? MGDP_E_BOUNDS : !act_ok ? MGDP_E_ACTION : MGDP_OK;
+    const int fi = inb ? fy * g.W + fx : 0;
+    const int ft = ty[fi], fc = co[fi], fs = st[fi];
+    const bool ok = o.stat == MGDP_OK;
     const bool fnone = ft == T_EMPTY;
-    if (a == 0) {
-        o.d = (d + 3) & 3;
-    } else if (a == 1) {
-        o.d = (d + 1) & 3;
-    } else if (a == 2) {
-        const bool overlap = ft == T_GOAL || ft == T_FLOOR || ft == T_LAVA || (ft == T_DOOR && st[fi] == D_OPEN);
-        if (fnone || overlap) { o.x = fx; o.y = fy; }
-        if (ft == T_GOAL) { o.term = 1; o.r = reward_fn(o.sc, ms); }
-        if (ft == T_LAVA) o.term = 1;
-    } else if (a == 3) {
-        if ((ft == T_KEY || ft == T_BALL || ft == T_BOX) && ct == 0) {
-            o.ct = ft; o.cc = co[fi];
-            o.mut = 1; o.nt = T_EMPTY; o.nc = 0; o.ns = 0;
-        }
-    } else if (a == 4) {
-        if (fnone && ct != 0) {
-            o.mut = 1; o.nt = ct; o.nc = cc; o.ns = 0;
-            o.ct = 0; o.cc = 0;
-        }
-    } else if (a == 5) {
-        if (ft == T_DOOR) {
-            const int s = st[fi];
-            if (s == D_LOCKED) {
-                if (ct == T_KEY && cc == co[fi]) { o.mut = 1; o.nt = ft; o.nc = co[fi]; o.ns = D_OPEN; }
-            } else {
-                o.mut = 1; o.nt = ft; o.nc = co[fi]; o.ns = s == D_OPEN ? D_CLOSED : D_OPEN;
-            }
-        } else if (ft == T_BOX) {  // Box(contains=None).toggle -> empty cell
-            o.mut = 1; o.nt = T_EMPTY; o.nc = 0; o.ns = 0;
-        }
-    }
+    // left / right (:536-541)
+    o.d = !ok ? d : a == 0 ? ((d + 3) & 3) : a == 1 ? ((d + 1) & 3) : d;
+    // forward (:544-553): can_overlap = Goal, Floor, Lava, open Door (world_object.py)
+    const bool fwd = ok && a == 2;
+    const uint32_t fb = 1u << (ft & 31);  // type bit: comparison chains are lowered to branches
+    const bool overlap = ((fb & ((1u << T_GOAL) | (1u << T_FLOOR) | (1u << T_LAVA))) != 0) | ((ft == T_DOOR) & (fs == D_OPEN));
+    const bool move = fwd && (fnone || overlap);
+    o.x = move ? fx : x;
+    o.y = move ? fy : y;
+    const bool goal = fwd && ft == T_GOAL;
+    o.term = goal || (fwd && ft == T_LAVA);
+    if (goal) o.r = reward_fn(o.sc, ms);
+    // pickup (:556-561): Key / Ball / Box, hands empty
+    const bool pickup = ok & (a == 3) & ((fb & ((1u << T_KEY) | (1u << T_BALL) | (1u << T_BOX))) != 0) & (ct == 0);
+    // drop (:564-568): front empty, carrying
+    const bool drop = ok && a == 4 && fnone && ct != 0;
+    // toggle (:571-575): Door.toggle (locked: needs the carried Key of its colour, unlocks and
+    // opens; else flips is_open, world_object.py:185-195); Box(contains=None).toggle -> empty
+    const bool tdoor = ok && a == 5 && ft == T_DOOR && (fs != D_LOCKED || (ct == T_KEY && cc == fc));
+    const bool tbox = ok && a == 5 && ft == T_BOX;
+    const bool clear = pickup || tbox;
+    o.mut = clear || drop || tdoor;
+    o.fi = fi;
+    o.nt = clear ? T_EMPTY : drop ? ct : ft;
+    o.nc = clear ? 0 : drop ? cc : fc;
+    o.ns = tdoor ? (fs == D_OPEN ? D_CLOSED : D_OPEN) : 0;
+    o.ct = pickup ? ft : drop ? 0 : ct;
+    o.cc = pickup ? fc : drop ? 0 : cc;
+    if (!ok) return o;
     if (o.sc >= ms) o.trunc = 1;
     if (g.nd_mask) {  // NoDeath.step: front cell before, agent's cell after the step (never mutated)
         const bool going = a == 2 && !fnone && ((g.nd_mask >> ft) & 1u);
@@ -352,6 +353,186 @@ envs_step_kernel(EnvGeo g, uint8_t *__restrict__ TY, uint8_t *__restrict__ CO, u
     copy_out(obs + (long long)e0 * obs_bytes, smem, n * obs_bytes);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Lane-group step kernel (the default): kGroup = 8 lanes per env, 32 envs per 256-thread
+// workgroup, so a 65536-env batch is 8192 waves (8 per SIMD) instead of 1024 one-thread-per-env
+// waves whose dependent HBM and LDS latencies nothing could hide.  Per env:
+//   * every lane of the group runs step_one on the same (broadcast) loads; lane 0 alone writes
+//     the per-env results and the front-cell mutation;
+//   * lane v < vs stages row v of the view box (3 planes, dword loads aligned with v_alignbyte)
+//     into the group's LDS window; the wave executes its LDS accesses in issue order, so the other
+//     lanes' rows are visible to the reads below without a barrier (the group is inside one wave);
+//   * lane i < vs owns view column i: its see-behind bits are OR-reduced over the group (xor
+//     shuffles), process_vis runs on the 64-bit mask in bit-parallel form (process_vis_bits), and
+//     the lane encodes its column -- obs bytes [3*vs*i, 3*vs*(i+1)) of the env, contiguous because
+//     the obs is x-major -- into the LDS obs tile, which leaves with 16-B coalesced stores.
+// Bit-identical to envs_step_kernel (tests/test_gpu_step.py runs both against the reference's
+// trajectories and the oracle).
+// ------------------------------------------------------------------------------------------------
+constexpr int kGroup = 8;
+constexpr int kGroupBlock = 256;
+constexpr int kGroupEnvs = kGroupBlock / kGroup;
+
+__device__ __forceinline__ uint32_t rev8(uint32_t v) { return __builtin_bitreverse32(v) >> 24; }
+
+// process_vis (grid.py:291-328) on the see-behind mask sb (bit j*8+i = view cell (i, j)), one row
+// per step from j = vs-1 up.  In row j the left-to-right pass visits i = 0..vs-2: a visible
+// see-behind cell makes i+1 visible and marks (i, j-1), (i+1, j-1).  Bit i's value when visited is
+// final for that pass (only i-1 can set it before), so the pass equals the closure of the row's
+// seeds m moving up through the see-behind run p = sb & [0, vs-2]: adding the seeds x = m & p to p
+// carries through each seeded run and sets the bit past its end, hence L = m | ((p + x) ^ p).  The
+// right-to-left pass (i = vs-1..1) is the same closure in bit-reversed order, seeded by L.  Checked
+// against the literal loop on 200k random masks for vs = 3, 5, 7 before use.
+template <int VS>
+__device__ __forceinline__ unsigned long long process_vis_bits(unsigned long long sb) {
+    constexpr uint32_t limL = (1u << (VS - 1)) - 1u;
+    constexpr uint32_t limR = ((1u << VS) - 1u) & ~1u;
+    unsigned long long mask = 0;
+    uint32_t up = 0;
+#pragma unroll
+    for (int j = VS - 1; j >= 0; --j) {
+        const uint32_t m = up | (j == VS - 1 ? 1u << (VS / 2) : 0u);
+        const uint32_t s = (uint32_t)(sb >> (8 * j)) & 0xffu;
+        const uint32_t p = s & limL;
+        const uint32_t L = m | ((p + (m & p)) ^ p);
+        const uint32_t g1 = L & p;
+        const uint32_t q = s & limR;
+        const uint32_t Lr = rev8(L), qr = rev8(q);
+        const uint32_t R = rev8(Lr | ((qr + (Lr & qr)) ^ qr));
+        const uint32_t g2 = R & q;
+        up = g1 | (g1 << 1) | g2 | (g2 >> 1);
+        mask |= (unsigned long long)R << (8 * j);
+    }
+    return mask;
+}
+
+__device__ __forceinline__ unsigned long long group_or(unsigned long long v) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#pragma unroll
+    for (int o = 1; o < kGroup; o <<= 1) {
+        lo |= (uint32_t)__shfl_xor((int)lo, o);
+        hi |= (uint32_t)__shfl_xor((int)hi, o);
+    }
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+template <int VS>
+__global__ void __launch_bounds__(kGroupBlock)
+envs_step_group_kernel(EnvGeo g, uint8_t *__restrict__ TY, uint8_t *__restrict__ CO, uint8_t *__restrict__ ST,
+                       int32_t *__restrict__ agent, int32_t *__restrict__ carry,
+                       const int32_t *__restrict__ max_steps, const uint8_t *__restrict__ see,
+                       const int32_t *__restrict__ actions, uint8_t *__restrict__ obs,
+                       int32_t *__restrict__ direction, double *__restrict__ reward,
+                       uint8_t *__restrict__ terminated, uint8_t *__restrict__ truncated,
+                       int32_t *__restrict__ status, int observe_only) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int OB = VS * VS * 3;            // obs bytes per env
+    constexpr int WD = 3 * VS * 2;             // window dwords per env (3 planes x VS rows x 8 B)
+    constexpr int RB = kWinRow;                // window row bytes
+    const int slot = threadIdx.x / kGroup, r = threadIdx.x % kGroup;
+    const int e0 = blockIdx.x * kGroupEnvs;
+    const int e = e0 + slot;
+    uint8_t *img = smem + slot * OB;
+    uint32_t *win = reinterpret_cast<uint32_t *>(smem + round_up(kGroupEnvs * OB, 16)) + slot * (WD + 1);
+    const uint8_t *wb = reinterpret_cast<const uint8_t *>(win);
+    if (e < g.B) {
+        uint8_t *ty = TY + (long long)e * g.HWp;
+        uint8_t *co = CO + (long long)e * g.HWp;
+        uint8_t *st = ST + (long long)e * g.HWp;
+        const int4 ag = reinterpret_cast<const int4 *>(agent)[e];
+        const int2 cr = reinterpret_cast<const int2 *>(carry)[e];
+        StepOut o{ag.x, ag.y, ag.z, ag.w, cr.x, cr.y, MGDP_OK, 0, 0, 0, 0, 0, 0, 0, 0.0};
+        if (!observe_only) o = step_one(g, ty, co, st, ag.x, ag.y, ag.z, ag.w, cr.x, cr.y, actions[e], max_steps[e]);
+        if (o.stat == MGDP_OK) {
+            int tlx, tly, bx, by;
+            view_box(o.x, o.y, o.d, VS, tlx, tly, bx, by);
+            if (r < VS) {  // lane r stages window row r
+                const int nd = g.HWp >> 2;
+                const int off = (by + r) * g.W + bx;
+                const int a = off >> 2;  // floor: off may be negative left of / above the grid
+                const int sh = off & 3;
+                const uint32_t *P[3] = {reinterpret_cast<const uint32_t *>(ty), reinterpret_cast<const uint32_t *>(co),
+                                        reinterpret_cast<const uint32_t *>(st)};
+                uint32_t w[3][3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) w[p][q] = P[p][min(max(a + q, 0), nd - 1)];  // only in-grid bytes are read
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    win[(p * VS + r) * 2 + 0] = __builtin_amdgcn_alignbyte(w[p][1], w[p][0], sh);
+                    win[(p * VS + r) * 2 + 1] = __builtin_amdgcn_alignbyte(w[p][2], w[p][1], sh);
+                }
+            }
+            asm volatile("" ::: "memory");
+            if (o.mut && r == 0) {  // the front cell as the step left it (in the view: the agent did not move)
+                const int fy = o.fi / g.W, fx = o.fi - fy * g.W;
+                const int w = (fy - by) * RB + (fx - bx);
+                uint8_t *wm = reinterpret_cast<uint8_t *>(win);
+                wm[w] = (uint8_t)o.nt; wm[VS * RB + w] = (uint8_t)o.nc; wm[2 * VS * RB + w] = (uint8_t)o.ns;
+                ty[o.fi] = (uint8_t)o.nt; co[o.fi] = (uint8_t)o.nc; st[o.fi] = (uint8_t)o.ns;
+            }
+            asm volatile("" ::: "memory");
+            const int fx = kDX[o.d], fy = kDY[o.d], rx = -fy, ry = fx;
+            const int i = r;
+            // Column i's world cells (wx0 - fx*j, wy0 - fy*j), read branch-free: an out-of-grid
+            // cell reads window byte 0 and is then replaced (out of bounds -> Wall, grid.py:136-139).
+            const int wx0 = tlx + rx * i, wy0 = tly + ry * i;
+            uint32_t tv[VS], cv[VS], sv[VS];
+            bool inb[VS];
+            unsigned long long sb = 0;
+#pragma unroll
+            for (int j = 0; j < VS; ++j) {
+                const int wx = wx0 - fx * j, wy = wy0 - fy * j;
+                inb[j] = i < VS && (unsigned)wx < (unsigned)g.W && (unsigned)wy < (unsigned)g.H;
+                const int ow = inb[j] ? (wy - by) * RB + (wx - bx) : 0;
+                tv[j] = wb[ow]; cv[j] = wb[VS * RB + ow]; sv[j] = wb[2 * VS * RB + ow];
+                // see_behind as bit tests (comparison chains are lowered to branches)
+                const uint32_t tb = 1u << (tv[j] & 31u);
+                const bool behind = !(tb & (1u << T_WALL)) & !((tb & (1u << T_DOOR)) && sv[j] != D_OPEN);
+                sb |= (unsigned long long)(inb[j] && behind) << (j * 8 + (i & 7));
+            }
+            sb = group_or(sb);
+            const unsigned long long mask = see[e] ? ~0ull : process_vis_bits<VS>(sb);
+            if (i < VS) {  // encode column i, grid.py:244-268; the carried object at (VS/2, VS-1)
+                uint8_t *col = img + i * VS * 3;
+                const bool centre_col = i == VS / 2;
+#pragma unroll
+                for (int j = 0; j < VS; ++j) {
+                    uint32_t t = inb[j] ? tv[j] : (uint32_t)T_WALL;
+                    uint32_t c = inb[j] ? (tv[j] == T_EMPTY ? 0u : cv[j]) : (uint32_t)C_GREY;
+                    uint32_t s = inb[j] && tv[j] != T_EMPTY ? sv[j] : 0u;
+                    if (j == VS - 1 && centre_col) {
+                        t = o.ct > 0 ? (uint32_t)o.ct : (uint32_t)T_EMPTY;
+                        c = o.ct > 0 ? (uint32_t)o.cc : 0u;
+                        s = 0;
+                    }
+                    const bool vis = (mask >> (j * 8 + i)) & 1ull;
+                    col[3 * j] = (uint8_t)(vis ? t : 0u);
+                    col[3 * j + 1] = (uint8_t)(vis ? c : 0u);
+                    col[3 * j + 2] = (uint8_t)(vis ? s : 0u);
+                }
+            }
+        } else if (r < VS) {
+            for (int k = 0; k < 3 * VS; ++k) img[r * VS * 3 + k] = 0;
+        }
+        if (r == 0) {
+            if (!observe_only) {
+                reinterpret_cast<int4 *>(agent)[e] = make_int4(o.x, o.y, o.d, o.sc);
+                reinterpret_cast<int2 *>(carry)[e] = make_int2(o.ct, o.cc);
+                reward[e] = o.r;
+                terminated[e] = (uint8_t)o.term;
+                truncated[e] = (uint8_t)o.trunc;
+                status[e] = o.stat;
+            }
+            direction[e] = o.d;
+        }
+    }
+    __syncthreads();
+    const int n = min(kGroupEnvs, g.B - e0);
+    copy_out(obs + (long long)e0 * OB, smem, n * OB);
+}
+
 }  // namespace mgdp
 
 using namespace mgdp;
@@ -367,7 +548,10 @@ struct mgdp_envs {
     double *d_rew = nullptr;
     uint32_t nd_mask = 0;
     double death_cost = -1.0;
-    bool win = true;  // windowed gen_obs (MGDP_STEP_WIN=0: the per-cell HBM byte loads of gen_obs_one)
+    // step kernel: 0 = envs_step_group_kernel (8 lanes per env, default), 1 = envs_step_kernel with
+    // the staged window, 2 = envs_step_kernel with per-cell HBM byte loads (gen_obs_one).
+    // MGDP_STEP_KERNEL=group|thread|thread_bytes selects one (measured alternatives, all tested).
+    int kmode = 0;
 };
 
 namespace {
@@ -376,11 +560,20 @@ EnvGeo env_geo(const mgdp_envs *E) { return EnvGeo{E->B, E->W, E->H, E->HWp, E->
 
 int launch_step(mgdp_envs *E, const int32_t *d_act, uint8_t *d_obs, int32_t *d_dir, double *d_rew,
                 uint8_t *d_term, uint8_t *d_trunc, int32_t *d_status, int observe_only) {
-    const int grid = (E->B + kStepBlock - 1) / kStepBlock;
-    const int smem = (int)round_up(kStepBlock * E->vs * E->vs * 3, 16) + kStepBlock * win_stride(E->vs);
-    hipLaunchKernelGGL(E->win ? envs_step_kernel<true> : envs_step_kernel<false>, dim3(grid), dim3(kStepBlock), smem, E->stream, env_geo(E),
-                       E->d_ty, E->d_co, E->d_st, E->d_agent, E->d_carry, E->d_max, E->d_see, d_act,
-                       d_obs, d_dir, d_rew, d_term, d_trunc, d_status, observe_only);
+    if (E->kmode == 0) {
+        const int grid = (E->B + kGroupEnvs - 1) / kGroupEnvs;
+        const int smem = (int)round_up(kGroupEnvs * E->vs * E->vs * 3, 16) + kGroupEnvs * (3 * E->vs * 2 + 1) * 4;
+        auto k = E->vs == 7 ? envs_step_group_kernel<7> : E->vs == 5 ? envs_step_group_kernel<5> : envs_step_group_kernel<3>;
+        hipLaunchKernelGGL(k, dim3(grid), dim3(kGroupBlock), smem, E->stream, env_geo(E),
+                           E->d_ty, E->d_co, E->d_st, E->d_agent, E->d_carry, E->d_max, E->d_see, d_act,
+                           d_obs, d_dir, d_rew, d_term, d_trunc, d_status, observe_only);
+    } else {
+        const int grid = (E->B + kStepBlock - 1) / kStepBlock;
+        const int smem = (int)round_up(kStepBlock * E->vs * E->vs * 3, 16) + kStepBlock * win_stride(E->vs);
+        hipLaunchKernelGGL(E->kmode == 1 ? envs_step_kernel<true> : envs_step_kernel<false>, dim3(grid), dim3(kStepBlock), smem, E->stream, env_geo(E),
+                           E->d_ty, E->d_co, E->d_st, E->d_agent, E->d_carry, E->d_max, E->d_see, d_act,
+                           d_obs, d_dir, d_rew, d_term, d_trunc, d_status, observe_only);
+    }
     MGDP_HIP(hipGetLastError());
     return 0;
 }
@@ -397,11 +590,18 @@ int mgdp_envs_create(int32_t device, int32_t B, int32_t W, int32_t H, int32_t vi
     int ndev = 0;
     MGDP_HIP(hipGetDeviceCount(&ndev));
     MGDP_CHECK(device >= 0 && device < ndev, MGDP_E_HIP, "device %d not available (%d visible)", device, ndev);
+    int kmode = 0;
+    if (const char *ev = std::getenv("MGDP_STEP_KERNEL")) {
+        const std::string m(ev);
+        MGDP_CHECK(m == "group" || m == "thread" || m == "thread_bytes", MGDP_E_INVALID,
+                   "MGDP_STEP_KERNEL must be group, thread or thread_bytes (got %s)", ev);
+        kmode = m == "group" ? 0 : m == "thread" ? 1 : 2;
+    }
     DeviceGuard guard(device);
     mgdp_envs *E = new mgdp_envs();
     E->device = device; E->B = B; E->W = W; E->H = H; E->HW = W * H; E->HWp = (int)round_up(W * H, 16);
     E->vs = view_size;
-    if (const char *ev = std::getenv("MGDP_STEP_WIN")) E->win = std::atoi(ev) != 0;
+    E->kmode = kmode;
     const size_t P = (size_t)B * E->HWp;
     hipError_t e = hipSuccess;
     auto al = [&](void **p, size_t n) { if (e == hipSuccess) e = hipMalloc(p, n); };

@@ -27,8 +27,13 @@ def grid_digest(enc):
     return np.frombuffer(hashlib.sha256(enc.tobytes()).digest()[:8], dtype=np.uint64)[0]
 
 
+STEP_KERNELS = ["group", "thread", "thread_bytes"]  # MGDP_STEP_KERNEL (csrc/envs.hip), read at create
+
+
+@pytest.mark.parametrize("kernel", STEP_KERNELS)
 @pytest.mark.parametrize("name", traj_names())
-def test_batched_step_matches_reference_trajectories(name):
+def test_batched_step_matches_reference_trajectories(name, kernel, monkeypatch):
+    monkeypatch.setenv("MGDP_STEP_KERNEL", kernel)
     t = load(f"traj_{name}.npz")
     B = t["actions"].shape[0]
     venv = MiniGridVecEnv(IDS[name], B)
@@ -136,12 +141,14 @@ def test_vector_autoreset():
     ("MiniGrid-Empty-16x16-v0", 7), ("MiniGrid-DoorKey-5x5-v0", 7), ("MiniGrid-DoorKey-8x8-v0", 5),
     ("MiniGrid-FourRooms-v0", 3), ("MiniGrid-LavaGapS7-v0", 5), ("MiniGrid-DistShift1-v0", 7),
 ])
-def test_full_batch_random_actions_vs_batched_oracle(env_id, view):
+@pytest.mark.parametrize("kernel", STEP_KERNELS)
+def test_full_batch_random_actions_vs_batched_oracle(env_id, view, kernel, monkeypatch):
     """Every env of a 4096-env batch, every step: obs bytes, fp64 reward, flags, agent, carry and
     step_count equal the oracle's step() restatement (orc_step_batch) on the same action stream;
     the final grids too (pickup / drop / toggle mutations).  Covers agents at the grid border
     (view windows outside the grid) and the 3 / 5 / 7 view sizes."""
-    B, steps = 4096, 96
+    monkeypatch.setenv("MGDP_STEP_KERNEL", kernel)
+    B, steps = 4096 + 5, 96  # not a multiple of any kernel's envs per workgroup
     venv = MiniGridVecEnv(env_id, B, agent_view_size=view)
     venv.reset(seed=7)
     st0 = venv.get_state()

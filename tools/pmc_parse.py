@@ -20,6 +20,14 @@ RUNS = {
     "doorkey65536_fused": ("doorkey65536/fused/cell/f32", "vi_fused_kernel", None),
     "lava65536_fused": ("lava65536/fused/cell/f32", "vi_fused_kernel", None),
     "fourrooms4096_fused": ("fourrooms4096/fused/cell/f32", "vi_fused_kernel", None),
+    # step / generator side benches (tools/pmc_side.sh); dword-wide scattered reads: the x2
+    # correction is calibrated for 16-B streaming reads only (raw value kept beside it)
+    "step_doorkey16x65536": ("step_doorkey16x65536/step", "envs_step_group_kernel", None),
+    "step_fourrooms65536": ("step_fourrooms65536/step", "envs_step_group_kernel", None),
+    "step_lava65536": ("step_lava65536/step", "envs_step_group_kernel", None),
+    "gen_lava65536": ("gen_lava65536/gen", "gen_grids_kernel", None),
+    "gen_fourrooms65536": ("gen_fourrooms65536/gen", "gen_grids_kernel", None),
+    "gen_doorkey16x65536": ("gen_doorkey16x65536/gen", "gen_grids_kernel", None),
 }
 
 
@@ -31,7 +39,7 @@ def per_dispatch(path, kernel):
     return vals
 
 
-res = {}
+res = json.load(open(OUT)) if os.path.exists(OUT) else {}  # merge: passes come from several calls
 for run, (key, kernel, solves) in RUNS.items():
     if not os.path.isdir(os.path.join(SRC, f"{run}_FETCH_SIZE")):
         continue
@@ -51,6 +59,9 @@ for run, (key, kernel, solves) in RUNS.items():
         "bytes_per_launch": 2.0 * fetch + write,
         "note": "2*FETCH_SIZE + WRITE_SIZE per launch (gfx950 FETCH_SIZE half-count correction)",
     }
+    if run.startswith(("step_", "gen_")):
+        res[key]["note"] += "; dword/byte-wide accesses: the x2 is calibrated for 16-B streaming reads only"
+        res[key]["src"] = SRC
     if solves:  # one resident launch served `solves` requests (bench.py scales per solve)
         res[key]["solves_per_launch"] = solves
         res[key]["bytes_per_solve"] = res[key]["bytes_per_launch"] / solves
