@@ -378,11 +378,36 @@ def step_bench(args, rank, world, local, dist, red_dev):
     trunc = torch.empty(B, dtype=torch.uint8, device=dev)
     status = torch.empty(B, dtype=torch.int32, device=dev)
 
+    # raw device pointers: the per-launch host cost is the ctypes call alone
+    act_ptrs = [acts[i].data_ptr() for i in range(acts.shape[0])]
+    outs = tuple(t.data_ptr() for t in (obs, dirn, rew, term, trunc, status))
+
     def launch(i):
-        venv.step_device(acts[i], obs, dirn, rew, term, trunc, status)
+        venv.step_device(act_ptrs[i], *outs)
 
     torch.cuda.synchronize()  # actions / outputs allocated on the default stream
-    elapsed, kern_s = _timed_launches(args, launch, dist, stream)
+    # Kernel time: one HIP event pair on the launch stream around the K back-to-back launches.  The
+    # host issues a launch in less time than the kernel runs (tools/probe_step: 2.7 us per call vs
+    # 11 us), so the stream stays busy and (end - start) / K is the launch duration plus the
+    # inter-dispatch gap -- a conservative per-launch time.  Per-launch event pairs
+    # (mgdp_envs_enable_timing) cost ~8 us of host time per launch and would throttle the loop.
+    for i in range(args.warmup):
+        launch(i)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(args.steps):
+        launch(args.warmup + i)
+    ev1.record(stream)
+    stream.synchronize()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_s = ev0.elapsed_time(ev1) / 1000.0
     assert int(status.max().item()) == 0, "step kernel reported an error status"
     elapsed_max, steps_total = _max_over_ranks(dist, red_dev, elapsed, float(B) * args.steps)
     out = None
@@ -403,7 +428,8 @@ def step_bench(args, rank, world, local, dist, red_dev):
                          "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                          "traffic": load_traffic(f"{args.workload}/step", 1.0), "launches": args.steps,
                          "avg_launch_us": avg * 1e6, "alg_bytes_per_launch": bpe * B,
-                         "alg_bytes_per_env_step": bpe},
+                         "alg_bytes_per_env_step": bpe,
+                         "timing": "one event pair on the launch stream around the K launches / K"},
         }
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = step_cpu_baseline(venv, acts, args.cpu_budget)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MGDP_ABI_VERSION 2
+#define MGDP_ABI_VERSION 3
 
 enum {
     MGDP_OK = 0,
@@ -185,6 +185,11 @@ int mgdp_envs_step(mgdp_envs *envs, const int32_t *actions, uint8_t *obs, int32_
 int mgdp_envs_step_device(mgdp_envs *envs, const int32_t *d_actions, uint8_t *d_obs,
                           int32_t *d_direction, double *d_reward, uint8_t *d_terminated,
                           uint8_t *d_truncated, int32_t *d_status);
+/* HIP-event timing of the step kernel launches (begin/end timestamps of each dispatch, as the
+ * rocprofv3 kernel trace reports them); kernel_time synchronises the stream and returns the total
+ * since enable_timing. */
+int mgdp_envs_enable_timing(mgdp_envs *envs, int32_t on);
+int mgdp_envs_kernel_time(mgdp_envs *envs, double *total_ms, int64_t *launches);
 /* Read back env state: enc B*W*H*3 (x-major), agent B*3, carry B*2 (type,color; 0 = none),
  * step_count B.  Any pointer may be NULL. */
 int mgdp_envs_get_state(mgdp_envs *envs, uint8_t *enc, int32_t *agent, int32_t *carry,

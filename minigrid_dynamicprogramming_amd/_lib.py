@@ -99,6 +99,8 @@ SIGNATURES = {
     "mgdp_envs_observe": (ctypes.c_int, [_P, _P, _P]),
     "mgdp_envs_step": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P]),
     "mgdp_envs_step_device": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P]),
+    "mgdp_envs_enable_timing": (ctypes.c_int, [_P, _I32]),
+    "mgdp_envs_kernel_time": (ctypes.c_int, [_P, _DP, _I64P]),
     "mgdp_envs_get_state": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "mgdp_envs_set_state": (ctypes.c_int, [_P, _P, _P, _P, _P]),
 }
@@ -124,7 +126,7 @@ def load():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.mgdp_abi_version() != 2:
+    if L.mgdp_abi_version() != 3:
         raise MgdpError("libmgdp ABI version mismatch")
     _lib = L
     return L
@@ -159,9 +161,9 @@ def require_gpu():
 
 
 def ptr(a) -> ctypes.c_void_p:
-    """Pointer of a contiguous numpy array or a torch tensor (host or device)."""
-    if a is None:
-        return None
+    """Pointer of a contiguous numpy array or a torch tensor (host or device); ints pass through."""
+    if a is None or isinstance(a, int):
+        return a
     if hasattr(a, "data_ptr"):
         return ctypes.c_void_p(a.data_ptr())
     return a.ctypes.data_as(ctypes.c_void_p)

@@ -4,20 +4,23 @@
 // :448-479 (get_view_exts), :235-240 (_reward); minigrid/core/grid.py:110-143 (rotate_left,
 // slice), :244-268 (encode), :291-328 (process_vis); minigrid/core/world_object.py (cell
 // predicates, Door.toggle :185-195, Box.toggle :291-294).  Pinned by tests/test_gpu_step.py against
-// 256-step trajectories captured from the reference (tests/golden/traj_*.npz).
+// 256-step trajectories captured from the reference (tests/golden/traj_*.npz) and against the
+// oracle's step() restatement on 4096-env batches.
 //
 // Layout in HBM (B envs of W x H):
-//   ty, co, st  uint8 [B][HWp]   OBJECT_TO_IDX / COLOR_TO_IDX / door state per cell, row-major
+//   cell        uint8 [B][HWp]   one-byte cell code (type, colour, state), row-major, see cell_code
 //   agent       int32 [B][4]     x, y, dir, step_count
 //   carry       int32 [B][2]     carried (type, colour); type 0 = nothing
 //   max_steps   int32 [B], see uint8 [B] (see_through_walls)
-// One thread per env.  The V x V view is never materialised: view cell (i, j) maps to world
-// top_left - f*j + r*i (f = DIR_TO_VEC[dir], r = right_vec, minigrid_env.py:421-446), which equals
-// the reference's slice + (dir+1) x rotate_left; process_vis runs on a 64-bit visibility mask.
-// Observations are assembled in LDS and leave with 16-byte coalesced stores.
+// One step = one envs_step_kernel launch: 8 lanes per env (see the kernel).  The V x V view is
+// never materialised: view cell (i, j) maps to world top_left - f*j + r*i (f = DIR_TO_VEC[dir],
+// r = right_vec, minigrid_env.py:421-446), which equals the reference's slice + (dir+1) x
+// rotate_left; process_vis runs on a 64-bit visibility mask.
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+
+#include <hip/hip_ext.h>
 
 #include "common.h"
 
@@ -32,78 +35,24 @@ struct EnvGeo {
     double death_cost;
 };
 
-constexpr int kStepBlock = 64;  // envs per workgroup; obs staging = 64 * 147 B (16-B multiple)
-
-__device__ __forceinline__ bool see_behind(int t, int s) {
-    if (t == T_WALL) return false;
-    if (t == T_DOOR) return s == D_OPEN;
-    return true;
+// One-byte cell code.  Grid.encode() (grid.py:244-268) gives every cell (type, colour, state) with
+// type <= 10, colour <= 5 and state != 0 only for doors (WorldObj.encode returns state 0,
+// Door.encode :197-213 open 0 / closed 1 / locked 2), so a cell fits a byte: type*8 + colour, or
+// 0x80 | state*8 + colour for a door.  One plane instead of three cuts the bytes the view windows
+// pull from HBM by 3x (the window rows are read at cache-line granularity, i.e. most of each grid).
+__host__ __device__ inline uint32_t cell_code(int t, int c, int s) {
+    return t == T_DOOR ? 0x80u | ((uint32_t)s << 3) | (uint32_t)c : ((uint32_t)t << 3) | (uint32_t)c;
 }
-
-// gen_obs for one env into `img` (vs*vs*3 bytes, x-major [i][j][3]) in LDS.
-__device__ void gen_obs_one(const EnvGeo &g, const uint8_t *ty, const uint8_t *co, const uint8_t *st,
-                            int ax, int ay, int d, int ct, int cc, bool see_through, uint8_t *img) {
-    const int vs = g.vs, hs = vs / 2;
-    const int fx = kDX[d], fy = kDY[d];
-    const int rx = -fy, ry = fx;
-    const int tlx = ax + fx * (vs - 1) - rx * hs;
-    const int tly = ay + fy * (vs - 1) - ry * hs;
-    // see-behind mask, bit (j*8 + i)
-    unsigned long long sb = 0, mask = 0;
-    for (int j = 0; j < vs; ++j)
-        for (int i = 0; i < vs; ++i) {
-            const int wx = tlx - fx * j + rx * i, wy = tly - fy * j + ry * i;
-            bool s = false;  // out of bounds -> Wall (grid.py:136-139)
-            if (wx >= 0 && wy >= 0 && wx < g.W && wy < g.H) {
-                const int idx = wy * g.W + wx;
-                s = see_behind(ty[idx], st[idx]);
-            }
-            if (s) sb |= 1ull << (j * 8 + i);
-        }
-    if (see_through) {
-        mask = ~0ull;
-    } else {  // process_vis, grid.py:291-328, literal loop order
-        mask = 1ull << ((vs - 1) * 8 + hs);
-        for (int j = vs - 1; j >= 0; --j) {
-            for (int i = 0; i < vs - 1; ++i) {
-                const unsigned long long b = 1ull << (j * 8 + i);
-                if (!(mask & b) || !(sb & b)) continue;
-                mask |= b << 1;
-                if (j > 0) mask |= (b << 1 >> 8) | (b >> 8);
-            }
-            for (int i = vs - 1; i >= 1; --i) {
-                const unsigned long long b = 1ull << (j * 8 + i);
-                if (!(mask & b) || !(sb & b)) continue;
-                mask |= b >> 1;
-                if (j > 0) mask |= (b >> 1 >> 8) | (b >> 8);
-            }
-        }
-    }
-    // encode, grid.py:244-268 (None -> (1,0,0), hidden -> (0,0,0)); carried object at (hs, vs-1)
-    for (int i = 0; i < vs; ++i)
-        for (int j = 0; j < vs; ++j) {
-            uint8_t *o = img + (i * vs + j) * 3;
-            int t = 0, c = 0, s = 0;
-            if (mask & (1ull << (j * 8 + i))) {
-                if (i == hs && j == vs - 1) {
-                    if (ct > 0) { t = ct; c = cc; } else { t = T_EMPTY; }
-                } else {
-                    const int wx = tlx - fx * j + rx * i, wy = tly - fy * j + ry * i;
-                    if (wx >= 0 && wy >= 0 && wx < g.W && wy < g.H) {
-                        const int idx = wy * g.W + wx;
-                        t = ty[idx];
-                        if (t != T_EMPTY) { c = co[idx]; s = st[idx]; }
-                    } else {
-                        t = T_WALL; c = C_GREY;
-                    }
-                }
-            }
-            o[0] = (uint8_t)t; o[1] = (uint8_t)c; o[2] = (uint8_t)s;
-        }
+__host__ __device__ inline void cell_decode(uint32_t code, int &t, int &c, int &s) {
+    const bool door = (code & 0x80u) != 0;
+    t = door ? (int)T_DOOR : (int)(code >> 3);
+    c = (int)(code & 7u);
+    s = door ? (int)((code >> 3) & 3u) : 0;
 }
+constexpr uint32_t kCodeWall = (uint32_t)T_WALL * 8u + (uint32_t)C_GREY;  // padding / out-of-grid filler
 
 __device__ __forceinline__ void copy_out(uint8_t *dst, const uint8_t *src, int bytes) {
-    // dst is 16-B aligned when the block starts at a multiple of kStepBlock envs (147*64 = 9408)
+    // dst is 16-B aligned: a workgroup's first env is a multiple of 32 (32*147 = 4704 = 16*294)
     if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0 && (bytes & 15) == 0) {
         const uint4 *s = reinterpret_cast<const uint4 *>(src);
         uint4 *d = reinterpret_cast<uint4 *>(dst);
@@ -120,18 +69,10 @@ __device__ __forceinline__ double reward_fn(int sc, int ms) {
     return 1.0 - t;
 }
 
-// ------------------------------------------------------------------------------------------------
-// Windowed gen_obs.  The view's vs x vs cells always cover an axis-aligned world box
-// [bx, bx+vs) x [by, by+vs) (rotation only permutes them), so the thread stages that box of the
-// three planes into its own LDS window with 3*vs*3 independent dword loads (all in flight at
-// once; byte-aligned with v_alignbyte so window cell (u, v) is byte u of row v) instead of ~5*vs*vs
-// dependent byte loads from HBM, and the visibility and encode passes read LDS.  Rows outside the
-// grid are loaded from a clamped address and never read (bounds are tested in world coordinates,
-// exactly as gen_obs_one does).  Bit-identical to gen_obs_one.
-// ------------------------------------------------------------------------------------------------
-constexpr int kWinRow = 8;                    // bytes per staged window row (vs <= 7)
-__host__ __device__ constexpr int win_stride(int vs) { return 3 * vs * kWinRow + 4; }  // odd dword count
+constexpr int kWinRow = 8;  // bytes per staged window row (vs + 1 <= 8 columns)
 
+// The view's vs x vs cells always cover the axis-aligned world box [bx, bx+vs) x [by, by+vs)
+// (rotation only permutes them); (tlx, tly) is the view's top-left (get_view_exts, :448-479).
 __device__ __forceinline__ void view_box(int ax, int ay, int d, int vs, int &tlx, int &tly, int &bx, int &by) {
     const int hs = vs / 2;
     const int fx = kDX[d], fy = kDY[d], rx = -fy, ry = fx;
@@ -141,104 +82,18 @@ __device__ __forceinline__ void view_box(int ax, int ay, int d, int vs, int &tlx
     by = tly + min(0, -fy * (vs - 1)) + min(0, ry * (vs - 1));
 }
 
-template <int VS>
-__device__ __forceinline__ void stage_window(const EnvGeo &g, const uint8_t *ty, const uint8_t *co, const uint8_t *st,
-                                             int bx, int by, uint32_t *win) {
-    const int nd = g.HWp >> 2;
-    const uint32_t *P[3] = {reinterpret_cast<const uint32_t *>(ty), reinterpret_cast<const uint32_t *>(co),
-                            reinterpret_cast<const uint32_t *>(st)};
-    uint32_t w[3][VS][3];
-#pragma unroll
-    for (int v = 0; v < VS; ++v) {
-        const int o = (by + v) * g.W + bx;
-        const int a = o >> 2;  // floor(o / 4): o may be negative left of / above the grid
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            const int idx = min(max(a + q, 0), nd - 1);  // only bytes of in-grid cells are ever read
-#pragma unroll
-            for (int p = 0; p < 3; ++p) w[p][v][q] = P[p][idx];
-        }
-    }
-#pragma unroll
-    for (int v = 0; v < VS; ++v) {
-        const int sh = ((by + v) * g.W + bx) & 3;
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-            win[(p * VS + v) * 2 + 0] = __builtin_amdgcn_alignbyte(w[p][v][1], w[p][v][0], sh);
-            win[(p * VS + v) * 2 + 1] = __builtin_amdgcn_alignbyte(w[p][v][2], w[p][v][1], sh);
-        }
-    }
-}
-
-// gen_obs_one on the staged window `wb` (plane p, row v, column u at wb[(p*vs + v)*8 + u]).
-__device__ void gen_obs_win(const EnvGeo &g, const uint8_t *wb, int tlx, int tly, int bx, int by, int d, int ct,
-                            int cc, bool see_through, uint8_t *img) {
-    const int vs = g.vs, hs = vs / 2;
-    const int fx = kDX[d], fy = kDY[d];
-    const int rx = -fy, ry = fx;
-    const uint8_t *WT = wb, *WC = wb + vs * kWinRow, *WS = wb + 2 * vs * kWinRow;
-    unsigned long long sb = 0, mask = 0;
-    for (int j = 0; j < vs; ++j)
-        for (int i = 0; i < vs; ++i) {
-            const int wx = tlx - fx * j + rx * i, wy = tly - fy * j + ry * i;
-            bool s = false;  // out of bounds -> Wall (grid.py:136-139)
-            if (wx >= 0 && wy >= 0 && wx < g.W && wy < g.H) {
-                const int o = (wy - by) * kWinRow + (wx - bx);
-                s = see_behind(WT[o], WS[o]);
-            }
-            if (s) sb |= 1ull << (j * 8 + i);
-        }
-    if (see_through) {
-        mask = ~0ull;
-    } else {  // process_vis, grid.py:291-328, literal loop order
-        mask = 1ull << ((vs - 1) * 8 + hs);
-        for (int j = vs - 1; j >= 0; --j) {
-            for (int i = 0; i < vs - 1; ++i) {
-                const unsigned long long b = 1ull << (j * 8 + i);
-                if (!(mask & b) || !(sb & b)) continue;
-                mask |= b << 1;
-                if (j > 0) mask |= (b << 1 >> 8) | (b >> 8);
-            }
-            for (int i = vs - 1; i >= 1; --i) {
-                const unsigned long long b = 1ull << (j * 8 + i);
-                if (!(mask & b) || !(sb & b)) continue;
-                mask |= b >> 1;
-                if (j > 0) mask |= (b >> 1 >> 8) | (b >> 8);
-            }
-        }
-    }
-    for (int i = 0; i < vs; ++i)
-        for (int j = 0; j < vs; ++j) {
-            uint8_t *o = img + (i * vs + j) * 3;
-            int t = 0, c = 0, s = 0;
-            if (mask & (1ull << (j * 8 + i))) {
-                if (i == hs && j == vs - 1) {
-                    if (ct > 0) { t = ct; c = cc; } else { t = T_EMPTY; }
-                } else {
-                    const int wx = tlx - fx * j + rx * i, wy = tly - fy * j + ry * i;
-                    if (wx >= 0 && wy >= 0 && wx < g.W && wy < g.H) {
-                        const int w = (wy - by) * kWinRow + (wx - bx);
-                        t = WT[w];
-                        if (t != T_EMPTY) { c = WC[w]; s = WS[w]; }
-                    } else {
-                        t = T_WALL; c = C_GREY;
-                    }
-                }
-            }
-            o[0] = (uint8_t)t; o[1] = (uint8_t)c; o[2] = (uint8_t)s;
-        }
-}
-
 // One env step: MiniGridEnv.step (minigrid_env.py:520-590) on registers; the front-cell mutation
 // of pickup / drop / toggle is returned (mut, nt/nc/ns) instead of written, so the caller orders it
-// against the window staging.
+// against the window it stages.
 struct StepOut {
     int x, y, d, sc, ct, cc, stat, term, trunc, mut, fi, nt, nc, ns;
     double r;
 };
 
-__device__ __forceinline__ StepOut step_one(const EnvGeo &g, const uint8_t *ty, const uint8_t *co, const uint8_t *st,
-                                            int x, int y, int d, int sc, int ct, int cc, int a, int ms) {
+// Rd: cell reader, rd(x, y) -> (type, colour, state) of in-grid cell (x, y) of this env.
+template <typename Rd>
+__device__ __forceinline__ StepOut step_core(const EnvGeo &g, const Rd &rd, int x, int y, int d, int sc, int ct,
+                                             int cc, int a, int ms) {
     // Branch-free over the action (a wave steps envs with different actions): every effect is
     // computed and selected.  step_count += 1 first (:523); an out-of-grid front cell fails before
     // the action branch (Grid.get assert, :533), an unknown action after it (:579-580).
@@ -248,7 +103,8 @@ __device__ __forceinline__ StepOut step_one(const EnvGeo &g, const uint8_t *ty, 
     const bool act_ok = (unsigned)a <= 6u;
     o.stat = !inb ? MGDP_E_BOUNDS : !act_ok ? MGDP_E_ACTION : MGDP_OK;
     const int fi = inb ? fy * g.W + fx : 0;
-    const int ft = ty[fi], fc = co[fi], fs = st[fi];
+    int ft, fc, fs;
+    rd(inb ? fx : 0, inb ? fy : 0, ft, fc, fs);
     const bool ok = o.stat == MGDP_OK;
     const bool fnone = ft == T_EMPTY;
     // left / right (:536-541)
@@ -283,7 +139,8 @@ __device__ __forceinline__ StepOut step_one(const EnvGeo &g, const uint8_t *ty, 
     if (o.sc >= ms) o.trunc = 1;
     if (g.nd_mask) {  // NoDeath.step: front cell before, agent's cell after the step (never mutated)
         const bool going = a == 2 && !fnone && ((g.nd_mask >> ft) & 1u);
-        const int ct_now = ty[o.y * g.W + o.x];
+        int ct_now, c_now, s_now;
+        rd(o.x, o.y, ct_now, c_now, s_now);
         const bool in_death = ct_now != T_EMPTY && ((g.nd_mask >> ct_now) & 1u);
         if (o.term && (going || in_death)) {
             o.term = 0;
@@ -293,85 +150,25 @@ __device__ __forceinline__ StepOut step_one(const EnvGeo &g, const uint8_t *ty, 
     return o;
 }
 
-template <bool WIN>
-__global__ void __launch_bounds__(kStepBlock)
-envs_step_kernel(EnvGeo g, uint8_t *__restrict__ TY, uint8_t *__restrict__ CO, uint8_t *__restrict__ ST,
-                 int32_t *__restrict__ agent, int32_t *__restrict__ carry,
-                 const int32_t *__restrict__ max_steps, const uint8_t *__restrict__ see,
-                 const int32_t *__restrict__ actions, uint8_t *__restrict__ obs,
-                 int32_t *__restrict__ direction, double *__restrict__ reward,
-                 uint8_t *__restrict__ terminated, uint8_t *__restrict__ truncated,
-                 int32_t *__restrict__ status, int observe_only) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int obs_bytes = g.vs * g.vs * 3;
-    const int e0 = blockIdx.x * kStepBlock;
-    const int e = e0 + threadIdx.x;
-    uint8_t *img = smem + threadIdx.x * obs_bytes;
-    uint32_t *win = reinterpret_cast<uint32_t *>(smem + round_up(kStepBlock * obs_bytes, 16) +
-                                                 threadIdx.x * win_stride(g.vs));
-    if (e < g.B) {
-        uint8_t *ty = TY + (long long)e * g.HWp;
-        uint8_t *co = CO + (long long)e * g.HWp;
-        uint8_t *st = ST + (long long)e * g.HWp;
-        const int4 ag = reinterpret_cast<const int4 *>(agent)[e];
-        const int2 cr = reinterpret_cast<const int2 *>(carry)[e];
-        StepOut o{ag.x, ag.y, ag.z, ag.w, cr.x, cr.y, MGDP_OK, 0, 0, 0, 0, 0, 0, 0, 0.0};
-        if (!observe_only) o = step_one(g, ty, co, st, ag.x, ag.y, ag.z, ag.w, cr.x, cr.y, actions[e], max_steps[e]);
-        if (!WIN && o.mut) { ty[o.fi] = (uint8_t)o.nt; co[o.fi] = (uint8_t)o.nc; st[o.fi] = (uint8_t)o.ns; }
-        if (o.stat == MGDP_OK) {
-            if (WIN) {
-                int tlx, tly, bx, by;
-                view_box(o.x, o.y, o.d, g.vs, tlx, tly, bx, by);
-                if (g.vs == 7) stage_window<7>(g, ty, co, st, bx, by, win);
-                else if (g.vs == 5) stage_window<5>(g, ty, co, st, bx, by, win);
-                else stage_window<3>(g, ty, co, st, bx, by, win);
-                uint8_t *wb = reinterpret_cast<uint8_t *>(win);
-                if (o.mut) {  // the front cell (in the view: the agent did not move) as the step left it
-                    const int w = (o.fi / g.W - by) * kWinRow + (o.fi % g.W - bx);
-                    wb[w] = (uint8_t)o.nt; wb[g.vs * kWinRow + w] = (uint8_t)o.nc; wb[2 * g.vs * kWinRow + w] = (uint8_t)o.ns;
-                    ty[o.fi] = (uint8_t)o.nt; co[o.fi] = (uint8_t)o.nc; st[o.fi] = (uint8_t)o.ns;
-                }
-                gen_obs_win(g, wb, tlx, tly, bx, by, o.d, o.ct, o.cc, see[e] != 0, img);
-            } else {
-                gen_obs_one(g, ty, co, st, o.x, o.y, o.d, o.ct, o.cc, see[e] != 0, img);
-            }
-        } else {
-            for (int i = 0; i < obs_bytes; ++i) img[i] = 0;
-        }
-        if (!observe_only) {
-            reinterpret_cast<int4 *>(agent)[e] = make_int4(o.x, o.y, o.d, o.sc);
-            reinterpret_cast<int2 *>(carry)[e] = make_int2(o.ct, o.cc);
-            reward[e] = o.r;
-            terminated[e] = (uint8_t)o.term;
-            truncated[e] = (uint8_t)o.trunc;
-            status[e] = o.stat;
-        }
-        direction[e] = o.d;
-    }
-    __syncthreads();
-    const int n = min(kStepBlock, g.B - e0);
-    copy_out(obs + (long long)e0 * obs_bytes, smem, n * obs_bytes);
-}
-
 // ------------------------------------------------------------------------------------------------
-// Lane-group step kernel (the default): kGroup = 8 lanes per env, 32 envs per 256-thread
-// workgroup, so a 65536-env batch is 8192 waves (8 per SIMD) instead of 1024 one-thread-per-env
-// waves whose dependent HBM and LDS latencies nothing could hide.  Per env:
-//   * every lane of the group runs step_one on the same (broadcast) loads; lane 0 alone writes
-//     the per-env results and the front-cell mutation;
-//   * lane v < vs stages row v of the view box (3 planes, dword loads aligned with v_alignbyte)
-//     into the group's LDS window; the wave executes its LDS accesses in issue order, so the other
-//     lanes' rows are visible to the reads below without a barrier (the group is inside one wave);
+// envs_step_kernel: G = 4 (or 8, MGDP_STEP_GROUP) lanes per env, 256 / G envs per 256-thread
+// workgroup, so a 65536-env batch is 4096 waves (4 per SIMD).  Per env:
+//   * lane v stages row v of the window box with 3 dword loads aligned by v_alignbyte into the
+//     group's LDS window.  The box is the view box after the turn (left / right change only the
+//     direction), extended by one cell along the heading for forward, so it holds both possible
+//     views, the front cell and the agent's next cell: one dependent HBM round trip after the
+//     agent record, and the step reads LDS.  The wave executes its LDS accesses in issue order, so
+//     the other lanes' rows are visible without a barrier (the group lies inside one wave);
+//   * every lane runs step_core on the window (uniform per group); lane 0 alone writes the per-env
+//     results and the front-cell mutation (window and HBM);
 //   * lane i < vs owns view column i: its see-behind bits are OR-reduced over the group (xor
 //     shuffles), process_vis runs on the 64-bit mask in bit-parallel form (process_vis_bits), and
 //     the lane encodes its column -- obs bytes [3*vs*i, 3*vs*(i+1)) of the env, contiguous because
 //     the obs is x-major -- into the LDS obs tile, which leaves with 16-B coalesced stores.
-// Bit-identical to envs_step_kernel (tests/test_gpu_step.py runs both against the reference's
-// trajectories and the oracle).
+// Measured (DoorKey-16 x 65536, profiles/): one thread per env with three byte planes 49 us per
+// step; 8 lanes per env 16.5 us; one byte plane instead of three, below.
 // ------------------------------------------------------------------------------------------------
-constexpr int kGroup = 8;
-constexpr int kGroupBlock = 256;
-constexpr int kGroupEnvs = kGroupBlock / kGroup;
+constexpr int kGroupBlock = 256;  // threads per workgroup (G lanes per env, 256 / G envs)
 
 __device__ __forceinline__ uint32_t rev8(uint32_t v) { return __builtin_bitreverse32(v) >> 24; }
 
@@ -406,115 +203,136 @@ __device__ __forceinline__ unsigned long long process_vis_bits(unsigned long lon
     return mask;
 }
 
+template <int G>
 __device__ __forceinline__ unsigned long long group_or(unsigned long long v) {
     uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
 #pragma unroll
-    for (int o = 1; o < kGroup; o <<= 1) {
+    for (int o = 1; o < G; o <<= 1) {
         lo |= (uint32_t)__shfl_xor((int)lo, o);
         hi |= (uint32_t)__shfl_xor((int)hi, o);
     }
     return ((unsigned long long)hi << 32) | lo;
 }
 
-template <int VS>
+template <int VS, int G>
 __global__ void __launch_bounds__(kGroupBlock)
-envs_step_group_kernel(EnvGeo g, uint8_t *__restrict__ TY, uint8_t *__restrict__ CO, uint8_t *__restrict__ ST,
-                       int32_t *__restrict__ agent, int32_t *__restrict__ carry,
-                       const int32_t *__restrict__ max_steps, const uint8_t *__restrict__ see,
-                       const int32_t *__restrict__ actions, uint8_t *__restrict__ obs,
-                       int32_t *__restrict__ direction, double *__restrict__ reward,
-                       uint8_t *__restrict__ terminated, uint8_t *__restrict__ truncated,
-                       int32_t *__restrict__ status, int observe_only) {
+envs_step_kernel(EnvGeo g, uint8_t *__restrict__ CELL, int32_t *__restrict__ agent, int32_t *__restrict__ carry,
+                 const int32_t *__restrict__ max_steps, const uint8_t *__restrict__ see,
+                 const int32_t *__restrict__ actions, uint8_t *__restrict__ obs,
+                 int32_t *__restrict__ direction, double *__restrict__ reward,
+                 uint8_t *__restrict__ terminated, uint8_t *__restrict__ truncated,
+                 int32_t *__restrict__ status, int observe_only) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int OB = VS * VS * 3;            // obs bytes per env
-    constexpr int WD = 3 * VS * 2;             // window dwords per env (3 planes x VS rows x 8 B)
-    constexpr int RB = kWinRow;                // window row bytes
-    const int slot = threadIdx.x / kGroup, r = threadIdx.x % kGroup;
-    const int e0 = blockIdx.x * kGroupEnvs;
+    constexpr int OB = VS * VS * 3;  // obs bytes per env
+    constexpr int WR = VS + 1;       // staged rows: the view box plus the forward cell
+    constexpr int RB = kWinRow;
+    constexpr int WD = WR * RB / 4;  // window dwords per env
+    constexpr int NE = kGroupBlock / G;        // envs per workgroup
+    constexpr int NR = (WR + G - 1) / G;       // window rows staged per lane
+    constexpr int NC = (VS + G - 1) / G;       // view columns per lane
+    const int slot = threadIdx.x / G, r = threadIdx.x % G;
+    const int e0 = blockIdx.x * NE;
     const int e = e0 + slot;
     uint8_t *img = smem + slot * OB;
-    uint32_t *win = reinterpret_cast<uint32_t *>(smem + round_up(kGroupEnvs * OB, 16)) + slot * (WD + 1);
-    const uint8_t *wb = reinterpret_cast<const uint8_t *>(win);
+    uint32_t *win = reinterpret_cast<uint32_t *>(smem + round_up(NE * OB, 16)) + slot * (WD + 1);
+    uint8_t *wb = reinterpret_cast<uint8_t *>(win);
     if (e < g.B) {
-        uint8_t *ty = TY + (long long)e * g.HWp;
-        uint8_t *co = CO + (long long)e * g.HWp;
-        uint8_t *st = ST + (long long)e * g.HWp;
+        uint8_t *cell = CELL + (long long)e * g.HWp;
         const int4 ag = reinterpret_cast<const int4 *>(agent)[e];
         const int2 cr = reinterpret_cast<const int2 *>(carry)[e];
-        StepOut o{ag.x, ag.y, ag.z, ag.w, cr.x, cr.y, MGDP_OK, 0, 0, 0, 0, 0, 0, 0, 0.0};
-        if (!observe_only) o = step_one(g, ty, co, st, ag.x, ag.y, ag.z, ag.w, cr.x, cr.y, actions[e], max_steps[e]);
-        if (o.stat == MGDP_OK) {
-            int tlx, tly, bx, by;
-            view_box(o.x, o.y, o.d, VS, tlx, tly, bx, by);
-            if (r < VS) {  // lane r stages window row r
+        const int act = observe_only ? -1 : actions[e];
+        const int ms = observe_only ? 1 : max_steps[e];
+        const int d1 = act == 0 ? ((ag.z + 3) & 3) : act == 1 ? ((ag.z + 1) & 3) : ag.z;
+        int tlx, tly, bx, by;
+        view_box(ag.x, ag.y, d1, VS, tlx, tly, bx, by);
+        if (act == 2) { bx += min(kDX[ag.z], 0); by += min(kDY[ag.z], 0); }
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {  // lane r stages window rows r, r+G, ...
+            const int row = r + G * k;
+            if (row < WR) {
                 const int nd = g.HWp >> 2;
-                const int off = (by + r) * g.W + bx;
+                const int off = (by + row) * g.W + bx;
                 const int a = off >> 2;  // floor: off may be negative left of / above the grid
                 const int sh = off & 3;
-                const uint32_t *P[3] = {reinterpret_cast<const uint32_t *>(ty), reinterpret_cast<const uint32_t *>(co),
-                                        reinterpret_cast<const uint32_t *>(st)};
-                uint32_t w[3][3];
+                const uint32_t *P = reinterpret_cast<const uint32_t *>(cell);
+                uint32_t w[3];
 #pragma unroll
-                for (int p = 0; p < 3; ++p)
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) w[p][q] = P[p][min(max(a + q, 0), nd - 1)];  // only in-grid bytes are read
-#pragma unroll
-                for (int p = 0; p < 3; ++p) {
-                    win[(p * VS + r) * 2 + 0] = __builtin_amdgcn_alignbyte(w[p][1], w[p][0], sh);
-                    win[(p * VS + r) * 2 + 1] = __builtin_amdgcn_alignbyte(w[p][2], w[p][1], sh);
-                }
+                for (int q = 0; q < 3; ++q) w[q] = P[min(max(a + q, 0), nd - 1)];  // only in-grid bytes are read
+                win[row * 2 + 0] = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
+                win[row * 2 + 1] = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
             }
+        }
+        asm volatile("" ::: "memory");  // the group's rows are written before any lane reads them
+        StepOut o{ag.x, ag.y, ag.z, ag.w, cr.x, cr.y, MGDP_OK, 0, 0, 0, 0, 0, 0, 0, 0.0};
+        if (!observe_only) {
+            // cells outside the staged box are only asked for by turns (whose result ignores them)
+            const auto rd = [&](int cx, int cy, int &t, int &c, int &s) {
+                const int u = cx - bx, v = cy - by;
+                const bool in = (unsigned)u < (unsigned)RB && (unsigned)v < (unsigned)WR;
+                cell_decode(in ? wb[v * RB + u] : 0u, t, c, s);
+            };
+            o = step_core(g, rd, ag.x, ag.y, ag.z, ag.w, cr.x, cr.y, act, ms);
+        }
+        if (o.stat == MGDP_OK) {
+            int bx2, by2;
+            view_box(o.x, o.y, o.d, VS, tlx, tly, bx2, by2);
             asm volatile("" ::: "memory");
             if (o.mut && r == 0) {  // the front cell as the step left it (in the view: the agent did not move)
                 const int fy = o.fi / g.W, fx = o.fi - fy * g.W;
-                const int w = (fy - by) * RB + (fx - bx);
-                uint8_t *wm = reinterpret_cast<uint8_t *>(win);
-                wm[w] = (uint8_t)o.nt; wm[VS * RB + w] = (uint8_t)o.nc; wm[2 * VS * RB + w] = (uint8_t)o.ns;
-                ty[o.fi] = (uint8_t)o.nt; co[o.fi] = (uint8_t)o.nc; st[o.fi] = (uint8_t)o.ns;
+                const uint8_t code = (uint8_t)cell_code(o.nt, o.nc, o.ns);
+                wb[(fy - by) * RB + (fx - bx)] = code;
+                cell[o.fi] = code;
             }
             asm volatile("" ::: "memory");
             const int fx = kDX[o.d], fy = kDY[o.d], rx = -fy, ry = fx;
-            const int i = r;
-            // Column i's world cells (wx0 - fx*j, wy0 - fy*j), read branch-free: an out-of-grid
-            // cell reads window byte 0 and is then replaced (out of bounds -> Wall, grid.py:136-139).
-            const int wx0 = tlx + rx * i, wy0 = tly + ry * i;
-            uint32_t tv[VS], cv[VS], sv[VS];
-            bool inb[VS];
+            // Lane r owns view columns i = r, r+G, ...  Column i's world cells (wx0 - fx*j,
+            // wy0 - fy*j) are read branch-free: an out-of-grid cell reads window byte 0 and is then
+            // replaced (out of bounds -> Wall, grid.py:136-139).
+            uint32_t cv[NC][VS];
+            bool inb[NC][VS];
             unsigned long long sb = 0;
 #pragma unroll
-            for (int j = 0; j < VS; ++j) {
-                const int wx = wx0 - fx * j, wy = wy0 - fy * j;
-                inb[j] = i < VS && (unsigned)wx < (unsigned)g.W && (unsigned)wy < (unsigned)g.H;
-                const int ow = inb[j] ? (wy - by) * RB + (wx - bx) : 0;
-                tv[j] = wb[ow]; cv[j] = wb[VS * RB + ow]; sv[j] = wb[2 * VS * RB + ow];
-                // see_behind as bit tests (comparison chains are lowered to branches)
-                const uint32_t tb = 1u << (tv[j] & 31u);
-                const bool behind = !(tb & (1u << T_WALL)) & !((tb & (1u << T_DOOR)) && sv[j] != D_OPEN);
-                sb |= (unsigned long long)(inb[j] && behind) << (j * 8 + (i & 7));
-            }
-            sb = group_or(sb);
-            const unsigned long long mask = see[e] ? ~0ull : process_vis_bits<VS>(sb);
-            if (i < VS) {  // encode column i, grid.py:244-268; the carried object at (VS/2, VS-1)
-                uint8_t *col = img + i * VS * 3;
-                const bool centre_col = i == VS / 2;
+            for (int k = 0; k < NC; ++k) {
+                const int i = r + G * k;
+                const int wx0 = tlx + rx * i, wy0 = tly + ry * i;
 #pragma unroll
                 for (int j = 0; j < VS; ++j) {
-                    uint32_t t = inb[j] ? tv[j] : (uint32_t)T_WALL;
-                    uint32_t c = inb[j] ? (tv[j] == T_EMPTY ? 0u : cv[j]) : (uint32_t)C_GREY;
-                    uint32_t s = inb[j] && tv[j] != T_EMPTY ? sv[j] : 0u;
-                    if (j == VS - 1 && centre_col) {
-                        t = o.ct > 0 ? (uint32_t)o.ct : (uint32_t)T_EMPTY;
-                        c = o.ct > 0 ? (uint32_t)o.cc : 0u;
-                        s = 0;
-                    }
-                    const bool vis = (mask >> (j * 8 + i)) & 1ull;
-                    col[3 * j] = (uint8_t)(vis ? t : 0u);
-                    col[3 * j + 1] = (uint8_t)(vis ? c : 0u);
-                    col[3 * j + 2] = (uint8_t)(vis ? s : 0u);
+                    const int wx = wx0 - fx * j, wy = wy0 - fy * j;
+                    inb[k][j] = i < VS && (unsigned)wx < (unsigned)g.W && (unsigned)wy < (unsigned)g.H;
+                    cv[k][j] = wb[inb[k][j] ? (wy - by) * RB + (wx - bx) : 0];
+                    // see_behind (world_object.py): not a wall (type 2: codes 16..23), not a closed or
+                    // locked door (codes 0x88.. / 0x90..)
+                    const uint32_t x = cv[k][j];
+                    const bool behind = ((x >> 3) != (uint32_t)T_WALL) & ((x & 0x98u) != 0x88u) & ((x & 0x98u) != 0x90u);
+                    sb |= (unsigned long long)(inb[k][j] && behind) << (j * 8 + (i & 7));
                 }
             }
-        } else if (r < VS) {
-            for (int k = 0; k < 3 * VS; ++k) img[r * VS * 3 + k] = 0;
+            sb = group_or<G>(sb);
+            const unsigned long long mask = see[e] ? ~0ull : process_vis_bits<VS>(sb);
+#pragma unroll
+            for (int k = 0; k < NC; ++k) {  // encode column i, grid.py:244-268; the carried object at (VS/2, VS-1)
+                const int i = r + G * k;
+                if (i < VS) {
+                    uint8_t *col = img + i * VS * 3;
+                    const bool centre_col = i == VS / 2;
+#pragma unroll
+                    for (int j = 0; j < VS; ++j) {
+                        int t, c, s;
+                        cell_decode(inb[k][j] ? cv[k][j] : kCodeWall, t, c, s);
+                        if (j == VS - 1 && centre_col) {
+                            t = o.ct > 0 ? o.ct : (int)T_EMPTY;
+                            c = o.ct > 0 ? o.cc : 0;
+                            s = 0;
+                        }
+                        const bool vis = (mask >> (j * 8 + i)) & 1ull;
+                        col[3 * j] = (uint8_t)(vis ? t : 0);
+                        col[3 * j + 1] = (uint8_t)(vis ? c : 0);
+                        col[3 * j + 2] = (uint8_t)(vis ? s : 0);
+                    }
+                }
+            }
+        } else {
+            for (int k = r; k < OB; k += G) img[k] = 0;
         }
         if (r == 0) {
             if (!observe_only) {
@@ -529,7 +347,7 @@ envs_step_group_kernel(EnvGeo g, uint8_t *__restrict__ TY, uint8_t *__restrict__
         }
     }
     __syncthreads();
-    const int n = min(kGroupEnvs, g.B - e0);
+    const int n = min(NE, g.B - e0);
     copy_out(obs + (long long)e0 * OB, smem, n * OB);
 }
 
@@ -541,39 +359,65 @@ struct mgdp_envs {
     int device = 0, B = 0, W = 0, H = 0, HW = 0, HWp = 0, vs = 7;
     hipStream_t stream = nullptr;
     bool own_stream = false;
-    uint8_t *d_ty = nullptr, *d_co = nullptr, *d_st = nullptr, *d_see = nullptr;
+    uint8_t *d_cell = nullptr, *d_see = nullptr;  // d_cell: one-byte cell codes [B][HWp]
     int32_t *d_agent = nullptr, *d_carry = nullptr, *d_max = nullptr, *d_act = nullptr, *d_dir = nullptr,
             *d_status = nullptr;
     uint8_t *d_obs = nullptr, *d_term = nullptr, *d_trunc = nullptr;
     double *d_rew = nullptr;
     uint32_t nd_mask = 0;
     double death_cost = -1.0;
-    // step kernel: 0 = envs_step_group_kernel (8 lanes per env, default), 1 = envs_step_kernel with
-    // the staged window, 2 = envs_step_kernel with per-cell HBM byte loads (gen_obs_one).
-    // MGDP_STEP_KERNEL=group|thread|thread_bytes selects one (measured alternatives, all tested).
-    int kmode = 0;
+    int group = 4;  // lanes per env in envs_step_kernel (MGDP_STEP_GROUP = 4 or 8; 4 measured faster)
+    // step-kernel timing (mgdp_envs_enable_timing): pooled event pairs handed to hipExtLaunchKernelGGL
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev, ev_pool;
+    double total_ms = 0.0;
+    long long launches = 0;
 };
 
 namespace {
+
+int timed_collect(mgdp_envs *E) {  // after a stream sync
+    for (auto &p : E->ev) {
+        float ms = 0.f;
+        MGDP_HIP(hipEventElapsedTime(&ms, p.first, p.second));
+        E->total_ms += ms;
+        E->launches += 1;
+        E->ev_pool.push_back(p);
+    }
+    E->ev.clear();
+    return 0;
+}
 
 EnvGeo env_geo(const mgdp_envs *E) { return EnvGeo{E->B, E->W, E->H, E->HWp, E->vs, E->nd_mask, E->death_cost}; }
 
 int launch_step(mgdp_envs *E, const int32_t *d_act, uint8_t *d_obs, int32_t *d_dir, double *d_rew,
                 uint8_t *d_term, uint8_t *d_trunc, int32_t *d_status, int observe_only) {
-    if (E->kmode == 0) {
-        const int grid = (E->B + kGroupEnvs - 1) / kGroupEnvs;
-        const int smem = (int)round_up(kGroupEnvs * E->vs * E->vs * 3, 16) + kGroupEnvs * (3 * E->vs * 2 + 1) * 4;
-        auto k = E->vs == 7 ? envs_step_group_kernel<7> : E->vs == 5 ? envs_step_group_kernel<5> : envs_step_group_kernel<3>;
-        hipLaunchKernelGGL(k, dim3(grid), dim3(kGroupBlock), smem, E->stream, env_geo(E),
-                           E->d_ty, E->d_co, E->d_st, E->d_agent, E->d_carry, E->d_max, E->d_see, d_act,
-                           d_obs, d_dir, d_rew, d_term, d_trunc, d_status, observe_only);
-    } else {
-        const int grid = (E->B + kStepBlock - 1) / kStepBlock;
-        const int smem = (int)round_up(kStepBlock * E->vs * E->vs * 3, 16) + kStepBlock * win_stride(E->vs);
-        hipLaunchKernelGGL(E->kmode == 1 ? envs_step_kernel<true> : envs_step_kernel<false>, dim3(grid), dim3(kStepBlock), smem, E->stream, env_geo(E),
-                           E->d_ty, E->d_co, E->d_st, E->d_agent, E->d_carry, E->d_max, E->d_see, d_act,
-                           d_obs, d_dir, d_rew, d_term, d_trunc, d_status, observe_only);
+    const int ne = kGroupBlock / E->group;
+    const int grid = (E->B + ne - 1) / ne;
+    const int smem = (int)round_up(ne * E->vs * E->vs * 3, 16) + ne * ((E->vs + 1) * kWinRow + 4);
+    auto k = E->group == 8 ? (E->vs == 7 ? envs_step_kernel<7, 8> : E->vs == 5 ? envs_step_kernel<5, 8> : envs_step_kernel<3, 8>)
+                           : (E->vs == 7 ? envs_step_kernel<7, 4> : E->vs == 5 ? envs_step_kernel<5, 4> : envs_step_kernel<3, 4>);
+    hipEvent_t ta = nullptr, tb = nullptr;
+    if (E->timing) {
+        if (E->ev.size() >= 4096) {  // bound the pending pairs
+            MGDP_HIP(hipStreamSynchronize(E->stream));
+            if (int rc = timed_collect(E)) return rc;
+        }
+        std::pair<hipEvent_t, hipEvent_t> p;
+        if (!E->ev_pool.empty()) {
+            p = E->ev_pool.back();
+            E->ev_pool.pop_back();
+        } else {
+            MGDP_HIP(hipEventCreate(&p.first));
+            MGDP_HIP(hipEventCreate(&p.second));
+        }
+        E->ev.push_back(p);
+        ta = p.first;
+        tb = p.second;
     }
+    hipExtLaunchKernelGGL(k, dim3(grid), dim3(kGroupBlock), smem, E->stream, ta, tb, 0, env_geo(E), E->d_cell, E->d_agent,
+                       E->d_carry, E->d_max, E->d_see, d_act, d_obs, d_dir, d_rew, d_term, d_trunc, d_status,
+                       observe_only);
     MGDP_HIP(hipGetLastError());
     return 0;
 }
@@ -590,22 +434,20 @@ int mgdp_envs_create(int32_t device, int32_t B, int32_t W, int32_t H, int32_t vi
     int ndev = 0;
     MGDP_HIP(hipGetDeviceCount(&ndev));
     MGDP_CHECK(device >= 0 && device < ndev, MGDP_E_HIP, "device %d not available (%d visible)", device, ndev);
-    int kmode = 0;
-    if (const char *ev = std::getenv("MGDP_STEP_KERNEL")) {
-        const std::string m(ev);
-        MGDP_CHECK(m == "group" || m == "thread" || m == "thread_bytes", MGDP_E_INVALID,
-                   "MGDP_STEP_KERNEL must be group, thread or thread_bytes (got %s)", ev);
-        kmode = m == "group" ? 0 : m == "thread" ? 1 : 2;
+    int group = 4;
+    if (const char *ev = std::getenv("MGDP_STEP_GROUP")) {
+        group = std::atoi(ev);
+        MGDP_CHECK(group == 4 || group == 8, MGDP_E_INVALID, "MGDP_STEP_GROUP must be 4 or 8 (got %s)", ev);
     }
     DeviceGuard guard(device);
     mgdp_envs *E = new mgdp_envs();
+    E->group = group;
     E->device = device; E->B = B; E->W = W; E->H = H; E->HW = W * H; E->HWp = (int)round_up(W * H, 16);
     E->vs = view_size;
-    E->kmode = kmode;
     const size_t P = (size_t)B * E->HWp;
     hipError_t e = hipSuccess;
     auto al = [&](void **p, size_t n) { if (e == hipSuccess) e = hipMalloc(p, n); };
-    al((void **)&E->d_ty, P); al((void **)&E->d_co, P); al((void **)&E->d_st, P);
+    al((void **)&E->d_cell, P);
     al((void **)&E->d_see, B);
     al((void **)&E->d_agent, sizeof(int32_t) * 4 * B);
     al((void **)&E->d_carry, sizeof(int32_t) * 2 * B);
@@ -617,9 +459,7 @@ int mgdp_envs_create(int32_t device, int32_t B, int32_t W, int32_t H, int32_t vi
     al((void **)&E->d_term, B); al((void **)&E->d_trunc, B);
     al((void **)&E->d_rew, sizeof(double) * B);
     if (e == hipSuccess) { e = hipStreamCreateWithFlags(&E->stream, hipStreamNonBlocking); E->own_stream = e == hipSuccess; }
-    if (e == hipSuccess) e = hipMemset(E->d_ty, T_WALL, P);
-    if (e == hipSuccess) e = hipMemset(E->d_co, C_GREY, P);
-    if (e == hipSuccess) e = hipMemset(E->d_st, 0, P);
+    if (e == hipSuccess) e = hipMemset(E->d_cell, (int)kCodeWall, P);
     if (e == hipSuccess) e = hipMemset(E->d_agent, 0, sizeof(int32_t) * 4 * B);
     if (e == hipSuccess) e = hipMemset(E->d_carry, 0, sizeof(int32_t) * 2 * B);
     if (e != hipSuccess) {
@@ -634,9 +474,11 @@ int mgdp_envs_destroy(mgdp_envs *E) {
     if (!E) return 0;
     DeviceGuard guard(E->device);
     if (E->stream) (void)hipStreamSynchronize(E->stream);
-    void *ps[] = {E->d_ty, E->d_co, E->d_st, E->d_see, E->d_agent, E->d_carry, E->d_max, E->d_act,
+    void *ps[] = {E->d_cell, E->d_see, E->d_agent, E->d_carry, E->d_max, E->d_act,
                   E->d_dir, E->d_status, E->d_obs, E->d_term, E->d_trunc, E->d_rew};
     for (void *p : ps) (void)hipFree(p);
+    for (auto &p : E->ev) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
+    for (auto &p : E->ev_pool) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
     if (E->own_stream) (void)hipStreamDestroy(E->stream);
     delete E;
     return 0;
@@ -673,8 +515,9 @@ int mgdp_envs_load(mgdp_envs *E, const uint8_t *enc, const int32_t *agent, const
         MGDP_CHECK(x >= 0 && y >= 0 && x < W && y < H && d >= 0 && d < 4, MGDP_E_BOUNDS,
                    "env %d: agent (%d,%d,%d) outside the grid", b, x, y, d);
     }
-    // x-major (W,H,3) -> row-major planes
-    std::vector<uint8_t> ty((size_t)B * HWp, T_WALL), co((size_t)B * HWp, C_GREY), st((size_t)B * HWp, 0);
+    // x-major (W,H,3) -> row-major one-byte cell codes (cell_code); what a byte cannot hold is an
+    // encoding Grid.encode() never produces
+    std::vector<uint8_t> cl((size_t)B * HWp, (uint8_t)kCodeWall);
     std::vector<int32_t> ag((size_t)B * 4), cr((size_t)B * 2, 0);
     for (int b = 0; b < B; ++b) {
         if (mask && !mask[b]) continue;
@@ -682,19 +525,17 @@ int mgdp_envs_load(mgdp_envs *E, const uint8_t *enc, const int32_t *agent, const
         for (int x = 0; x < W; ++x)
             for (int y = 0; y < H; ++y) {
                 const uint8_t *c = eb + (x * H + y) * 3;
-                const size_t i = (size_t)b * HWp + y * W + x;
-                ty[i] = c[0];
-                co[i] = c[0] == T_EMPTY ? 0 : c[1];
-                st[i] = c[0] == T_EMPTY ? 0 : c[2];
+                const int t = c[0], co = t == T_EMPTY ? 0 : c[1], st = t == T_EMPTY ? 0 : c[2];
+                MGDP_CHECK(t <= T_AGENT && co <= 5 && (t == T_DOOR ? st <= D_LOCKED : st == 0), MGDP_E_INVALID,
+                           "env %d cell (%d,%d): encoding (%d,%d,%d) is not a Grid.encode() cell", b, x, y, t, c[1], c[2]);
+                cl[(size_t)b * HWp + y * W + x] = (uint8_t)cell_code(t, co, st);
             }
         ag[4 * b] = agent[3 * b]; ag[4 * b + 1] = agent[3 * b + 1]; ag[4 * b + 2] = agent[3 * b + 2]; ag[4 * b + 3] = 0;
     }
     std::vector<int32_t> ms(max_steps, max_steps + B);
     std::vector<uint8_t> se(see_through, see_through + B);
     if (!mask) {
-        MGDP_HIP(hipMemcpyAsync(E->d_ty, ty.data(), ty.size(), hipMemcpyHostToDevice, E->stream));
-        MGDP_HIP(hipMemcpyAsync(E->d_co, co.data(), co.size(), hipMemcpyHostToDevice, E->stream));
-        MGDP_HIP(hipMemcpyAsync(E->d_st, st.data(), st.size(), hipMemcpyHostToDevice, E->stream));
+        MGDP_HIP(hipMemcpyAsync(E->d_cell, cl.data(), cl.size(), hipMemcpyHostToDevice, E->stream));
         MGDP_HIP(hipMemcpyAsync(E->d_agent, ag.data(), ag.size() * 4, hipMemcpyHostToDevice, E->stream));
         MGDP_HIP(hipMemcpyAsync(E->d_carry, cr.data(), cr.size() * 4, hipMemcpyHostToDevice, E->stream));
         MGDP_HIP(hipMemcpyAsync(E->d_max, ms.data(), ms.size() * 4, hipMemcpyHostToDevice, E->stream));
@@ -703,9 +544,7 @@ int mgdp_envs_load(mgdp_envs *E, const uint8_t *enc, const int32_t *agent, const
         for (int b = 0; b < B; ++b) {
             if (!mask[b]) continue;
             const size_t o = (size_t)b * HWp;
-            MGDP_HIP(hipMemcpyAsync(E->d_ty + o, &ty[o], HWp, hipMemcpyHostToDevice, E->stream));
-            MGDP_HIP(hipMemcpyAsync(E->d_co + o, &co[o], HWp, hipMemcpyHostToDevice, E->stream));
-            MGDP_HIP(hipMemcpyAsync(E->d_st + o, &st[o], HWp, hipMemcpyHostToDevice, E->stream));
+            MGDP_HIP(hipMemcpyAsync(E->d_cell + o, &cl[o], HWp, hipMemcpyHostToDevice, E->stream));
             MGDP_HIP(hipMemcpyAsync(E->d_agent + 4 * b, &ag[4 * b], 16, hipMemcpyHostToDevice, E->stream));
             MGDP_HIP(hipMemcpyAsync(E->d_carry + 2 * b, &cr[2 * b], 8, hipMemcpyHostToDevice, E->stream));
             MGDP_HIP(hipMemcpyAsync(E->d_max + b, &ms[b], 4, hipMemcpyHostToDevice, E->stream));
@@ -759,6 +598,27 @@ int mgdp_envs_step(mgdp_envs *E, const int32_t *actions, uint8_t *obs, int32_t *
     return 0;
 }
 
+int mgdp_envs_enable_timing(mgdp_envs *E, int32_t on) {
+    MGDP_CHECK(E, MGDP_E_INVALID, "null handle");
+    DeviceGuard guard(E->device);
+    MGDP_HIP(hipStreamSynchronize(E->stream));
+    if (int rc = timed_collect(E)) return rc;  // drop launches timed before this call
+    E->timing = on != 0;
+    E->total_ms = 0.0;
+    E->launches = 0;
+    return 0;
+}
+
+int mgdp_envs_kernel_time(mgdp_envs *E, double *total_ms, int64_t *launches) {
+    MGDP_CHECK(E, MGDP_E_INVALID, "null handle");
+    DeviceGuard guard(E->device);
+    MGDP_HIP(hipStreamSynchronize(E->stream));
+    if (int rc = timed_collect(E)) return rc;
+    if (total_ms) *total_ms = E->total_ms;
+    if (launches) *launches = (int64_t)E->launches;
+    return 0;
+}
+
 int mgdp_envs_get_state(mgdp_envs *E, uint8_t *enc, int32_t *agent, int32_t *carry, int32_t *step_count) {
     MGDP_CHECK(E, MGDP_E_INVALID, "null handle");
     DeviceGuard guard(E->device);
@@ -766,12 +626,10 @@ int mgdp_envs_get_state(mgdp_envs *E, uint8_t *enc, int32_t *agent, int32_t *car
     std::vector<int32_t> ag((size_t)B * 4);
     MGDP_HIP(hipMemcpyAsync(ag.data(), E->d_agent, ag.size() * 4, hipMemcpyDeviceToHost, E->stream));
     if (carry) MGDP_HIP(hipMemcpyAsync(carry, E->d_carry, 8 * (size_t)B, hipMemcpyDeviceToHost, E->stream));
-    std::vector<uint8_t> ty, co, st;
+    std::vector<uint8_t> cl;
     if (enc) {
-        ty.resize((size_t)B * HWp); co.resize(ty.size()); st.resize(ty.size());
-        MGDP_HIP(hipMemcpyAsync(ty.data(), E->d_ty, ty.size(), hipMemcpyDeviceToHost, E->stream));
-        MGDP_HIP(hipMemcpyAsync(co.data(), E->d_co, co.size(), hipMemcpyDeviceToHost, E->stream));
-        MGDP_HIP(hipMemcpyAsync(st.data(), E->d_st, st.size(), hipMemcpyDeviceToHost, E->stream));
+        cl.resize((size_t)B * HWp);
+        MGDP_HIP(hipMemcpyAsync(cl.data(), E->d_cell, cl.size(), hipMemcpyDeviceToHost, E->stream));
     }
     MGDP_HIP(hipStreamSynchronize(E->stream));
     for (int b = 0; b < B; ++b) {
@@ -783,7 +641,9 @@ int mgdp_envs_get_state(mgdp_envs *E, uint8_t *enc, int32_t *agent, int32_t *car
                 for (int y = 0; y < H; ++y) {
                     const size_t i = (size_t)b * HWp + y * W + x;
                     uint8_t *c = eb + (x * H + y) * 3;
-                    c[0] = ty[i]; c[1] = co[i]; c[2] = st[i];
+                    int t, co, st;
+                    cell_decode(cl[i], t, co, st);
+                    c[0] = (uint8_t)t; c[1] = (uint8_t)co; c[2] = (uint8_t)st;
                 }
         }
     }

@@ -152,10 +152,23 @@ class MiniGridVecEnv:
         return obs, self._rew.copy(), term, trunc, info
 
     def step_device(self, actions, obs, direction, reward, terminated, truncated, status):
-        """Zero-copy step on device buffers (torch CUDA tensors or raw pointers), asynchronous."""
-        _lib.check(self.L.mgdp_envs_step_device(self.h, _lib.ptr(actions), _lib.ptr(obs), _lib.ptr(direction),
-                                                _lib.ptr(reward), _lib.ptr(terminated), _lib.ptr(truncated),
-                                                _lib.ptr(status)), "mgdp_envs_step_device")
+        """Zero-copy step on device buffers (torch CUDA tensors or raw device pointers as ints),
+        asynchronous on the handle's stream.  Raw pointers skip every per-call conversion."""
+        p = _lib.ptr
+        rc = self.L.mgdp_envs_step_device(self.h, p(actions), p(obs), p(direction), p(reward), p(terminated),
+                                          p(truncated), p(status))
+        if rc:
+            _lib.check(rc, "mgdp_envs_step_device")
+
+    def enable_timing(self, on: bool):
+        """Time every step-kernel launch with a HIP event pair on the launch itself."""
+        _lib.check(self.L.mgdp_envs_enable_timing(self.h, int(on)), "mgdp_envs_enable_timing")
+
+    def kernel_time(self):
+        """(total ms, launches) of the step kernel since enable_timing(True); synchronises."""
+        ms, n = ctypes.c_double(0), ctypes.c_int64(0)
+        _lib.check(self.L.mgdp_envs_kernel_time(self.h, ctypes.byref(ms), ctypes.byref(n)), "mgdp_envs_kernel_time")
+        return ms.value, n.value
 
     def set_stream(self, stream):
         _lib.check(self.L.mgdp_envs_set_stream(self.h, ctypes.c_void_p(int(stream) if stream else 0)),

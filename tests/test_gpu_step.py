@@ -27,13 +27,13 @@ def grid_digest(enc):
     return np.frombuffer(hashlib.sha256(enc.tobytes()).digest()[:8], dtype=np.uint64)[0]
 
 
-STEP_KERNELS = ["group", "thread", "thread_bytes"]  # MGDP_STEP_KERNEL (csrc/envs.hip), read at create
+GROUPS = ["8", "4"]  # MGDP_STEP_GROUP: lanes per env in envs_step_kernel, read at create
 
 
-@pytest.mark.parametrize("kernel", STEP_KERNELS)
+@pytest.mark.parametrize("group", GROUPS)
 @pytest.mark.parametrize("name", traj_names())
-def test_batched_step_matches_reference_trajectories(name, kernel, monkeypatch):
-    monkeypatch.setenv("MGDP_STEP_KERNEL", kernel)
+def test_batched_step_matches_reference_trajectories(name, group, monkeypatch):
+    monkeypatch.setenv("MGDP_STEP_GROUP", group)
     t = load(f"traj_{name}.npz")
     B = t["actions"].shape[0]
     venv = MiniGridVecEnv(IDS[name], B)
@@ -141,13 +141,13 @@ def test_vector_autoreset():
     ("MiniGrid-Empty-16x16-v0", 7), ("MiniGrid-DoorKey-5x5-v0", 7), ("MiniGrid-DoorKey-8x8-v0", 5),
     ("MiniGrid-FourRooms-v0", 3), ("MiniGrid-LavaGapS7-v0", 5), ("MiniGrid-DistShift1-v0", 7),
 ])
-@pytest.mark.parametrize("kernel", STEP_KERNELS)
-def test_full_batch_random_actions_vs_batched_oracle(env_id, view, kernel, monkeypatch):
+@pytest.mark.parametrize("group", GROUPS)
+def test_full_batch_random_actions_vs_batched_oracle(env_id, view, group, monkeypatch):
     """Every env of a 4096-env batch, every step: obs bytes, fp64 reward, flags, agent, carry and
     step_count equal the oracle's step() restatement (orc_step_batch) on the same action stream;
     the final grids too (pickup / drop / toggle mutations).  Covers agents at the grid border
     (view windows outside the grid) and the 3 / 5 / 7 view sizes."""
-    monkeypatch.setenv("MGDP_STEP_KERNEL", kernel)
+    monkeypatch.setenv("MGDP_STEP_GROUP", group)
     B, steps = 4096 + 5, 96  # not a multiple of any kernel's envs per workgroup
     venv = MiniGridVecEnv(env_id, B, agent_view_size=view)
     venv.reset(seed=7)
@@ -170,4 +170,20 @@ def test_full_batch_random_actions_vs_batched_oracle(env_id, view, kernel, monke
     W, H = ob.W, ob.H
     enc = np.stack([p[:, : W * H].reshape(B, H, W).transpose(0, 2, 1) for p in (ob.ty, ob.co, ob.st)], axis=-1)
     np.testing.assert_array_equal(st["enc"], enc)
+    venv.close()
+
+
+def test_load_rejects_cells_grid_encode_never_produces():
+    """The device keeps one byte per cell (csrc/envs.hip cell_code): type <= 10, colour <= 5 and a
+    non-zero state only on doors, which is every Grid.encode() cell; anything else is refused."""
+    venv = MiniGridVecEnv("MiniGrid-Empty-5x5-v0", 2)
+    venv.reset(seed=0)
+    st = venv.get_state()
+    enc = st["enc"].copy()
+    enc[1, 2, 2] = (6, 1, 1)  # a ball with state 1
+    with pytest.raises(ValueError):  # MGDP_E_INVALID
+        venv.load(enc, st["agent"])
+    enc[1, 2, 2] = (4, 3, 2)  # a locked blue door is fine
+    venv.load(enc, st["agent"])
+    np.testing.assert_array_equal(venv.get_state()["enc"], enc)
     venv.close()

@@ -11,9 +11,6 @@ timeout -k 10 120 env MGDP_PERSISTENT=0 ./tools/probe_serve nopersist >> $OUT/pr
 for w in step_doorkey16x65536 step_fourrooms65536 step_lava65536; do
   timeout -k 10 300 python bench.py --workload $w --steps 20 --warmup 3 --cpu-budget 10 > $OUT/$w.json 2> $OUT/$w.err || { echo "$w failed"; exit 1; }
 done
-for w in step_doorkey16x65536 step_fourrooms65536; do
-  timeout -k 10 300 env MGDP_STEP_KERNEL=thread python bench.py --workload $w --steps 20 --warmup 3 --no-cpu > $OUT/${w}_thread.json 2> $OUT/${w}_thread.err || { echo "$w thread failed"; exit 1; }
-done
 for w in gen_lava65536 gen_fourrooms65536 gen_doorkey16x65536; do
   timeout -k 10 300 python bench.py --workload $w --steps 5 --warmup 1 --cpu-budget 10 > $OUT/$w.json 2> $OUT/$w.err || { echo "$w failed"; exit 1; }
 done

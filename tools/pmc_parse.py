@@ -22,9 +22,9 @@ RUNS = {
     "fourrooms4096_fused": ("fourrooms4096/fused/cell/f32", "vi_fused_kernel", None),
     # step / generator side benches (tools/pmc_side.sh); dword-wide scattered reads: the x2
     # correction is calibrated for 16-B streaming reads only (raw value kept beside it)
-    "step_doorkey16x65536": ("step_doorkey16x65536/step", "envs_step_group_kernel", None),
-    "step_fourrooms65536": ("step_fourrooms65536/step", "envs_step_group_kernel", None),
-    "step_lava65536": ("step_lava65536/step", "envs_step_group_kernel", None),
+    "step_doorkey16x65536": ("step_doorkey16x65536/step", "envs_step_kernel", None),
+    "step_fourrooms65536": ("step_fourrooms65536/step", "envs_step_kernel", None),
+    "step_lava65536": ("step_lava65536/step", "envs_step_kernel", None),
     "gen_lava65536": ("gen_lava65536/gen", "gen_grids_kernel", None),
     "gen_fourrooms65536": ("gen_fourrooms65536/gen", "gen_grids_kernel", None),
     "gen_doorkey16x65536": ("gen_doorkey16x65536/gen", "gen_grids_kernel", None),
