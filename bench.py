@@ -145,8 +145,8 @@ def load_traffic(key, solves_per_launch):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="empty16", choices=sorted(WORKLOADS) + sorted(STEP_WORKLOADS) + sorted(GEN_WORKLOADS))
     ap.add_argument("--method", default="fused", choices=["fused", "sweep"])
     ap.add_argument("--mapping", default="cell", choices=["cell", "sa"])
@@ -219,6 +219,9 @@ def main():
     sweeps = []
     for _ in range(args.steps):
         sweeps.append(one_solve())
+    # make the last solve final: a resident lone-grid server is told to leave (it exits within a
+    # poll) and the stream drained; a device synchronize alone would wait out the server's idle limit
+    vi.synchronize()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0

@@ -152,6 +152,9 @@ int mgdp_vi_get_dv_trace(mgdp_vi *vi, double *trace, int32_t n);
 int mgdp_vi_device_buffers(mgdp_vi *vi, void **d_V, void **d_pi);
 int mgdp_vi_num_states(const mgdp_vi_desc *desc, int64_t *S);
 
+/* Complete all work of the handle: a resident lone-grid server is asked to leave and the stream
+ * is drained (V / pi of the last solve are in HBM).  Every result getter does this implicitly. */
+int mgdp_vi_synchronize(mgdp_vi *vi);
 /* HIP-event timing of the dominant kernel (fused solve or sweep), on the stream it runs on. */
 int mgdp_vi_enable_timing(mgdp_vi *vi, int32_t on);
 int mgdp_vi_kernel_time(mgdp_vi *vi, double *total_ms, int64_t *launches);

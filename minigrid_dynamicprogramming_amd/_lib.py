@@ -85,6 +85,7 @@ SIGNATURES = {
     "mgdp_vi_get_dv_trace": (ctypes.c_int, [_P, _P, _I32]),
     "mgdp_vi_device_buffers": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
     "mgdp_vi_num_states": (ctypes.c_int, [ctypes.POINTER(ViDesc), _I64P]),
+    "mgdp_vi_synchronize": (ctypes.c_int, [_P]),
     "mgdp_vi_enable_timing": (ctypes.c_int, [_P, _I32]),
     "mgdp_vi_kernel_time": (ctypes.c_int, [_P, _DP, _I64P]),
     "mgdp_vi_persistent": (ctypes.c_int, [_P, _I32P]),

@@ -911,6 +911,14 @@ int mgdp_vi_device_buffers(mgdp_vi *vi, void **d_V, void **d_pi) {
     return 0;
 }
 
+int mgdp_vi_synchronize(mgdp_vi *vi) {
+    MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
+    DeviceGuard guard(vi->d.device);
+    if (int rc = server_stop(vi)) return rc;
+    MGDP_HIP(hipStreamSynchronize(vi->stream));
+    return 0;
+}
+
 int mgdp_vi_enable_timing(mgdp_vi *vi, int32_t on) {
     MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
     DeviceGuard guard(vi->d.device);

@@ -280,6 +280,10 @@ class ValueIteration:
         return VIResult(self.values(), self.policy(), self.sweeps, self.converged, self.dv, self.model,
                         self.W, self.H)
 
+    def synchronize(self):
+        """Complete all work of the handle (a resident lone-grid server leaves, the stream drains)."""
+        _lib.check(self.L.mgdp_vi_synchronize(self.h), "mgdp_vi_synchronize")
+
     def enable_timing(self, on: bool = True):
         _lib.check(self.L.mgdp_vi_enable_timing(self.h, int(on)), "mgdp_vi_enable_timing")
 
