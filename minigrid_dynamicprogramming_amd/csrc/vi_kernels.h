@@ -59,12 +59,12 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
         }
         return true;
     }
-    if (soa) {
+    if (SERVED || soa) {  // served lone grids are always on this path (serve_eligible): no other code in the server
         if (MODEL == MGDP_MODEL_XYD) {
-            if (k_target < 0) fused_fast_xyd_soa<T, SLIP, true>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+            if (SERVED || k_target < 0) fused_fast_xyd_soa<T, SLIP, true>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
             else fused_fast_xyd_soa<T, SLIP, false>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
         } else {
-            if (k_target < 0) fused_fast_dk_soa<T, true>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+            if (SERVED || k_target < 0) fused_fast_dk_soa<T, true>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
             else fused_fast_dk_soa<T, false>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
         }
         if (threadIdx.x == 0) {
@@ -72,7 +72,9 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
             dvenv[e] = dvl;
         }
         return true;  // V and pi were written by their owner threads
-    } else if (fast && MODEL == MGDP_MODEL_XYD && geo.pair) {
+    }
+    if constexpr (SERVED) return true;
+    if (fast && MODEL == MGDP_MODEL_XYD && geo.pair) {
         int vf = 0;
         if (k_target < 0) fused_fast_xyd2<T, SLIP, true>(geo, cf, cl, V0, pis, slots, flags, k, k_target, vf, dvl, done);
         else fused_fast_xyd2<T, SLIP, false>(geo, cf, cl, V0, pis, slots, flags, k, k_target, vf, dvl, done);
