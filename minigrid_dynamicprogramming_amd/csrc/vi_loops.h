@@ -265,23 +265,30 @@ __device__ __forceinline__ void fused_fast_xyd_soa(const Geo &geo, const Coef<T>
     // One sweep from Vin to Vout; false = the rule stopped before it.  The ping-pong is unrolled
     // by two below, so each copy has fixed LDS addresses and a fixed flag parity.  Idle threads
     // shadow cell 0, so their |dV| equals cell 0's and needs no masking.
+    // The stop test of the previous sweep (LOCAL) is read before this sweep's neighbour values
+    // (LDS returns in order) but consulted only after this sweep's arithmetic, so it is off the
+    // critical path; a sweep past the stopping point computes into the register set the caller
+    // discards and writes nothing.
     auto sweep = [&](const T *Vin, T *Vout, const V4<T> &in, V4<T> &out) -> bool {
+        if (LOCAL ? k >= geo.max_sweeps : k >= k_target) return false;
+        uint4 fl = make_uint4(0u, 0u, 0u, 0u);  // the previous sweep's flags (all 16 bytes: no branch on the wave count)
+        if (LOCAL) fl = *reinterpret_cast<const uint4 *>(flags + (parity ^ 1) * 16);
         T nbv[4];
         xyd_load_nb(tp, Vin, nbv);
-        if (LOCAL) {
-            if (k >= geo.max_sweeps) return false;
-            if (k > k_start && !flags_any(flags, parity ^ 1)) return false;
-        } else if (k >= k_target) {
-            return false;
-        }
         uint32_t pk;
         const T rg = HMODE ? rgoal[k_target - 1 - k] : (T)1;
+        T d;
         if (HMODE == 2) {
-            diff = xyd_step<T, SLIP, true, ND, true>(tp, cf, in, nbv, out, pk, rg);
+            d = xyd_step<T, SLIP, true, ND, true>(tp, cf, in, nbv, out, pk, rg);
             if (own_cell) *reinterpret_cast<uint32_t *>(pit + (long long)(k_target - 1 - k) * pit_stride + c * 4) = pk;
         } else {
-            diff = xyd_step<T, SLIP, false, ND, HMODE != 0>(tp, cf, in, nbv, out, pk, rg);
+            d = xyd_step<T, SLIP, false, ND, HMODE != 0>(tp, cf, in, nbv, out, pk, rg);
         }
+        if (LOCAL) {
+            asm volatile("" ::"v"(d));  // keep the arithmetic ahead of the test (no sinking past it)
+            if (k > k_start && (fl.x | fl.y | fl.z | fl.w) == 0u) return false;
+        }
+        diff = d;
 #pragma unroll
         for (int q = 0; q < 4; ++q) Vout[q * HW + c] = out.v[q];
         if (LOCAL) flag_write(diff >= cf.tol, flags, parity);
@@ -430,24 +437,27 @@ __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> 
     int cur = 0, parity = 0;
     T diff = (T)0;
     auto sweep = [&](const T *Vin, T *Vout, const T (&in)[16], T (&outv)[16]) -> bool {  // see fused_fast_xyd_soa
+        if (LOCAL ? k >= geo.max_sweeps : k >= k_target) return false;
+        uint4 fl = make_uint4(0u, 0u, 0u, 0u);  // the previous sweep's flags (all 16 bytes: no branch on the wave count)
+        if (LOCAL) fl = *reinterpret_cast<const uint4 *>(flags + (parity ^ 1) * 16);
         V4<T> nbs[4];
         dk_load_nb(tp, Vin, nbs);
-        if (LOCAL) {
-            if (k >= geo.max_sweeps) return false;
-            if (k > k_start && !flags_any(flags, parity ^ 1)) return false;
-        } else if (k >= k_target) {
-            return false;
-        }
         uint32_t pk[4];
         const T rg = HMODE ? rgoal[k_target - 1 - k] : (T)1;
+        T d;
         if (HMODE == 2) {
-            diff = dk_step<T, true, true>(tp, cf, in, nbs, outv, pk, rg);
+            d = dk_step<T, true, true>(tp, cf, in, nbs, outv, pk, rg);
             if (own_cell)
                 *reinterpret_cast<uint4 *>(pit + (long long)(k_target - 1 - k) * pit_stride + c * 16) =
                     make_uint4(pk[0], pk[1], pk[2], pk[3]);
         } else {
-            diff = dk_step<T, false, HMODE != 0>(tp, cf, in, nbs, outv, pk, rg);
+            d = dk_step<T, false, HMODE != 0>(tp, cf, in, nbs, outv, pk, rg);
         }
+        if (LOCAL) {
+            asm volatile("" ::"v"(d));  // keep the arithmetic ahead of the test (no sinking past it)
+            if (k > k_start && (fl.x | fl.y | fl.z | fl.w) == 0u) return false;
+        }
+        diff = d;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
             *reinterpret_cast<V4<T> *>(Vout + (q * HW + c) * 4) =
