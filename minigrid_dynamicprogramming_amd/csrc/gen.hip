@@ -385,9 +385,15 @@ gen_grids_kernel(mgdp_gen_desc d, long long seed0, int B, uint8_t *__restrict__ 
     if (enc) {
         const long long base = (long long)b0 * cellb;
         const int total = nb * cellb;
-        for (int i = threadIdx.x; i < total; i += kGenBlock) {
-            const int e = i / cellb, o = i - e * cellb;
-            enc[base + i] = smem[e * rec + o];
+        if (rec == cellb && (total & 15) == 0 && (base & 15) == 0) {  // records are contiguous: 16-B copy
+            const uint4 *s = reinterpret_cast<const uint4 *>(smem);
+            uint4 *o = reinterpret_cast<uint4 *>(enc + base);
+            for (int i = threadIdx.x; i < (total >> 4); i += kGenBlock) o[i] = s[i];
+        } else {
+            for (int i = threadIdx.x; i < total; i += kGenBlock) {
+                const int e = i / cellb, o = i - e * cellb;
+                enc[base + i] = smem[e * rec + o];
+            }
         }
     }
     if (cells) {  // row-major type codes

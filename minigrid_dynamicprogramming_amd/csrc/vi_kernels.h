@@ -5,12 +5,16 @@
 #pragma once
 
 namespace mgdp {
+template <typename T, int MODEL> struct TopoOf { using type = XydTopo<T>; };
+template <typename T> struct TopoOf<T, MGDP_MODEL_DOORKEY> { using type = DkTopo; };
+
+// pre: the cell topology a persistent server resolved once per residency (SERVED only)
 template <typename T, int MODEL, bool SLIP, int MAP, bool SERVED = false, int WP = 0>
 __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, const uint8_t *__restrict__ cells,
                                            T *__restrict__ V, int8_t *__restrict__ pi, int32_t *__restrict__ kenv,
                                            double *__restrict__ dvenv, unsigned long long *__restrict__ host_out,
                                            int k_target, int fresh, bool lone, unsigned int epoch, int e,
-                                           int &k, double &dvl) {
+                                           int &k, double &dvl, const typename TopoOf<T, MODEL>::type *pre = nullptr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
     T *V0 = reinterpret_cast<T *>(smem);
@@ -60,11 +64,15 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
         return true;
     }
     if (SERVED || soa) {  // served lone grids are always on this path (serve_eligible): no other code in the server
-        if (MODEL == MGDP_MODEL_XYD) {
-            if (SERVED || k_target < 0) fused_fast_xyd_soa<T, SLIP, true>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+        if constexpr (MODEL == MGDP_MODEL_XYD) {
+            if (SERVED || k_target < 0)
+                fused_fast_xyd_soa<T, SLIP, true>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl,
+                                                  done, nullptr, nullptr, 0, pre);
             else fused_fast_xyd_soa<T, SLIP, false>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
         } else {
-            if (SERVED || k_target < 0) fused_fast_dk_soa<T, true>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+            if (SERVED || k_target < 0)
+                fused_fast_dk_soa<T, true>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done,
+                                           nullptr, nullptr, 0, pre);
             else fused_fast_dk_soa<T, false>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
         }
         if (threadIdx.x == 0) {
@@ -160,6 +168,14 @@ vi_serve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     unsigned long long t_last = t_start;
     __syncthreads();
+    // the cells stay put while the server is resident: resolve this thread's cell topology once
+    typename TopoOf<T, MODEL>::type topo;
+    if constexpr (WP == 0) {
+        const uint8_t *cl = reinterpret_cast<const uint8_t *>(smem + L.cells_off());
+        const int cc = (int)threadIdx.x < geo.HW ? (int)threadIdx.x : 0;
+        if constexpr (MODEL == MGDP_MODEL_XYD) topo = xyd_topo_soa<T>(cl, geo, cc);
+        else topo = dk_topo_soa(cl, geo, cc);
+    }
     while (true) {
         if (lane == 0) {
             for (int i = 0; i < wave; ++i) __builtin_amdgcn_s_sleep(8);  // stagger the pollers
@@ -184,7 +200,7 @@ vi_serve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
         int k;
         double dvl;
         if (!fused_grid<T, MODEL, SLIP, MAP, true, WP>(geo, cf, cells, V, pi, kenv, dvenv, host_out, -1, 1, true,
-                                                   (unsigned int)cmd, 0, k, dvl) &&
+                                                   (unsigned int)cmd, 0, k, dvl, WP == 0 ? &topo : nullptr) &&
             threadIdx.x == 0)
             publish_tagged(host_out, k, dvl, (unsigned int)cmd);
         served = cmd;

@@ -244,13 +244,14 @@ __device__ __forceinline__ void fused_fast_xyd_soa(const Geo &geo, const Coef<T>
                                                    const T *Vg, T *Vg_out, int8_t *pig, int &k,
                                                    int k_target, double &dvl, const Done &done,
                                                    const T *rgoal = nullptr, int8_t *pit = nullptr,
-                                                   long long pit_stride = 0) {
+                                                   long long pit_stride = 0, const XydTopo<T> *pre = nullptr) {
     const int c = threadIdx.x;
     const int cc = c < geo.HW ? c : 0;  // idle threads shadow cell 0 and never write
     const bool own_cell = c < geo.HW;
     const int HW = geo.HWs;  // LDS stride: every thread (idle ones too) owns a slot, so LDS writes need no mask
     const int k_start = k;
-    const XydTopo<T> tp = xyd_topo_soa<T, ND>(cl, geo, cc);
+    // pre: the topology the persistent server resolved once per residency (cells cannot change)
+    const XydTopo<T> tp = pre ? *pre : xyd_topo_soa<T, ND>(cl, geo, cc);
     V4<T> own;
     if (k == 0) {
         own = V4<T>{{(T)0, (T)0, (T)0, (T)0}};
@@ -418,13 +419,13 @@ __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> 
                                                   const T *Vg, T *Vg_out, int8_t *pig, int &k,
                                                   int k_target, double &dvl, const Done &done,
                                                   const T *rgoal = nullptr, int8_t *pit = nullptr,
-                                                  long long pit_stride = 0) {
+                                                  long long pit_stride = 0, const DkTopo *pre = nullptr) {
     const int c = threadIdx.x;
     const int cc = c < geo.HW ? c : 0;
     const bool own_cell = c < geo.HW;
     const int HW = geo.HWs;  // LDS stride: every thread (idle ones too) owns a slot, so LDS writes need no mask
     const int k_start = k;
-    const DkTopo tp = dk_topo_soa(cl, geo, cc);
+    const DkTopo tp = pre ? *pre : dk_topo_soa(cl, geo, cc);  // pre: see fused_fast_xyd_soa
     T own[16];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {

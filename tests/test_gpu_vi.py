@@ -253,6 +253,30 @@ def test_persistent_server_requests_and_handoffs(monkeypatch):
     vi.close()
 
 
+def test_synchronize_ends_the_server_and_results_stay_final(monkeypatch):
+    """mgdp_vi_synchronize (bench.py's end of the timed region): a resident server leaves at once,
+    the stream drains, V / pi of the last served solve are in HBM, and the next solve relaunches."""
+    monkeypatch.setenv("MGDP_PERSISTENT", "1")
+    monkeypatch.setenv("MGDP_SERVE_IDLE_US", "2000000")  # it would not leave on its own
+    t = load("table_empty16_s0.npz")
+    cells = cells_from_enc(t["enc"])[None]
+    o = oracle.value_iteration(0, cells, dtype="f32")
+    vi = mg.ValueIteration(cells, dtype="f32")
+    assert vi.persistent
+    vi.enable_timing(True)
+    for _ in range(5):
+        assert vi.solve() == o["sweeps"]
+    vi.synchronize()
+    ms, n = vi.kernel_time()
+    assert n == 1 and ms > 0  # one launch served all five, and it has ended
+    np.testing.assert_array_equal(vi.values(), o["V"])
+    np.testing.assert_array_equal(vi.policy(), o["pi"])
+    assert vi.solve() == o["sweeps"]  # relaunched
+    vi.synchronize()
+    np.testing.assert_array_equal(vi.values(), o["V"])
+    vi.close()
+
+
 def test_persistent_server_lifetime_cap_relaunch(monkeypatch):
     """Servers that leave on their lifetime cap while the host still counts them resident: the
     host finds the stream drained with its request unserved and relaunches; results stay exact."""
