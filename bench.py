@@ -255,7 +255,7 @@ def main():
     achieved = bytes_alg / max(launches, 1) / avg_launch_s / 1e9 if launches else 0.0
     comp_bytes = compulsory_bytes_per_sweep(vi.S, HW, tsize) * vi.B * (sum(sweeps))
     persistent = vi.persistent
-    kernel_name = ("vi_serve_kernel" if persistent else "vi_fused_kernel") if args.method == "fused" else "vi_sweep_kernel"
+    kernel_name = vi.kernel_name
     key = f"{args.workload}/{args.method}/{args.mapping}/{args.dtype}"
     roofline = {
         "bound": "hbm", "kernel": kernel_name,
@@ -549,7 +549,7 @@ def hbm_side_measurement(args, n_solves=3):
         avg = ms / 1000.0 / max(n, 1)
         ach = upd * bpu / max(n, 1) / avg / 1e9
         comp = compulsory_bytes_per_sweep(vi.S, vi.W * vi.H, tsize) * vi.B * sum(ks) / max(n, 1) / avg / 1e9
-        res[method] = {"kernel": "vi_sweep_kernel" if method == "sweep" else "vi_fused_kernel",
+        res[method] = {"kernel": vi.kernel_name,
                        "updates_per_s": upd / el, "sweeps": ks[-1], "launches": n, "avg_launch_us": avg * 1e6,
                        "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                        "compulsory_gbs": comp, "compulsory_frac": comp / HBM_PEAK_GBS,

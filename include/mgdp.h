@@ -124,6 +124,9 @@ int mgdp_vi_load_cells_device(mgdp_vi *vi, const uint8_t *d_cells);
 int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *converged_out);
 /* *on = 1 if mgdp_vi_solve on this handle goes through the persistent server. */
 int mgdp_vi_persistent(const mgdp_vi *vi, int32_t *on);
+/* Name of the kernel mgdp_vi_kernel_time times on this handle (as rocprofv3 lists it): vi_serve_kernel,
+ * vi_fused_kernel, vi_fused_opts_kernel, vi_sweep_pipe_kernel or vi_sweep_kernel; NULL on error. */
+const char *mgdp_vi_kernel_name(const mgdp_vi *vi);
 
 /* Multi-device protocol (DESIGN.md "convergence across GPUs"): every rank calls
  *   mgdp_vi_reset -> mgdp_vi_run_local(&k_local) -> all-reduce(MAX) k -> mgdp_vi_run_to(k, &dv)

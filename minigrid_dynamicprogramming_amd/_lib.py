@@ -89,6 +89,7 @@ SIGNATURES = {
     "mgdp_vi_enable_timing": (ctypes.c_int, [_P, _I32]),
     "mgdp_vi_kernel_time": (ctypes.c_int, [_P, _DP, _I64P]),
     "mgdp_vi_persistent": (ctypes.c_int, [_P, _I32P]),
+    "mgdp_vi_kernel_name": (ctypes.c_char_p, [_P]),
     "mgdp_vi_get_policy_t": (ctypes.c_int, [_P, _P]),
     "mgdp_gen_grids": (ctypes.c_int, [ctypes.POINTER(GenDesc), _I32, _P, ctypes.c_int64, _I32, _P, _P, _P]),
     "mgdp_gen_grids_host": (ctypes.c_int, [ctypes.POINTER(GenDesc), _I32, ctypes.c_int64, _I32, _P, _P, _P]),

@@ -366,7 +366,7 @@ struct mgdp_envs {
     double *d_rew = nullptr;
     uint32_t nd_mask = 0;
     double death_cost = -1.0;
-    int group = 4;  // lanes per env in envs_step_kernel (MGDP_STEP_GROUP = 4 or 8; 4 measured faster)
+    int group = 4;  // lanes per env in envs_step_kernel (MGDP_STEP_GROUP = 2, 4 or 8; 4 measured fastest)
     // step-kernel timing (mgdp_envs_enable_timing): pooled event pairs handed to hipExtLaunchKernelGGL
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev, ev_pool;
@@ -395,8 +395,10 @@ int launch_step(mgdp_envs *E, const int32_t *d_act, uint8_t *d_obs, int32_t *d_d
     const int ne = kGroupBlock / E->group;
     const int grid = (E->B + ne - 1) / ne;
     const int smem = (int)round_up(ne * E->vs * E->vs * 3, 16) + ne * ((E->vs + 1) * kWinRow + 4);
-    auto k = E->group == 8 ? (E->vs == 7 ? envs_step_kernel<7, 8> : E->vs == 5 ? envs_step_kernel<5, 8> : envs_step_kernel<3, 8>)
-                           : (E->vs == 7 ? envs_step_kernel<7, 4> : E->vs == 5 ? envs_step_kernel<5, 4> : envs_step_kernel<3, 4>);
+    auto pick = [&](auto k7, auto k5, auto k3) { return E->vs == 7 ? k7 : E->vs == 5 ? k5 : k3; };
+    auto k = E->group == 8   ? pick(envs_step_kernel<7, 8>, envs_step_kernel<5, 8>, envs_step_kernel<3, 8>)
+             : E->group == 2 ? pick(envs_step_kernel<7, 2>, envs_step_kernel<5, 2>, envs_step_kernel<3, 2>)
+                             : pick(envs_step_kernel<7, 4>, envs_step_kernel<5, 4>, envs_step_kernel<3, 4>);
     hipEvent_t ta = nullptr, tb = nullptr;
     if (E->timing) {
         if (E->ev.size() >= 4096) {  // bound the pending pairs
@@ -437,7 +439,7 @@ int mgdp_envs_create(int32_t device, int32_t B, int32_t W, int32_t H, int32_t vi
     int group = 4;
     if (const char *ev = std::getenv("MGDP_STEP_GROUP")) {
         group = std::atoi(ev);
-        MGDP_CHECK(group == 4 || group == 8, MGDP_E_INVALID, "MGDP_STEP_GROUP must be 4 or 8 (got %s)", ev);
+        MGDP_CHECK(group == 2 || group == 4 || group == 8, MGDP_E_INVALID, "MGDP_STEP_GROUP must be 2, 4 or 8 (got %s)", ev);
     }
     DeviceGuard guard(device);
     mgdp_envs *E = new mgdp_envs();

@@ -864,6 +864,15 @@ int mgdp_vi_persistent(const mgdp_vi *vi, int32_t *on) {
     return 0;
 }
 
+const char *mgdp_vi_kernel_name(const mgdp_vi *vi) {
+    if (!vi) { set_error("null handle"); return nullptr; }
+    if (vi->d.method == MGDP_METHOD_FUSED) {
+        if (vi->opts) return "vi_fused_opts_kernel";
+        return serve_eligible(vi) ? "vi_serve_kernel" : "vi_fused_kernel";
+    }
+    return vi->d.mapping == MGDP_MAP_CELL && vi->sweep_pipe ? "vi_sweep_pipe_kernel" : "vi_sweep_kernel";
+}
+
 int mgdp_vi_get_values(mgdp_vi *vi, void *V) {
     MGDP_CHECK(vi && V, MGDP_E_INVALID, "null argument");
     DeviceGuard guard(vi->d.device);

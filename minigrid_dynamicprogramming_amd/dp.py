@@ -193,6 +193,14 @@ class ValueIteration:
         _lib.check(self.L.mgdp_vi_persistent(self.h, ctypes.byref(on)), "mgdp_vi_persistent")
         return bool(on.value)
 
+    @property
+    def kernel_name(self) -> str:
+        """The kernel kernel_time() times on this handle, as rocprofv3 lists it."""
+        n = self.L.mgdp_vi_kernel_name(self.h)
+        if n is None:
+            _lib.check(_lib.MGDP_E_INVALID, "mgdp_vi_kernel_name")
+        return n.decode()
+
     def load(self, grids):
         """Install new grids of the same shape (mgdp_vi_load_cells); the next solve uses them."""
         cells, enc = to_cells(grids)

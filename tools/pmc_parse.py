@@ -15,7 +15,7 @@ OUT = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_traffic.json"
 # run -> (bench key, kernel, solves per launch for a persistent server launch or None)
 RUNS = {
     "empty16": ("empty16/fused/cell/f32", "vi_serve_kernel", 20),
-    "empty16x65536_sweep": ("empty16x65536/sweep/cell/f32", "vi_sweep_kernel", None),
+    "empty16x65536_sweep": ("empty16x65536/sweep/cell/f32", "vi_sweep_pipe_kernel", None),
     "empty16x65536_fused": ("empty16x65536/fused/cell/f32", "vi_fused_kernel", None),
     "doorkey65536_fused": ("doorkey65536/fused/cell/f32", "vi_fused_kernel", None),
     "lava65536_fused": ("lava65536/fused/cell/f32", "vi_fused_kernel", None),
