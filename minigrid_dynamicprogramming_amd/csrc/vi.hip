@@ -89,6 +89,7 @@ struct mgdp_vi {
     int quad = 0;                 // fused XYD: 4 threads per cell
     int pair = 0;                 // fused XYD: two-sweep step
     int wave_p = 0;               // lone XYD grid on one wave: cells per lane (fused_wave_xyd)
+    int cpt = 1;                  // batched XYD fused path: cells per thread (MGDP_CPT; 2 = fused_fast_xyd_soa_x2)
     int sweep_block = 256;
     int sweep_m = 1;              // grids staged per workgroup iteration (measured: m>1 no faster)
     int sweep_pipe = 2;           // register-pipelined sweep kernel: grids fetched ahead (0 = staged kernel)
@@ -248,6 +249,9 @@ int launch_fused_t(mgdp_vi *vi, int k_target) {
     const Geo g = make_geo(vi);
     const Smem L = smem_layout(vi->Ss, vi->HWp, sizeof(T), vi->nbuf);
     auto kern = pick_wave<FusedK, T, MODEL, SLIP, MAP>(vi);
+    if constexpr (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL)
+        if (vi->cpt == 2) kern = FusedK<T, MODEL, SLIP, MAP, -2>::fn;
+        else if (vi->cpt == 4) kern = FusedK<T, MODEL, SLIP, MAP, -4>::fn;
     if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
     TimedPair tp;
     if (int rc = timed_begin(vi, -1, &tp)) return rc;
@@ -605,6 +609,17 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
             vi->HWs = 64 * P;
             vi->Ss = vi->S / vi->HW * vi->HWs;
             vi->fused_block = 64;
+        }
+        // Batched XYD grids: N cells per thread divides the waves per grid by N (MGDP_CPT=1|2|4;
+        // measured on MI355X, profiles/r01_cpt/: 2 beats 1 by 7-25 %).
+        int cpt = 2;
+        if (const char *ev = std::getenv("MGDP_CPT")) cpt = std::atoi(ev);
+        if ((cpt == 2 || cpt == 4) && d.B > 1 && d.model == MGDP_MODEL_XYD && d.method == MGDP_METHOD_FUSED &&
+            !vi->pair && !vi->quad && !vi->opts && vi->HW <= 1024) {
+            vi->cpt = cpt;
+            vi->fused_block = (int)round_up((vi->HW + cpt - 1) / cpt, 64);
+            vi->HWs = cpt * vi->fused_block;
+            vi->Ss = vi->S / vi->HW * vi->HWs;
         }
     } else {
         int blk = d.B == 1 ? 1024 : 256;

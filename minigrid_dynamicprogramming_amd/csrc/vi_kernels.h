@@ -29,7 +29,9 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     const bool work = k_target < 0 ? (!(k > 0 && dvl < geo.tol) && k < geo.max_sweeps) : (k < k_target);
     if (!work) return false;
     const long long vb = (long long)e * geo.S;
-    const bool fast = MAP == MGDP_MAP_CELL && geo.HW <= (int)blockDim.x;
+    // WP < 0: -WP cells per thread on the batched direction-major path (fused_fast_xyd_soa_xn)
+    constexpr int CPT = WP < 0 ? -WP : 1;
+    const bool fast = MAP == MGDP_MAP_CELL && geo.HW <= CPT * (int)blockDim.x;
     const bool soa = fast && !geo.pair && !geo.quad;
     if (!SERVED) copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
     if (!soa) {
@@ -64,7 +66,10 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
         return true;
     }
     if (SERVED || soa) {  // served lone grids are always on this path (serve_eligible): no other code in the server
-        if constexpr (MODEL == MGDP_MODEL_XYD) {
+        if constexpr (MODEL == MGDP_MODEL_XYD && CPT > 1) {
+            if (k_target < 0) fused_fast_xyd_soa_xn<T, SLIP, true, CPT>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+            else fused_fast_xyd_soa_xn<T, SLIP, false, CPT>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+        } else if constexpr (MODEL == MGDP_MODEL_XYD) {
             if (SERVED || k_target < 0)
                 fused_fast_xyd_soa<T, SLIP, true>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl,
                                                   done, nullptr, nullptr, 0, pre);
@@ -125,7 +130,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
 // WP > 0: the one-wave lone-grid variant (fused_wave_xyd), 64 threads, so its WP cells per lane
 // may use the whole register file.
 template <typename T, int MODEL, bool SLIP, int MAP, int WP = 0>
-__global__ void __launch_bounds__(WP ? 64 : 1024)
+__global__ void __launch_bounds__(WP > 0 ? 64 : 1024)
 vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
@@ -154,7 +159,7 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
 constexpr unsigned long long kServeQuit = ~0ull;
 
 template <typename T, int MODEL, bool SLIP, int MAP, int WP = 0>
-__global__ void __launch_bounds__(WP ? 64 : 1024)
+__global__ void __launch_bounds__(WP > 0 ? 64 : 1024)
 vi_serve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ host_out, const unsigned long long *__restrict__ host_cmd,

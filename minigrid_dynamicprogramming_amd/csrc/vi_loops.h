@@ -321,6 +321,87 @@ __device__ __forceinline__ void fused_fast_xyd_soa(const Geo &geo, const Coef<T>
     }
 }
 
+// Batched XYD grids with N cells per thread (cells t + j*blockDim, j < N; HWs = N * blockDim): the
+// same sweep as fused_fast_xyd_soa on 1/N of the waves, so the per-sweep fixed work of a wave (flag
+// read, address set-up, ballot, barrier) is paid once per N cells.  Plain deterministic / slip
+// model only (the options kernel keeps one cell per thread).
+template <typename T, bool SLIP, bool LOCAL, int N, typename Done>
+__device__ __forceinline__ void fused_fast_xyd_soa_xn(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
+                                                      T *V0, T *V1, T *slots, uint8_t *flags,
+                                                      const T *Vg, T *Vg_out, int8_t *pig, int &k,
+                                                      int k_target, double &dvl, const Done &done) {
+    const int HW = geo.HWs;
+    int c[N];
+    XydTopo<T> tp[N];
+    V4<T> own[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        c[j] = (int)(threadIdx.x + j * blockDim.x);
+        const int cc = c[j] < geo.HW ? c[j] : 0;  // idle slots shadow cell 0 and never write HBM
+        tp[j] = xyd_topo_soa<T>(cl, geo, cc);
+        own[j] = k == 0 ? V4<T>{{(T)0, (T)0, (T)0, (T)0}} : *reinterpret_cast<const V4<T> *>(Vg + cc * 4);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) V0[d * HW + c[j]] = own[j].v[d];
+    }
+    const int k_start = k;
+    __syncthreads();
+    int cur = 0, parity = 0;
+    T diff = (T)0;
+    auto sweep = [&](const T *Vin, T *Vout, const V4<T> (&in)[N], V4<T> (&out)[N]) -> bool {  // see fused_fast_xyd_soa
+        if (LOCAL ? k >= geo.max_sweeps : k >= k_target) return false;
+        uint4 fl = make_uint4(0u, 0u, 0u, 0u);
+        if (LOCAL) fl = *reinterpret_cast<const uint4 *>(flags + (parity ^ 1) * 16);
+        T nbv[N][4];
+#pragma unroll
+        for (int j = 0; j < N; ++j) xyd_load_nb(tp[j], Vin, nbv[j]);
+        uint32_t pk;
+        T d = (T)0;
+#pragma unroll
+        for (int j = 0; j < N; ++j) d = vmax(d, xyd_step<T, SLIP, false>(tp[j], cf, in[j], nbv[j], out[j], pk));
+        if (LOCAL) {
+            asm volatile("" ::"v"(d));
+            if (k > k_start && (fl.x | fl.y | fl.z | fl.w) == 0u) return false;
+        }
+        diff = d;
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) Vout[q * HW + c[j]] = out[j].v[q];
+        if (LOCAL) flag_write(diff >= cf.tol, flags, parity);
+        __syncthreads();
+        parity ^= 1;
+        ++k;
+        return true;
+    };
+    V4<T> alt[N];
+    while (true) {
+        if (!sweep(V0, V1, own, alt)) { cur = 0; break; }
+        if (!sweep(V1, V0, alt, own)) {
+            cur = 1;
+#pragma unroll
+            for (int j = 0; j < N; ++j) own[j] = alt[j];
+            break;
+        }
+    }
+    dvl = (double)block_max(diff, slots, 0);
+    done(k, dvl);
+    const T *Vp = cur ? V0 : V1;  // V_{k-1}: pi of the last sweep is the argmax on it
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        if (c[j] < geo.HW) {
+            V4<T> op, tmp;
+            T nbv[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) op.v[q] = Vp[q * HW + c[j]];
+            xyd_load_nb(tp[j], Vp, nbv);
+            uint32_t pk;
+            xyd_step<T, SLIP, true>(tp[j], cf, op, nbv, tmp, pk);
+            *reinterpret_cast<uint32_t *>(pig + c[j] * 4) = pk;
+            *reinterpret_cast<V4<T> *>(Vg_out + c[j] * 4) = own[j];
+        }
+    }
+}
+
 // Lone XYD grid on ONE wave, P cells per lane (cell j*64 + lane, same direction-major tiles with
 // HWs = 64*P).  A wave's LDS instructions execute in issue order, so the writes of sweep k are
 // seen by the reads of sweep k+1 without a workgroup barrier, and the stopping rule is the wave's

@@ -161,14 +161,17 @@ def test_invalid_grids_raise():
         mg.value_iteration(open_border, model="xyd")
 
 
-@pytest.mark.parametrize("pair,quad", [("0", "0"), ("1", "0"), ("0", "1")])
+@pytest.mark.parametrize("pair,quad,cpt", [("0", "0", "1"), ("0", "0", "2"), ("0", "0", "4"), ("1", "0", "1"), ("0", "1", "1")])
 @pytest.mark.parametrize("slip", [None, 0.9])
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
-def test_fused_xyd_variants_bit_exact(pair, quad, slip, dtype, monkeypatch):
-    """Every fused XYD loop -- one thread per cell, the two-sweep step (3 LDS buffers), four
-    threads per cell with DPP quad exchange -- agrees with the oracle bit for bit."""
+def test_fused_xyd_variants_bit_exact(pair, quad, cpt, slip, dtype, monkeypatch):
+    """Every fused XYD loop -- one thread per cell, two cells per thread on batches (MGDP_CPT=2),
+    the two-sweep step (3 LDS buffers), four threads per cell with DPP quad exchange -- agrees with
+    the oracle bit for bit (batches of 7 and 64 grids with different own stopping sweeps also run
+    the advance-to-K loop)."""
     monkeypatch.setenv("MGDP_PAIR", pair)
     monkeypatch.setenv("MGDP_QUAD", quad)
+    monkeypatch.setenv("MGDP_CPT", cpt)
     for env in ("fourrooms", "lava11n5"):
         g = load(f"grids_{env}.npz")
         cells = np.stack([cells_from_enc(e) for e in g["enc"]])
@@ -262,7 +265,7 @@ def test_synchronize_ends_the_server_and_results_stay_final(monkeypatch):
     cells = cells_from_enc(t["enc"])[None]
     o = oracle.value_iteration(0, cells, dtype="f32")
     vi = mg.ValueIteration(cells, dtype="f32")
-    assert vi.persistent
+    assert vi.persistent and vi.kernel_name == "vi_serve_kernel"
     vi.enable_timing(True)
     for _ in range(5):
         assert vi.solve() == o["sweeps"]
@@ -275,6 +278,11 @@ def test_synchronize_ends_the_server_and_results_stay_final(monkeypatch):
     vi.synchronize()
     np.testing.assert_array_equal(vi.values(), o["V"])
     vi.close()
+    names = {m: mg.ValueIteration(np.repeat(cells, 2, axis=0), dtype="f32", method=m) for m in ("fused", "sweep")}
+    assert names["fused"].kernel_name == "vi_fused_kernel"
+    assert names["sweep"].kernel_name == "vi_sweep_pipe_kernel"  # Empty-16: the register-pipelined sweep
+    for v in names.values():
+        v.close()
 
 
 def test_persistent_server_lifetime_cap_relaunch(monkeypatch):
