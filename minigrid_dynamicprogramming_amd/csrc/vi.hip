@@ -274,6 +274,8 @@ int launch_serve_t(mgdp_vi *vi, unsigned int served) {
     const Geo g = make_geo(vi);
     const Smem L = smem_layout(vi->Ss, vi->HWp, sizeof(T), vi->nbuf);
     auto kern = pick_wave<ServeK, T, MODEL, SLIP, MAP>(vi);
+    if constexpr (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL)
+        if (vi->cpt == 2) kern = ServeK<T, MODEL, SLIP, MAP, -2>::fn;
     if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
     TimedPair tp;
     if (int rc = timed_begin(vi, -1, &tp)) return rc;
@@ -418,7 +420,7 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
 // Persistent solver hand-off (lone grid on the one-thread-per-cell fused path).
 bool serve_eligible(const mgdp_vi *vi) {
     return vi->persistent && !vi->opts && vi->d.method == MGDP_METHOD_FUSED && vi->d.B == 1 && vi->d.mapping == MGDP_MAP_CELL &&
-           (vi->HW <= vi->fused_block || vi->wave_p) && !vi->pair && !vi->quad;
+           (vi->HW <= vi->cpt * vi->fused_block || vi->wave_p) && !vi->pair && !vi->quad;
 }
 // Ask a resident server to leave and drain the stream.  Every entry point that enqueues other
 // work on the stream, or reads results, calls this first.
@@ -614,7 +616,10 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
         // measured on MI355X, profiles/r01_cpt/: 2 beats 1 by 7-25 %).
         int cpt = 2;
         if (const char *ev = std::getenv("MGDP_CPT")) cpt = std::atoi(ev);
-        if ((cpt == 2 || cpt == 4) && d.B > 1 && d.model == MGDP_MODEL_XYD && d.method == MGDP_METHOD_FUSED &&
+        int lone_cpt = 1;  // a lone grid (latency) keeps one cell per thread unless MGDP_LONE_CPT=2
+        if (const char *ev = std::getenv("MGDP_LONE_CPT")) lone_cpt = std::atoi(ev) == 2 ? 2 : 1;
+        if (d.B == 1) cpt = vi->wave_p ? 1 : lone_cpt;
+        if ((cpt == 2 || cpt == 4) && d.model == MGDP_MODEL_XYD && d.method == MGDP_METHOD_FUSED &&
             !vi->pair && !vi->quad && !vi->opts && vi->HW <= 1024) {
             vi->cpt = cpt;
             vi->fused_block = (int)round_up((vi->HW + cpt - 1) / cpt, 64);
