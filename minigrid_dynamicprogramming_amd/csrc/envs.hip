@@ -12,7 +12,7 @@
 //   agent       int32 [B][4]     x, y, dir, step_count
 //   carry       int32 [B][2]     carried (type, colour); type 0 = nothing
 //   max_steps   int32 [B], see uint8 [B] (see_through_walls)
-// One step = one envs_step_kernel launch: 8 lanes per env (see the kernel).  The V x V view is
+// One step = one envs_step_kernel launch: 2 lanes per env (see the kernel).  The V x V view is
 // never materialised: view cell (i, j) maps to world top_left - f*j + r*i (f = DIR_TO_VEC[dir],
 // r = right_vec, minigrid_env.py:421-446), which equals the reference's slice + (dir+1) x
 // rotate_left; process_vis runs on a 64-bit visibility mask.
@@ -151,8 +151,8 @@ __device__ __forceinline__ StepOut step_core(const EnvGeo &g, const Rd &rd, int 
 }
 
 // ------------------------------------------------------------------------------------------------
-// envs_step_kernel: G = 4 (or 8, MGDP_STEP_GROUP) lanes per env, 256 / G envs per 256-thread
-// workgroup, so a 65536-env batch is 4096 waves (4 per SIMD).  Per env:
+// envs_step_kernel: G = 2 (or 1, 4, 8: MGDP_STEP_GROUP) lanes per env, 256 / G envs per 256-thread
+// workgroup, so a 65536-env batch is 2048 waves (2 per SIMD).  Per env:
 //   * lane v stages row v of the window box with 3 dword loads aligned by v_alignbyte into the
 //     group's LDS window.  The box is the view box after the turn (left / right change only the
 //     direction), extended by one cell along the heading for forward, so it holds both possible
@@ -165,8 +165,10 @@ __device__ __forceinline__ StepOut step_core(const EnvGeo &g, const Rd &rd, int 
 //     shuffles), process_vis runs on the 64-bit mask in bit-parallel form (process_vis_bits), and
 //     the lane encodes its column -- obs bytes [3*vs*i, 3*vs*(i+1)) of the env, contiguous because
 //     the obs is x-major -- into the LDS obs tile, which leaves with 16-B coalesced stores.
-// Measured (DoorKey-16 x 65536, profiles/): one thread per env with three byte planes 49 us per
-// step; 8 lanes per env 16.5 us; one byte plane instead of three, below.
+// Measured (DoorKey-16 x 65536 per step, profiles/r01_step/): one thread per env on three byte
+// planes 49 us; 8 lanes per env 16.5 us; one byte plane + one round trip 15.7 us; 4 lanes 11.4 us;
+// out-of-grid cells staged as walls + a code -> (encoding, see_behind) table in LDS: 4 lanes
+// 11.1 us, 2 lanes 10.2 us.
 // ------------------------------------------------------------------------------------------------
 constexpr int kGroupBlock = 256;  // threads per workgroup (G lanes per env, 256 / G envs)
 
@@ -236,6 +238,17 @@ envs_step_kernel(EnvGeo g, uint8_t *__restrict__ CELL, int32_t *__restrict__ age
     uint8_t *img = smem + slot * OB;
     uint32_t *win = reinterpret_cast<uint32_t *>(smem + round_up(NE * OB, 16)) + slot * (WD + 1);
     uint8_t *wb = reinterpret_cast<uint8_t *>(win);
+    // cell code -> encoded (type | colour << 8 | state << 16) | see_behind << 24 (world_object.py:
+    // not a wall, not a closed / locked door); read per view cell instead of decoding
+    __shared__ uint32_t lut[256];
+    {
+        int t, c, st;
+        cell_decode(threadIdx.x, t, c, st);  // blockDim == 256: one entry per thread
+        c = t == T_EMPTY ? 0 : c;
+        const bool behind = t != T_WALL && !(t == T_DOOR && st != D_OPEN);
+        lut[threadIdx.x] = (uint32_t)t | ((uint32_t)c << 8) | ((uint32_t)st << 16) | ((uint32_t)behind << 24);
+    }
+    __syncthreads();
     if (e < g.B) {
         uint8_t *cell = CELL + (long long)e * g.HWp;
         const int4 ag = reinterpret_cast<const int4 *>(agent)[e];
@@ -257,9 +270,18 @@ envs_step_kernel(EnvGeo g, uint8_t *__restrict__ CELL, int32_t *__restrict__ age
                 const uint32_t *P = reinterpret_cast<const uint32_t *>(cell);
                 uint32_t w[3];
 #pragma unroll
-                for (int q = 0; q < 3; ++q) w[q] = P[min(max(a + q, 0), nd - 1)];  // only in-grid bytes are read
-                win[row * 2 + 0] = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
-                win[row * 2 + 1] = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
+                for (int q = 0; q < 3; ++q) w[q] = P[min(max(a + q, 0), nd - 1)];  // clamped: out-of-grid bytes are replaced below
+                // Out-of-grid cells of the window become grey walls: slice() fills them with Wall()
+                // (grid.py:136-139), which encodes and blocks sight exactly like a grid wall, so the
+                // view loops below need no bounds tests.  Bytes [lo, hi) of the row are in the grid.
+                const int y = by + row;
+                const int lo = min(max(-bx, 0), 8), hi = (unsigned)y < (unsigned)g.H ? min(max(g.W - bx, 0), 8) : 0;
+                const unsigned long long keep = (hi > lo ? (~0ull >> (64 - 8 * (hi - lo))) << (8 * lo) : 0ull);
+                const unsigned long long bytes = ((unsigned long long)__builtin_amdgcn_alignbyte(w[2], w[1], sh) << 32) |
+                                                 __builtin_amdgcn_alignbyte(w[1], w[0], sh);
+                const unsigned long long v = (bytes & keep) | (0x0101010101010101ull * kCodeWall & ~keep);
+                win[row * 2 + 0] = (uint32_t)v;
+                win[row * 2 + 1] = (uint32_t)(v >> 32);
             }
         }
         asm volatile("" ::: "memory");  // the group's rows are written before any lane reads them
@@ -285,49 +307,37 @@ envs_step_kernel(EnvGeo g, uint8_t *__restrict__ CELL, int32_t *__restrict__ age
             }
             asm volatile("" ::: "memory");
             const int fx = kDX[o.d], fy = kDY[o.d], rx = -fy, ry = fx;
-            // Lane r owns view columns i = r, r+G, ...  Column i's world cells (wx0 - fx*j,
-            // wy0 - fy*j) are read branch-free: an out-of-grid cell reads window byte 0 and is then
-            // replaced (out of bounds -> Wall, grid.py:136-139).
+            // Lane r owns view columns i = r, r+G, ...  View cell (i, j) is world (wx0 - fx*j,
+            // wy0 - fy*j) with wx0 = tlx + rx*i, wy0 = tly + ry*i: window byte ow0 - j*(8*fy + fx).
+            // Every view cell lies in the staged box, and out-of-grid ones hold wall codes.
+            const int dj = RB * fy + fx;
             uint32_t cv[NC][VS];
-            bool inb[NC][VS];
             unsigned long long sb = 0;
 #pragma unroll
             for (int k = 0; k < NC; ++k) {
-                const int i = r + G * k;
-                const int wx0 = tlx + rx * i, wy0 = tly + ry * i;
+                const int i = min(r + G * k, VS - 1);  // lanes past the view re-read column VS-1, contribute no bits
+                const int ow0 = (tly + ry * i - by) * RB + (tlx + rx * i - bx);
 #pragma unroll
                 for (int j = 0; j < VS; ++j) {
-                    const int wx = wx0 - fx * j, wy = wy0 - fy * j;
-                    inb[k][j] = i < VS && (unsigned)wx < (unsigned)g.W && (unsigned)wy < (unsigned)g.H;
-                    cv[k][j] = wb[inb[k][j] ? (wy - by) * RB + (wx - bx) : 0];
-                    // see_behind (world_object.py): not a wall (type 2: codes 16..23), not a closed or
-                    // locked door (codes 0x88.. / 0x90..)
-                    const uint32_t x = cv[k][j];
-                    const bool behind = ((x >> 3) != (uint32_t)T_WALL) & ((x & 0x98u) != 0x88u) & ((x & 0x98u) != 0x90u);
-                    sb |= (unsigned long long)(inb[k][j] && behind) << (j * 8 + (i & 7));
+                    cv[k][j] = lut[wb[ow0 - j * dj]];
+                    if (r + G * k < VS) sb |= (unsigned long long)(cv[k][j] >> 24) << (j * 8 + i);
                 }
             }
             sb = group_or<G>(sb);
             const unsigned long long mask = see[e] ? ~0ull : process_vis_bits<VS>(sb);
+            const uint32_t carried = o.ct > 0 ? (uint32_t)o.ct | ((uint32_t)o.cc << 8) : (uint32_t)T_EMPTY;
 #pragma unroll
             for (int k = 0; k < NC; ++k) {  // encode column i, grid.py:244-268; the carried object at (VS/2, VS-1)
                 const int i = r + G * k;
                 if (i < VS) {
                     uint8_t *col = img + i * VS * 3;
-                    const bool centre_col = i == VS / 2;
 #pragma unroll
                     for (int j = 0; j < VS; ++j) {
-                        int t, c, s;
-                        cell_decode(inb[k][j] ? cv[k][j] : kCodeWall, t, c, s);
-                        if (j == VS - 1 && centre_col) {
-                            t = o.ct > 0 ? o.ct : (int)T_EMPTY;
-                            c = o.ct > 0 ? o.cc : 0;
-                            s = 0;
-                        }
-                        const bool vis = (mask >> (j * 8 + i)) & 1ull;
-                        col[3 * j] = (uint8_t)(vis ? t : 0);
-                        col[3 * j + 1] = (uint8_t)(vis ? c : 0);
-                        col[3 * j + 2] = (uint8_t)(vis ? s : 0);
+                        uint32_t x = (j == VS - 1 && i == VS / 2) ? carried : cv[k][j];
+                        x = (mask >> (j * 8 + i)) & 1ull ? x : 0u;
+                        col[3 * j] = (uint8_t)x;
+                        col[3 * j + 1] = (uint8_t)(x >> 8);
+                        col[3 * j + 2] = (uint8_t)(x >> 16);
                     }
                 }
             }
@@ -366,7 +376,7 @@ struct mgdp_envs {
     double *d_rew = nullptr;
     uint32_t nd_mask = 0;
     double death_cost = -1.0;
-    int group = 4;  // lanes per env in envs_step_kernel (MGDP_STEP_GROUP = 2, 4 or 8; 4 measured fastest)
+    int group = 2;  // lanes per env in envs_step_kernel (MGDP_STEP_GROUP = 1, 2, 4 or 8; 2 measured fastest)
     // step-kernel timing (mgdp_envs_enable_timing): pooled event pairs handed to hipExtLaunchKernelGGL
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev, ev_pool;
@@ -397,8 +407,9 @@ int launch_step(mgdp_envs *E, const int32_t *d_act, uint8_t *d_obs, int32_t *d_d
     const int smem = (int)round_up(ne * E->vs * E->vs * 3, 16) + ne * ((E->vs + 1) * kWinRow + 4);
     auto pick = [&](auto k7, auto k5, auto k3) { return E->vs == 7 ? k7 : E->vs == 5 ? k5 : k3; };
     auto k = E->group == 8   ? pick(envs_step_kernel<7, 8>, envs_step_kernel<5, 8>, envs_step_kernel<3, 8>)
-             : E->group == 2 ? pick(envs_step_kernel<7, 2>, envs_step_kernel<5, 2>, envs_step_kernel<3, 2>)
-                             : pick(envs_step_kernel<7, 4>, envs_step_kernel<5, 4>, envs_step_kernel<3, 4>);
+             : E->group == 4 ? pick(envs_step_kernel<7, 4>, envs_step_kernel<5, 4>, envs_step_kernel<3, 4>)
+             : E->group == 1 ? pick(envs_step_kernel<7, 1>, envs_step_kernel<5, 1>, envs_step_kernel<3, 1>)
+                             : pick(envs_step_kernel<7, 2>, envs_step_kernel<5, 2>, envs_step_kernel<3, 2>);
     hipEvent_t ta = nullptr, tb = nullptr;
     if (E->timing) {
         if (E->ev.size() >= 4096) {  // bound the pending pairs
@@ -436,10 +447,11 @@ int mgdp_envs_create(int32_t device, int32_t B, int32_t W, int32_t H, int32_t vi
     int ndev = 0;
     MGDP_HIP(hipGetDeviceCount(&ndev));
     MGDP_CHECK(device >= 0 && device < ndev, MGDP_E_HIP, "device %d not available (%d visible)", device, ndev);
-    int group = 4;
+    int group = 2;
     if (const char *ev = std::getenv("MGDP_STEP_GROUP")) {
         group = std::atoi(ev);
-        MGDP_CHECK(group == 2 || group == 4 || group == 8, MGDP_E_INVALID, "MGDP_STEP_GROUP must be 2, 4 or 8 (got %s)", ev);
+        MGDP_CHECK(group == 1 || group == 2 || group == 4 || group == 8, MGDP_E_INVALID,
+                   "MGDP_STEP_GROUP must be 1, 2, 4 or 8 (got %s)", ev);
     }
     DeviceGuard guard(device);
     mgdp_envs *E = new mgdp_envs();

@@ -27,7 +27,7 @@ def grid_digest(enc):
     return np.frombuffer(hashlib.sha256(enc.tobytes()).digest()[:8], dtype=np.uint64)[0]
 
 
-GROUPS = ["8", "4", "2"]  # MGDP_STEP_GROUP: lanes per env in envs_step_kernel, read at create
+GROUPS = ["8", "4", "2", "1"]  # MGDP_STEP_GROUP: lanes per env in envs_step_kernel, read at create
 
 
 @pytest.mark.parametrize("group", GROUPS)
