@@ -105,6 +105,7 @@ struct mgdp_vi {
     // device-wide synchronisation by another component can wait on it.
     unsigned long long serve_idle_ticks = 10000;     // 100 us at 100 MHz
     unsigned long long serve_life_ticks = 200000000; // 2 s
+    int serve_pollers = 1;  // waves polling the request word (MGDP_SERVE_POLLERS; 1 measured 0.2-0.4 us faster than 4)
     std::chrono::steady_clock::time_point serve_last{};  // host time of the last served result
 };
 
@@ -282,7 +283,7 @@ int launch_serve_t(mgdp_vi *vi, unsigned int served) {
     hipExtLaunchKernelGGL(kern, dim3(1), dim3(vi->fused_block), L.total(), vi->stream, tp.a, tp.b, 0, g,
                           make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv, vi->d_dvenv,
                           vi->d_hout, vi->d_hout + 4, (unsigned long long)served, vi->serve_idle_ticks,
-                          vi->serve_life_ticks);
+                          vi->serve_life_ticks, vi->serve_pollers);
     MGDP_HIP(hipGetLastError());
     return 0;
 }
@@ -399,6 +400,16 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
         }
     }
     std::atomic_thread_fence(std::memory_order_acquire);
+#ifdef MGDP_SERVE_TRACE
+    // trace build (tools/probe_serve_trace.sh): server-side s_memrealtime stamps, 10 ns ticks --
+    // [8] request seen by the workgroup, [9] result about to be published
+    if (tagged) {
+        static double n = 0, solve = 0;
+        n += 1;
+        solve += (double)(h[9] - h[8]) * 0.01;
+        if ((long long)n % 1000 == 0) std::fprintf(stderr, "serve trace: %.0f solves, request seen -> publish %.3f us\n", n, solve / n);
+    }
+#endif
     unsigned long long km, dvb, kmin;
     if (tagged) {
         km = kmin = h[5] & 0xffffffffull;
@@ -656,7 +667,7 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
             e = hipMemcpy(vi->d_rgoal, rg.data(), rg.size(), hipMemcpyHostToDevice);
         }
     }
-    if (e == hipSuccess) e = hipHostMalloc((void **)&vi->h_out, 8 * sizeof(unsigned long long),
+    if (e == hipSuccess) e = hipHostMalloc((void **)&vi->h_out, 16 * sizeof(unsigned long long),
                                            hipHostMallocMapped | hipHostMallocCoherent);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&vi->d_hout, vi->h_out, 0);
     if (e == hipSuccess) {
@@ -680,9 +691,10 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
         vi->sweep_pipe = 0;  // one thread per cell: grids of <= 1024 cells
     if (const char *ev = std::getenv("MGDP_SERVE_IDLE_US"))  // s_memrealtime ticks at 100 MHz
         vi->serve_idle_ticks = (unsigned long long)std::max(1LL, std::atoll(ev)) * 100ull;
+    if (const char *ev = std::getenv("MGDP_SERVE_POLLERS")) vi->serve_pollers = std::max(1, std::atoi(ev));
     if (const char *ev = std::getenv("MGDP_SERVE_LIFE_US"))
         vi->serve_life_ticks = (unsigned long long)std::max(1LL, std::atoll(ev)) * 100ull;
-    if (vi->h_out) std::memset(vi->h_out, 0, 8 * sizeof(unsigned long long));
+    if (vi->h_out) std::memset(vi->h_out, 0, 16 * sizeof(unsigned long long));
     if (e == hipSuccess) {  // arm the fused reduction (every launch re-arms it for the next)
         std::vector<unsigned long long> init((size_t)kRedShards * 4 + 2, 0ull);
         for (size_t i = 2; i < (size_t)kRedShards * 4; i += 4) init[i] = 0x7fffffffull;

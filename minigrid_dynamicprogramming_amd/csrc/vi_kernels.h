@@ -46,7 +46,12 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     T diff = (T)0;
     auto done = [&](int kk, double dv) {
         if (SERVED) {
-            if (threadIdx.x == 0) publish_tagged(host_out, kk, dv, epoch);
+            if (threadIdx.x == 0) {
+#ifdef MGDP_SERVE_TRACE
+                __hip_atomic_store(host_out + 9, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
+                publish_tagged(host_out, kk, dv, epoch);
+            }
         } else if (lone && threadIdx.x == 0) {
             publish(host_out, (unsigned long long)kk, (unsigned long long)__double_as_longlong(dv),
                     (unsigned long long)kk, epoch);
@@ -163,7 +168,7 @@ __global__ void __launch_bounds__(WP > 0 ? 64 : 1024)
 vi_serve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ host_out, const unsigned long long *__restrict__ host_cmd,
-                unsigned long long served, unsigned long long idle_ticks, unsigned long long life_ticks) {
+                unsigned long long served, unsigned long long idle_ticks, unsigned long long life_ticks, int pollers) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ unsigned long long s_cmd;
     const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
@@ -182,7 +187,7 @@ vi_serve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
         else topo = dk_topo_soa(cl, geo, cc);
     }
     while (true) {
-        if (lane == 0) {
+        if (lane == 0 && wave < pollers) {  // the other waves wait at the barrier
             for (int i = 0; i < wave; ++i) __builtin_amdgcn_s_sleep(8);  // stagger the pollers
             while (true) {
                 const unsigned long long cmd = __hip_atomic_load(host_cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -202,6 +207,10 @@ vi_serve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
         __syncthreads();
         const unsigned long long cmd = s_cmd;
         if (cmd == kServeQuit) break;
+#ifdef MGDP_SERVE_TRACE
+        if (threadIdx.x == 0)
+            __hip_atomic_store(host_out + 8, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
         int k;
         double dvl;
         if (!fused_grid<T, MODEL, SLIP, MAP, true, WP>(geo, cf, cells, V, pi, kenv, dvenv, host_out, -1, 1, true,
@@ -210,7 +219,11 @@ vi_serve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
             publish_tagged(host_out, k, dvl, (unsigned int)cmd);
         served = cmd;
         t_last = __builtin_amdgcn_s_memrealtime();
-        __syncthreads();  // every wave is past s_cmd and the LDS tiles before the next request
+        // Every wave is past s_cmd and the LDS tiles before the next request: an LDS-only barrier.
+        // The V / pi stores of this solve stay in flight while the next request is polled (a
+        // __syncthreads would drain them first); the host reads V / pi only after server_stop
+        // has drained the stream.
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
 }
 
