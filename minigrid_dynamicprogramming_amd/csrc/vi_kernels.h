@@ -157,7 +157,9 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
 // cannot change while it is resident (every other entry point stops it first), so they are staged
 // in LDS once.  Lane 0 of every wave polls the request word (relaxed system-scope loads, the waves
 // staggered by s_sleep so a new request is seen a fraction of a round trip after it lands) and
-// also watches the LDS word another wave may already have set.  Request r (!= the last served)
+// also watches the LDS word another wave may already have set.  By default only wave 0 polls
+// (`pollers` = 1; the others wait at the barrier): with four staggered pollers the barrier also
+// waited for the other waves' in-flight PCIe reads (measured 0.2-0.4 us per solve slower).  Request r (!= the last served)
 // runs a fresh fused solve whose {k, dV} is published tagged with r.  Every wave leaves on the quit
 // word, after `idle_ticks` without a request or after `life_ticks` in total (s_memrealtime,
 // 100 MHz); the host relaunches the server if a request finds it gone.
