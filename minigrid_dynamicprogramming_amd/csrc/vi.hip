@@ -90,6 +90,7 @@ struct mgdp_vi {
     int pair = 0;                 // fused XYD: two-sweep step
     int wave_p = 0;               // lone XYD grid on one wave: cells per lane (fused_wave_xyd)
     int cpt = 1;                  // batched XYD fused path: cells per thread (MGDP_CPT; 2 = fused_fast_xyd_soa_x2)
+    int dk1t = 0;                 // batched fp32 DoorKey on one LDS tile (MGDP_DK_1T; fused_fast_dk_1t)
     int sweep_block = 256;
     int sweep_m = 1;              // grids staged per workgroup iteration (measured: m>1 no faster)
     int sweep_pipe = 2;           // register-pipelined sweep kernel: grids fetched ahead (0 = staged kernel)
@@ -253,6 +254,8 @@ int launch_fused_t(mgdp_vi *vi, int k_target) {
     if constexpr (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL)
         if (vi->cpt == 2) kern = FusedK<T, MODEL, SLIP, MAP, -2>::fn;
         else if (vi->cpt == 4) kern = FusedK<T, MODEL, SLIP, MAP, -4>::fn;
+    if constexpr (MODEL == MGDP_MODEL_DOORKEY && MAP == MGDP_MAP_CELL && !SLIP)
+        if (vi->dk1t) kern = FusedK<T, MODEL, SLIP, MAP, kWpDk1t>::fn;
     if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
     TimedPair tp;
     if (int rc = timed_begin(vi, -1, &tp)) return rc;
@@ -636,6 +639,13 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
             vi->fused_block = (int)round_up((vi->HW + cpt - 1) / cpt, 64);
             vi->HWs = cpt * vi->fused_block;
             vi->Ss = vi->S / vi->HW * vi->HWs;
+        }
+        int dk1t = 0;
+        if (const char *ev = std::getenv("MGDP_DK_1T")) dk1t = std::atoi(ev) != 0;
+        if (dk1t && d.B > 1 && d.model == MGDP_MODEL_DOORKEY && d.dtype == MGDP_F32 && d.method == MGDP_METHOD_FUSED &&
+            !vi->opts && vi->HW <= vi->fused_block) {
+            vi->dk1t = 1;
+            vi->nbuf = 1;  // one V tile in LDS
         }
     } else {
         int blk = d.B == 1 ? 1024 : 256;

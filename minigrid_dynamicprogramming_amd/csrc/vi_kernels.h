@@ -5,6 +5,7 @@
 #pragma once
 
 namespace mgdp {
+constexpr int kWpDk1t = -100;  // vi_fused_kernel variant tag: batched DoorKey on one LDS tile
 template <typename T, int MODEL> struct TopoOf { using type = XydTopo<T>; };
 template <typename T> struct TopoOf<T, MGDP_MODEL_DOORKEY> { using type = DkTopo; };
 
@@ -29,8 +30,10 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     const bool work = k_target < 0 ? (!(k > 0 && dvl < geo.tol) && k < geo.max_sweeps) : (k < k_target);
     if (!work) return false;
     const long long vb = (long long)e * geo.S;
-    // WP < 0: -WP cells per thread on the batched direction-major path (fused_fast_xyd_soa_xn)
-    constexpr int CPT = WP < 0 ? -WP : 1;
+    // WP == kWpDk1t: batched DoorKey on one LDS tile (fused_fast_dk_1t); other WP < 0: -WP cells per
+    // thread on the batched XYD direction-major path (fused_fast_xyd_soa_xn)
+    constexpr bool DK1T = WP == kWpDk1t;
+    constexpr int CPT = WP < 0 && !DK1T ? -WP : 1;
     const bool fast = MAP == MGDP_MAP_CELL && geo.HW <= CPT * (int)blockDim.x;
     const bool soa = fast && !geo.pair && !geo.quad;
     if (!SERVED) copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
@@ -71,7 +74,10 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
         return true;
     }
     if (SERVED || soa) {  // served lone grids are always on this path (serve_eligible): no other code in the server
-        if constexpr (MODEL == MGDP_MODEL_XYD && CPT > 1) {
+        if constexpr (MODEL == MGDP_MODEL_DOORKEY && DK1T) {
+            if (k_target < 0) fused_fast_dk_1t<T, true>(geo, cf, cl, V0, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+            else fused_fast_dk_1t<T, false>(geo, cf, cl, V0, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+        } else if constexpr (MODEL == MGDP_MODEL_XYD && CPT > 1) {
             if (k_target < 0) fused_fast_xyd_soa_xn<T, SLIP, true, CPT>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
             else fused_fast_xyd_soa_xn<T, SLIP, false, CPT>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
         } else if constexpr (MODEL == MGDP_MODEL_XYD) {

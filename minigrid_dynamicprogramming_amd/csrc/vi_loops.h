@@ -582,6 +582,80 @@ __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> 
     }
 }
 
+// Batched DoorKey grids on ONE LDS tile (fp32): the two 16 KB tiles of fused_fast_dk_soa cap a CU
+// at 4 resident 16x16 grids, one tile at 8.  A sweep reads the neighbours' V_k from the tile,
+// passes a barrier (every read is done), tests the previous sweep's stop flags (read before the
+// barrier, so the test waits for nothing), computes V_{k+1} and overwrites the tile, then passes
+// the usual barrier: two barriers per sweep, same arithmetic.  The own cell's V_{k-1} and the
+// neighbour values it met stay in the alternating register sets, which is what the final pi pass
+// (argmax on V_{k-1}) needs; a sweep stopped by the test computes nothing.
+template <typename T, bool LOCAL, typename Done>
+__device__ __forceinline__ void fused_fast_dk_1t(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *Vt,
+                                                 T *slots, uint8_t *flags, const T *Vg, T *Vg_out, int8_t *pig,
+                                                 int &k, int k_target, double &dvl, const Done &done) {
+    const int c = threadIdx.x;
+    const int cc = c < geo.HW ? c : 0;
+    const bool own_cell = c < geo.HW;
+    const int HW = geo.HWs;
+    const int k_start = k;
+    const DkTopo tp = dk_topo_soa(cl, geo, cc);
+    T a[16], b[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const V4<T> x = k == 0 ? V4<T>{{(T)0, (T)0, (T)0, (T)0}} : *reinterpret_cast<const V4<T> *>(Vg + cc * 16 + 4 * q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[4 * q + j] = x.v[j];
+        *reinterpret_cast<V4<T> *>(Vt + (q * HW + c) * 4) = x;
+    }
+    __syncthreads();
+    int parity = 0;
+    T diff = (T)0;
+    V4<T> na[4], nb[4];
+    auto sweep = [&](const T (&in)[16], T (&outv)[16], V4<T> (&nbs)[4]) -> bool {
+        if (LOCAL ? k >= geo.max_sweeps : k >= k_target) return false;
+        uint4 fl = make_uint4(0u, 0u, 0u, 0u);
+        if (LOCAL) fl = *reinterpret_cast<const uint4 *>(flags + (parity ^ 1) * 16);
+        dk_load_nb(tp, Vt, nbs);
+        __syncthreads();  // every read of V_k is done before the tile is overwritten
+        if (LOCAL && k > k_start && (fl.x | fl.y | fl.z | fl.w) == 0u) return false;
+        uint32_t pk[4];
+        diff = dk_step<T, false>(tp, cf, in, nbs, outv, pk);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<V4<T> *>(Vt + (q * HW + c) * 4) =
+                V4<T>{{outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]}};
+        if (LOCAL) flag_write(diff >= cf.tol, flags, parity);
+        __syncthreads();
+        parity ^= 1;
+        ++k;
+        return true;
+    };
+    int last = 0;  // 0: the last committed sweep was a -> b with na; 1: b -> a with nb (one always commits)
+    while (true) {
+        if (!sweep(a, b, na)) break;
+        last = 0;
+        if (!sweep(b, a, nb)) break;
+        last = 1;
+    }
+    dvl = (double)block_max(diff, slots, 0);
+    done(k, dvl);
+    if (own_cell) {  // pi on V_{k-1}: the last committed sweep's input set and the neighbours it read
+        T tmp[16];
+        uint32_t pk[4];
+        if (last == 0) dk_step<T, true>(tp, cf, a, na, tmp, pk);
+        else dk_step<T, true>(tp, cf, b, nb, tmp, pk);
+        *reinterpret_cast<uint4 *>(pig + c * 16) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {  // V_k (element selects: a pointer to either set would put both in scratch)
+            V4<T> x;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x.v[j] = last == 0 ? b[4 * q + j] : a[4 * q + j];
+            *reinterpret_cast<V4<T> *>(Vg_out + c * 16 + 4 * q) = x;
+        }
+    }
+}
+
+
 // Two-sweep step for the XYD fast path (geo.pair, three LDS buffers).  V_{k+2}[c, d] needs V_{k+1} only at
 // the cell itself and at state (front(c, d), d); the thread recomputes that neighbour state with
 // exactly the neighbour's own operations (bit-identical), so two Jacobi sweeps cost one barrier.

@@ -307,10 +307,13 @@ def test_persistent_server_lifetime_cap_relaunch(monkeypatch):
 
 @pytest.mark.parametrize("persistent", ["0", "1"])
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
-def test_fused_doorkey_lone_and_batched_bit_exact(persistent, dtype, monkeypatch):
-    """DoorKey fused local loop, lone (persistent server or one launch) and batched, including
-    max_sweeps caps that end the loop before convergence."""
+@pytest.mark.parametrize("one_tile", ["0", "1"])
+def test_fused_doorkey_lone_and_batched_bit_exact(persistent, dtype, one_tile, monkeypatch):
+    """DoorKey fused local loop, lone (persistent server or one launch) and batched (two LDS tiles,
+    or one tile with two barriers per sweep: MGDP_DK_1T, fp32 batches), including max_sweeps caps
+    that end the loop before convergence."""
     monkeypatch.setenv("MGDP_PERSISTENT", persistent)
+    monkeypatch.setenv("MGDP_DK_1T", one_tile)
     for env in ("doorkey8", "doorkey16"):
         g = load(f"grids_{env}.npz")
         cells = np.stack([cells_from_enc(e) for e in g["enc"]])

@@ -11,6 +11,7 @@ timeout -k 10 300 python bench.py --no-cpu --no-hbm > $OUT/bench_default.json 2>
 for w in empty16x65536 doorkey65536 lava65536 fourrooms4096; do
   timeout -k 10 300 python bench.py --workload $w --steps 5 --warmup 1 --no-cpu > $OUT/bench_$w.json 2> $OUT/bench_$w.err || { echo "bench $w failed"; exit 1; }
 done
+timeout -k 10 300 env MGDP_DK_1T=1 python bench.py --workload doorkey65536 --steps 5 --warmup 1 --no-cpu > $OUT/bench_doorkey65536_dk1t.json 2> /dev/null || { echo "bench dk1t failed"; exit 1; }
 for w in empty16x65536 doorkey65536 lava65536 fourrooms4096; do
   timeout -k 10 300 env MGDP_CPT=1 python bench.py --workload $w --steps 5 --warmup 1 --no-cpu > $OUT/bench_${w}_cpt1.json 2> /dev/null || { echo "bench $w cpt1 failed"; exit 1; }
   timeout -k 10 300 env MGDP_CPT=4 python bench.py --workload $w --steps 5 --warmup 1 --no-cpu > $OUT/bench_${w}_cpt4.json 2> /dev/null || { echo "bench $w cpt4 failed"; exit 1; }
