@@ -198,10 +198,13 @@ def _solve_one(cells, dtype="f32", **kw):
     return out
 
 
+@pytest.mark.parametrize("pollers", ["1", "4"])
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
-def test_persistent_server_matches_launches(dtype, monkeypatch):
-    """A lone grid is solved by the resident vi_serve_kernel; it agrees bit for bit with one fused
-    launch per solve (MGDP_PERSISTENT=0) and with the oracle."""
+def test_persistent_server_matches_launches(dtype, pollers, monkeypatch):
+    """A lone grid is solved by the resident vi_serve_kernel (one or four waves polling the
+    request word, MGDP_SERVE_POLLERS); it agrees bit for bit with one fused launch per solve
+    (MGDP_PERSISTENT=0) and with the oracle."""
+    monkeypatch.setenv("MGDP_SERVE_POLLERS", pollers)
     for name in ("empty16_s0", "fourrooms_s1", "lava11n5_s0", "doorkey8_s2", "doorkey16_s0"):
         t = load(f"table_{name}.npz")
         cells = cells_from_enc(t["enc"])[None]
