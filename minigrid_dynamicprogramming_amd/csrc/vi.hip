@@ -394,6 +394,7 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
                 if (ready()) break;
                 if (tagged && relaunches < 4) {
                     ++relaunches;
+                    DeviceGuard guard(vi->d.device);  // the served fast path of mgdp_vi_solve holds none
                     if (int rc = dispatch<ServeF>(vi, vi->epoch - 1u)) return rc;
                     continue;
                 }
@@ -883,6 +884,46 @@ int mgdp_vi_finish(mgdp_vi *vi, int32_t sweeps) {
 
 int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *converged_out) {
     MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
+    // Resident lone-grid server: a solve is a request word and a wait on host memory, so the
+    // steady state makes no HIP call at all (no device guard either); anything else -- a server
+    // that may be leaving, a rounding-level fallback sweep -- takes the general path below.
+    if (vi->serving && serve_eligible(vi) && vi->d.horizon == 0) {
+        const double idle_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - vi->serve_last).count();
+        if (idle_us * 100.0 <= 0.5 * (double)vi->serve_idle_ticks) {
+            vi->cur = 0;
+            vi->k_done = 0;
+            vi->k_done_valid = false;
+            ++vi->epoch;
+            __atomic_store_n(vi->h_out + 4, (unsigned long long)vi->epoch, __ATOMIC_RELEASE);
+            vi->fresh = 0;
+            int32_t k = 0;
+            if (int rc = reduce_env(vi, &k, nullptr)) return rc;
+            vi->serve_last = std::chrono::steady_clock::now();
+            const double dv = vi->dv_red;
+            if (dv < vi->d.tol || k >= vi->d.max_sweeps) {
+                vi->k_done = k;
+                vi->sweeps = k;
+                vi->converged = dv < vi->d.tol;
+                if (sweeps_out) *sweeps_out = k;
+                if (dv_out) *dv_out = dv;
+                if (converged_out) *converged_out = vi->converged;
+                return 0;
+            }
+            // rounding broke the contraction: continue under the global rule on the general path
+            double dv2 = dv;
+            if (int rc = mgdp_vi_run_to(vi, k, &dv2)) return rc;
+            while (!(dv2 < vi->d.tol) && k < vi->d.max_sweeps) {
+                if (int rc = mgdp_vi_sweep(vi, &dv2)) return rc;
+                ++k;
+            }
+            if (int rc = mgdp_vi_finish(vi, k)) return rc;
+            vi->converged = dv2 < vi->d.tol;
+            if (sweeps_out) *sweeps_out = k;
+            if (dv_out) *dv_out = dv2;
+            if (converged_out) *converged_out = vi->converged;
+            return 0;
+        }
+    }
     if (int rc = mgdp_vi_reset(vi)) return rc;
     int32_t k = 0;
     if (int rc = mgdp_vi_run_local(vi, &k)) return rc;
