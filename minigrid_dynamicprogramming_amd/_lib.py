@@ -114,6 +114,21 @@ def lib_path() -> str:
     return LIB_PATH
 
 
+_RAW = None
+
+
+def raw_fn(name: str):
+    """`name` from a second handle on the loaded library with no argtypes: for hot calls whose
+    arguments are already ctypes objects, so the call skips ctypes' per-argument conversion."""
+    global _RAW
+    load()  # the checked load (ABI version, symbols) happens once
+    if _RAW is None:
+        _RAW = ctypes.CDLL(LIB_PATH)
+    fn = getattr(_RAW, name)
+    fn.restype = ctypes.c_int
+    return fn
+
+
 def load():
     """Load libmgdp.so (raises if it has not been built; see minigrid_dynamicprogramming_amd.build)."""
     global _lib

@@ -228,10 +228,12 @@ class ValueIteration:
 
     # -- single-device solve
     def solve(self) -> int:
-        if self._solve_args is None:  # reused out-parameters: no ctypes allocations per solve
+        if self._solve_args is None:  # reused ctypes arguments: nothing converted or allocated per solve
             self._out = (ctypes.c_int32(0), ctypes.c_double(0), ctypes.c_int32(0))
-            self._solve_args = (self.h,) + tuple(ctypes.byref(o) for o in self._out)
-        rc = self.L.mgdp_vi_solve(*self._solve_args)
+            self._solve_args = (ctypes.c_void_p(self.h.value if isinstance(self.h, ctypes.c_void_p) else self.h),) + \
+                tuple(ctypes.byref(o) for o in self._out)
+            self._solve_fn = _lib.raw_fn("mgdp_vi_solve")
+        rc = self._solve_fn(*self._solve_args)
         if rc:
             _lib.check(rc, "mgdp_vi_solve")
         k, dv, conv = self._out
