@@ -398,3 +398,36 @@ def test_one_wave_lone_grid_sizes(dtype, monkeypatch):
         np.testing.assert_array_equal(vi.values(), o["V"])
         np.testing.assert_array_equal(vi.policy(), o["pi"])
         vi.close()
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_maximum_and_ragged_grid_sizes(dtype, monkeypatch):
+    """The largest grids the LDS-resident kernels take (32 x 32 = 1024 cells: one thread per cell,
+    or 512 threads at two cells per thread) and non-square ones, lone and batched, every XYD
+    method against the oracle bit for bit; DoorKey at 32 x 32 in fp32 (two 64 KB V tiles) and the
+    refusal of the fp64 one, which cannot fit LDS."""
+    rng = np.random.default_rng(11)
+    for W, H in ((32, 32), (32, 7), (5, 32), (31, 29)):
+        cells = np.stack([_random_xyd_grid(rng, W, H) for _ in range(3)])
+        for sub in (cells[:1], cells):
+            o = oracle.value_iteration(0, sub, dtype=dtype)
+            for method, cpt in (("fused", "1"), ("fused", "2"), ("sweep", "1")):
+                monkeypatch.setenv("MGDP_CPT", cpt)
+                r = gpu_vi(sub, "xyd", dtype, method, "cell")
+                assert r.sweeps == o["sweeps"], (W, H, method, cpt)
+                np.testing.assert_array_equal(r.V, o["V"])
+                np.testing.assert_array_equal(r.pi, o["pi"])
+    from minigrid_dynamicprogramming_amd.envs import DoorKeyEnv
+
+    env = DoorKeyEnv(size=32)
+    dk = np.stack([env.generate(seed=s)[0][..., 0].T for s in range(3)]).astype(np.uint8)
+    if dtype == "f32":
+        for sub in (dk[:1], dk):
+            o = oracle.value_iteration(1, sub, dtype="f32")
+            r = gpu_vi(sub, "doorkey", "f32", "fused", "cell")
+            assert r.sweeps == o["sweeps"]
+            np.testing.assert_array_equal(r.V, o["V"])
+            np.testing.assert_array_equal(r.pi, o["pi"])
+    else:
+        with pytest.raises(ValueError):
+            gpu_vi(dk[:1], "doorkey", "f64", "fused", "cell")
