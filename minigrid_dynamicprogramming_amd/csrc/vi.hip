@@ -334,6 +334,8 @@ int launch_sweep_t(mgdp_vi *vi, int k, int check_prev, bool policy) {
     if constexpr (MAP == MGDP_MAP_CELL) {
         if (vi->sweep_pipe == 1) return launch_sweep_pipe<T, MODEL, SLIP, 1>(vi, Vin, Vout, k, check_prev, tp);
         if (vi->sweep_pipe == 2) return launch_sweep_pipe<T, MODEL, SLIP, 2>(vi, Vin, Vout, k, check_prev, tp);
+        if (vi->sweep_pipe == 3) return launch_sweep_pipe<T, MODEL, SLIP, 3>(vi, Vin, Vout, k, check_prev, tp);
+        if (vi->sweep_pipe == 4) return launch_sweep_pipe<T, MODEL, SLIP, 4>(vi, Vin, Vout, k, check_prev, tp);
     }
     return launch_sweep_kernel<T, MODEL, SLIP, MAP, false>(vi, Vin, Vout, k, check_prev, tp);
 }
@@ -696,7 +698,7 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     // compulsory: the prefetch registers collide with the 16-state backup's), so it keeps the
     // staged kernel unless MGDP_SWEEP_PIPE asks otherwise.
     if (d.model == MGDP_MODEL_DOORKEY) vi->sweep_pipe = 0;
-    if (const char *ev = std::getenv("MGDP_SWEEP_PIPE")) vi->sweep_pipe = std::min(2, std::max(0, std::atoi(ev)));
+    if (const char *ev = std::getenv("MGDP_SWEEP_PIPE")) vi->sweep_pipe = std::min(4, std::max(0, std::atoi(ev)));
     if (vi->HW > 1024 || d.mapping != MGDP_MAP_CELL ||
         sweep_pipe_smem_bytes(vi->S, vi->HW, vi->HWs, vi->HWp, vi->tsize) > 160 * 1024)
         vi->sweep_pipe = 0;  // one thread per cell: grids of <= 1024 cells

@@ -505,13 +505,12 @@ vi_sweep_pipe_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, con
         __syncthreads();  // the tile is rewritten by the next grid
     };
     int e = blockIdx.x;
-    while (true) {
-        if (e >= geo.B) break;
-        step(e, rows[0]);
-        e += stride;
-        if (DEPTH > 1) {
-            if (e >= geo.B) break;
-            step(e, rows[DEPTH - 1]);
+    bool more = true;
+    while (more) {  // the register slots rotate: slot j holds the grid DEPTH strides ahead of it
+#pragma unroll
+        for (int j = 0; j < DEPTH; ++j) {
+            if (e >= geo.B) { more = false; break; }
+            step(e, rows[j]);
             e += stride;
         }
     }

@@ -431,3 +431,21 @@ def test_maximum_and_ragged_grid_sizes(dtype, monkeypatch):
     else:
         with pytest.raises(ValueError):
             gpu_vi(dk[:1], "doorkey", "f64", "fused", "cell")
+
+
+@pytest.mark.parametrize("pipe", ["0", "1", "2", "3", "4"])
+def test_sweep_method_pipeline_depths(pipe, monkeypatch):
+    """The per-sweep HBM method on the staged kernel (MGDP_SWEEP_PIPE=0) and on the register-
+    pipelined kernel with grids fetched 1-4 strides ahead: every depth bit-exact vs the oracle,
+    batches that do not divide the grid-stride (tail handling) included."""
+    monkeypatch.setenv("MGDP_SWEEP_PIPE", pipe)
+    for env in ("fourrooms", "lava11n5"):
+        g = load(f"grids_{env}.npz")
+        cells = np.stack([cells_from_enc(e) for e in g["enc"]])
+        for sub in (cells[:1], cells[:5], cells):
+            for dtype in ("f32", "f64"):
+                r = gpu_vi(sub, "xyd", dtype, "sweep", "cell")
+                o = oracle.value_iteration(0, sub, dtype=dtype)
+                assert r.sweeps == o["sweeps"]
+                np.testing.assert_array_equal(r.V, o["V"])
+                np.testing.assert_array_equal(r.pi, o["pi"])
