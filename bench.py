@@ -109,6 +109,11 @@ def cpu_baseline(cells, model, gamma, tol, dtype, budget_s=8.0, nthreads=1):
 
     model_id = 0 if model == "xyd" else 1
     sample = cells[: min(len(cells), 32)]
+    replicated = nthreads > 1 and len(sample) < nthreads
+    if replicated:
+        # A lone-grid workload gives each thread 64 states per sweep, so a threaded solve measures
+        # fork/join, not the cores: time nthreads independent replicas instead (same sweeps).
+        sample = np.repeat(sample[:1], nthreads, axis=0)
     S = sample.shape[1] * sample.shape[2] * (4 if model_id == 0 else 16)
     A = 7 if model_id == 0 else 5
     updates = 0
@@ -123,6 +128,7 @@ def cpu_baseline(cells, model, gamma, tol, dtype, budget_s=8.0, nthreads=1):
             break
     return {"value": updates / el, "unit": "updates/s", "cores": nthreads, "kind": "port",
             "sample": f"{solves} full solves of {len(sample)} grid(s) of the same workload "
+                      f"{'(replicas of the one grid) ' if replicated else ''}"
                       f"({r['sweeps']} sweeps each, {dtype}), oracle/mgdp_oracle.c, {el:.1f} s"}
 
 
