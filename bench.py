@@ -105,31 +105,47 @@ def make_cells(spec, rank, world):
 
 def cpu_baseline(cells, model, gamma, tol, dtype, budget_s=8.0, nthreads=1):
     """Time the oracle (oracle/, a C restatement of the same algorithm) on a bounded sample."""
+    import threading
+
     from oracle import oracle
 
     model_id = 0 if model == "xyd" else 1
     sample = cells[: min(len(cells), 32)]
-    replicated = nthreads > 1 and len(sample) < nthreads
-    if replicated:
-        # A lone-grid workload gives each thread 64 states per sweep, so a threaded solve measures
-        # fork/join, not the cores: time nthreads independent replicas instead (same sweeps).
-        sample = np.repeat(sample[:1], nthreads, axis=0)
     S = sample.shape[1] * sample.shape[2] * (4 if model_id == 0 else 16)
     A = 7 if model_id == 0 else 5
-    updates = 0
-    solves = 0
+    # A lone-grid workload gives each OpenMP thread 64 states per sweep, so a threaded solve times
+    # fork/join, not the cores: run one independent single-threaded solve loop per thread instead
+    # (ctypes drops the GIL inside the oracle call).
+    replicated = nthreads > 1 and len(sample) < nthreads
+    loops = nthreads if replicated else 1
+    per_call = 1 if replicated else nthreads
+    counts = [[0, 0, 0] for _ in range(loops)]  # updates, solves, sweeps
     t0 = time.perf_counter()
-    while True:
-        r = oracle.value_iteration(model_id, sample, gamma, tol, dtype=dtype, nthreads=nthreads)
-        updates += len(sample) * S * A * r["sweeps"]
-        solves += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
+
+    def loop(c):
+        while True:
+            r = oracle.value_iteration(model_id, sample, gamma, tol, dtype=dtype, nthreads=per_call)
+            c[0] += len(sample) * S * A * r["sweeps"]
+            c[1] += 1
+            c[2] = r["sweeps"]
+            if time.perf_counter() - t0 >= budget_s:
+                break
+
+    if loops == 1:
+        loop(counts[0])
+    else:
+        ts = [threading.Thread(target=loop, args=(c,)) for c in counts]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    el = time.perf_counter() - t0
+    updates = sum(c[0] for c in counts)
+    solves = sum(c[1] for c in counts)
+    how = f", {loops} threads each solving its own replica" if replicated else ""
     return {"value": updates / el, "unit": "updates/s", "cores": nthreads, "kind": "port",
             "sample": f"{solves} full solves of {len(sample)} grid(s) of the same workload "
-                      f"{'(replicas of the one grid) ' if replicated else ''}"
-                      f"({r['sweeps']} sweeps each, {dtype}), oracle/mgdp_oracle.c, {el:.1f} s"}
+                      f"({counts[0][2]} sweeps each, {dtype}{how}), oracle/mgdp_oracle.c, {el:.1f} s"}
 
 
 def load_traffic(key, solves_per_launch):
