@@ -375,14 +375,14 @@ vi_sweep_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, const T 
         const long long vb = (long long)e0 * geo.S;
         __syncthreads();  // the previous group's LDS tile is no longer read
         copy16(cl, cells + (long long)e0 * geo.HWp, me * geo.HWp);
-        copy16(Vi, Vin + vb, me * vbytes);
+        copy16_nt_in(Vi, Vin + vb, me * vbytes);
         __syncthreads();
         for (int j = 0; j < me; ++j)
             acc = vmax(acc, sweep_lds<T, MODEL, SLIP, MAP, !POLICY, POLICY || MAP == MGDP_MAP_SA>(
                                 geo, cf, cl + j * geo.HWp, Vi + j * geo.S, Vo + j * geo.S, pis + j * pib));
         __syncthreads();
         if (!POLICY) {
-            copy16(Vout + vb, Vo, me * vbytes);
+            copy16_nt_out(Vout + vb, Vo, me * vbytes);
         } else {
             for (int j = 0; j < me; ++j) copy_pi(pi + vb + (long long)j * geo.S, pis + j * pib, geo.S);
         }
@@ -416,6 +416,33 @@ __host__ __device__ inline int sweep_pipe_smem_bytes(int S, int HW, int HWs, int
     return S / HW * HWs * tsize + HWp + 256;
 }
 
+// V is streamed once per sweep (Vin read, Vout written; the next sweep's Vin is the whole
+// 553 MB array again, far past the 256 MB MALL), so the loads and stores are nontemporal:
+// bit 0 stores, bit 1 loads.  Measured on empty16x65536 (profiles/r01_sweep_nt/): 107.8 µs
+// plain, 101.5 µs stores only, 98.0 µs both.
+#ifndef MGDP_SWEEP_NT
+#define MGDP_SWEEP_NT 3
+#endif
+template <typename T>
+__device__ __forceinline__ void st_v4(V4<T> *dst, const V4<T> &v) {
+    if (MGDP_SWEEP_NT & 1) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) __builtin_nontemporal_store(v.v[j], &dst->v[j]);
+    } else {
+        *dst = v;
+    }
+}
+template <typename T>
+__device__ __forceinline__ V4<T> ld_v4(const V4<T> *src) {
+    if (MGDP_SWEEP_NT & 2) {
+        V4<T> v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v.v[j] = __builtin_nontemporal_load(&src->v[j]);
+        return v;
+    }
+    return *src;
+}
+
 template <typename T, int MODEL, bool SLIP, int DEPTH>
 __global__ void __launch_bounds__(1024)
 vi_sweep_pipe_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, const T *__restrict__ Vin,
@@ -442,7 +469,7 @@ vi_sweep_pipe_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, con
         const long long ee = e < geo.B ? e : geo.B - 1;
         const V4<T> *src = reinterpret_cast<const V4<T> *>(Vin + ee * geo.S + (long long)cc * 4 * NV);
 #pragma unroll
-        for (int q = 0; q < NV; ++q) r.v[q] = src[q];
+        for (int q = 0; q < NV; ++q) r.v[q] = ld_v4(src + q);
         r.cw = reinterpret_cast<const uint32_t *>(cells + ee * geo.HWp)[cw_idx];
     };
     Row rows[DEPTH];
@@ -481,7 +508,7 @@ vi_sweep_pipe_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, con
             uint32_t pk;
             const T dv = xyd_step<T, SLIP, false>(tp, cf, own.v[0], nbv, out, pk);
             if (own_cell) {
-                *reinterpret_cast<V4<T> *>(dst) = out;
+                st_v4(reinterpret_cast<V4<T> *>(dst), out);
                 acc = vmax(acc, dv);
             }
         } else {
@@ -498,7 +525,7 @@ vi_sweep_pipe_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, con
             if (own_cell) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                    reinterpret_cast<V4<T> *>(dst)[q] = V4<T>{{outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]}};
+                    st_v4(reinterpret_cast<V4<T> *>(dst) + q, V4<T>{{outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]}});
                 acc = vmax(acc, dv);
             }
         }

@@ -120,6 +120,19 @@ __device__ __forceinline__ void copy16(void *dst, const void *src, int bytes) {
     uint4 *d = reinterpret_cast<uint4 *>(dst);
     for (int i = threadIdx.x; i < (bytes >> 4); i += blockDim.x) d[i] = s[i];
 }
+// The same copy with nontemporal HBM accesses, for V streamed once per launch (HBM -> LDS loads,
+// LDS -> HBM stores): the lines are not kept in L2/MALL for a re-read that never comes.
+typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void copy16_nt_in(void *dst, const void *src, int bytes) {
+    const u32x4_nt *s = reinterpret_cast<const u32x4_nt *>(src);
+    u32x4_nt *d = reinterpret_cast<u32x4_nt *>(dst);
+    for (int i = threadIdx.x; i < (bytes >> 4); i += blockDim.x) d[i] = __builtin_nontemporal_load(s + i);
+}
+__device__ __forceinline__ void copy16_nt_out(void *dst, const void *src, int bytes) {
+    const u32x4_nt *s = reinterpret_cast<const u32x4_nt *>(src);
+    u32x4_nt *d = reinterpret_cast<u32x4_nt *>(dst);
+    for (int i = threadIdx.x; i < (bytes >> 4); i += blockDim.x) __builtin_nontemporal_store(s[i], d + i);
+}
 __device__ __forceinline__ void zero16(void *dst, int bytes) {
     uint4 *d = reinterpret_cast<uint4 *>(dst);
     for (int i = threadIdx.x; i < (bytes >> 4); i += blockDim.x) d[i] = make_uint4(0, 0, 0, 0);
