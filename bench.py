@@ -51,6 +51,8 @@ STEP_WORKLOADS = {
     "step_doorkey16x65536": dict(env_id="MiniGrid-DoorKey-16x16-v0", per_gpu=65536),
     "step_fourrooms65536": dict(env_id="MiniGrid-FourRooms-v0", per_gpu=65536),
     "step_lava65536": dict(env_id="MiniGrid-LavaCrossingS11N5-v0", per_gpu=65536),
+    # 2^20 DoorKey-16 envs: ~390 MB of env state + obs per step, past the 256 MB MALL (HBM-bound sizing)
+    "step_doorkey16x1m": dict(env_id="MiniGrid-DoorKey-16x16-v0", per_gpu=1 << 20),
 }
 GEN_WORKLOADS = {
     "gen_lava65536": dict(env_id="MiniGrid-LavaCrossingS11N5-v0", per_gpu=65536),
@@ -178,6 +180,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline sampling")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-hbm", action="store_true", help="skip the HBM-roofline side measurement")
+    ap.add_argument("--no-f64", action="store_true", help="skip the fp64 (parity-mode) side measurement")
     args = ap.parse_args()
 
     import torch
@@ -213,19 +216,140 @@ def main():
         return
 
     import minigrid_dynamicprogramming_amd as mg
-    from minigrid_dynamicprogramming_amd.distributed import solve_sharded
 
     spec = WORKLOADS[args.workload]
     t_gen = time.perf_counter()
     cells, (lo, hi) = make_cells(spec, rank, world)
     log(f"[rank {rank}] {args.workload}: grids [{lo},{hi}) generated in {time.perf_counter() - t_gen:.1f}s")
-    vi = mg.ValueIteration(cells, gamma=args.gamma, tol=args.tol, dtype=args.dtype, method=args.method,
-                           mapping=args.mapping, device=local)
     sharded = spec["sharded"] and world > 1
+    reducer = None
+    if sharded:
+        from minigrid_dynamicprogramming_amd.distributed import Reducer
+
+        reducer = Reducer(timing=True)  # built once; its stream carries the shard's launches and collectives
+
+    m = measure(args, args.dtype, cells, local, dist, red_dev, reducer, sharded)
+    if rank != 0:  # the fp64 side line and the CPU baselines are N = 1 only
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    vi_info = m["info"]
+    A = vi_info["A"]
+    tsize = 4 if args.dtype == "f32" else 8
+    bpu = algorithmic_bytes_per_update(tsize, A)
+    HW = vi_info["W"] * vi_info["H"]
+    launches = m["launches"]
+    avg_launch_s = (m["kern_ms"] / 1000.0) / max(launches, 1)
+    # solves inside the timed launches: the K timed solves plus the priming solve a resident
+    # server's launch also spans
+    solves_in_launches = args.steps + m["primed"]
+    upd_per_solve = float(vi_info["updates_per_sweep"]) * m["sweeps"][-1]
+    alg_bytes_launch = upd_per_solve * solves_in_launches * bpu / max(launches, 1)
+    achieved = alg_bytes_launch / avg_launch_s / 1e9 if launches else 0.0
+    comp_launch = compulsory_bytes_per_solve(vi_info, tsize, args.method, m["sweeps"][-1]) * solves_in_launches / max(launches, 1)
+    key = f"{args.workload}/{args.method}/{args.mapping}/{args.dtype}"
+    traffic = load_traffic(key, solves_in_launches / max(launches, 1))
+    roofline = {
+        "bound": "hbm", "kernel": vi_info["kernel"],
+        "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+        "traffic": traffic, "launches": launches, "avg_launch_us": avg_launch_s * 1e6,
+        "alg_bytes_per_launch": alg_bytes_launch, "alg_bytes_per_update": bpu,
+        "solves_per_launch": solves_in_launches / max(launches, 1),
+        "compulsory_bytes_per_launch": comp_launch,
+        "compulsory_frac": comp_launch / max(avg_launch_s, 1e-30) / 1e9 / HBM_PEAK_GBS,
+        "note": ("achieved = SURVEY 8(d) algorithmic bytes (sizeof V + 1 + sizeof V / A per (s,a) update) per launch "
+                 "/ the launch's HIP-event duration; compulsory = the bytes this kernel must move per launch "
+                 "(fused/served: cells in + V and pi out once per solve; sweep: 2*S*sizeof V + W*H per "
+                 "grid-sweep); traffic = PMC HBM bytes per launch (profiles/pmc_traffic.json)"),
+    }
+    if args.workload == "empty16":
+        roofline["regime"] = ("single 4 KiB V grid on one resident workgroup: latency bound (barrier + LDS round trip "
+                              "per sweep, host hand-off per solve); HBM is not the limit here (SURVEY 8(d) "
+                              "caveats); see roofline_hbm for the kernels at the HBM-sized config R")
+    if vi_info["persistent"]:
+        roofline["launch_note"] = ("lone grid: one resident vi_serve_kernel launch serves the priming solve and every "
+                                   "timed solve (host posts a request word, the workgroup solves and publishes), so "
+                                   "its duration spans the timed region")
+    if roofline["frac"] > 1.0:  # LDS-served gathers: the algorithmic figure is not an HBM rate
+        roofline["alg_equiv_gbs"] = achieved
+        meas = traffic if traffic else comp_launch
+        roofline["achieved"] = meas / avg_launch_s / 1e9
+        roofline["frac"] = roofline["achieved"] / HBM_PEAK_GBS
+        roofline["achieved_basis"] = "pmc traffic" if traffic else "compulsory bytes"
+    out = {
+        "metric": METRIC,
+        "value": m["upd_total"] / m["elapsed_max"],
+        "unit": "updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": m["elapsed_max"] * 1000.0 / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong" if spec["sharded"] else "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": f"synthetic: {spec['env_id']} grids from the reference-exact generator "
+                f"({'seed 0 replicated' if spec['replicate'] else 'seeds ' + str(lo) + '..'})",
+        "config": {
+            "workload": args.workload, "env_id": spec["env_id"], "grids_per_gpu": hi - lo,
+            "global_grids": (hi - lo) * world if not spec["sharded"] else spec["global_grids"],
+            "states_per_grid": vi_info["S"], "actions": A, "gamma": args.gamma, "tol": args.tol,
+            "method": args.method, "mapping": args.mapping,
+            "parallelism": (f"shard{world} + RCCL dV all-reduce" if sharded else
+                            ("replicas only" if spec["replicate"] else f"independent batches x{world}")),
+        },
+        "sweeps": int(m["sweeps"][-1]),
+        "roofline": roofline,
+    }
+    if m.get("collectives"):
+        out["collectives"] = m["collectives"]
+    if args.dtype == "f32" and world == 1 and not args.no_f64:
+        m64 = measure(args, "f64", cells, local, dist, red_dev, reducer, sharded)
+        out["f64"] = {"value": m64["upd_total"] / m64["elapsed_max"], "unit": "updates/s",
+                      "ms_per_step": m64["elapsed_max"] * 1000.0 / args.steps, "sweeps": int(m64["sweeps"][-1]),
+                      "kernel": m64["info"]["kernel"],
+                      "note": "same workload and steps in fp64 (parity mode: bit-exact with the fp64 oracle)"}
+
+    if world == 1 and not args.no_hbm and args.workload == "empty16":
+        out["roofline_hbm"] = hbm_side_measurement(args)
+    if world == 1 and not args.no_cpu:
+        out["host"] = host_info()
+        out["cpu_baseline"] = cpu_baseline(cells, vi_info["model"], args.gamma, args.tol, args.dtype, args.cpu_budget)
+        out["cpu_baseline_all_cores"] = cpu_baseline(
+            cells, vi_info["model"], args.gamma, args.tol, args.dtype, max(2.0, args.cpu_budget / 4),
+            nthreads=out["host"]["cores_used"])
+        out["cpu_baseline_numpy"] = numpy_baseline(cells, vi_info["model"], args.gamma, args.tol, args.dtype,
+                                                   max(2.0, args.cpu_budget / 4))
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def compulsory_bytes_per_solve(info, tsize, method, sweeps):
+    """Bytes a solve must move between HBM and the CUs.  fused / served: the grid's cells in, V and
+    pi out, once per solve (V stays in LDS across sweeps); sweep: SURVEY 8(d)'s 2*S*sizeof V + W*H
+    per grid-sweep (V read and written every sweep) plus the pi pass."""
+    B, S, HW = info["B"], info["S"], info["W"] * info["H"]
+    if method == "fused":
+        return B * (HW + S * tsize + S)
+    return B * (compulsory_bytes_per_sweep(S, HW, tsize) * sweeps + S * tsize + HW + S)
+
+
+def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded):
+    """W warmup solves, then K timed solves (barrier + synchronize on both sides, max over ranks)."""
+    import torch
+
+    import minigrid_dynamicprogramming_amd as mg
+    from minigrid_dynamicprogramming_amd.distributed import solve_sharded
+
+    vi = mg.ValueIteration(cells, gamma=args.gamma, tol=args.tol, dtype=dtype, method=args.method,
+                           mapping=args.mapping, device=local)
 
     def one_solve():
         if sharded:
-            return solve_sharded(vi)["sweeps"]
+            return solve_sharded(vi, reducer=reducer)["sweeps"]
         return vi.solve()
 
     def barrier():
@@ -234,9 +358,20 @@ def main():
 
     for _ in range(args.warmup):
         one_solve()
+    # Enabling launch timing drains the stream (and asks a resident lone-grid server to leave), so
+    # the timed launches start after it; a persistent handle then gets one untimed priming solve,
+    # which relaunches the server (its launch is now timed), so the timed region holds no relaunch
+    # and its length does not depend on --steps.
     vi.enable_timing(True)
+    if reducer is not None:
+        reducer.collect()
+        reducer.reset_counters()
     barrier()
     torch.cuda.synchronize()
+    primed = 0
+    if vi.persistent:
+        one_solve()
+        primed = 1
     t0 = time.perf_counter()
     sweeps = []
     for _ in range(args.steps):
@@ -249,92 +384,76 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms, launches = vi.kernel_time()
     vi.enable_timing(False)
-
-    A = 7 if vi.model == "xyd" else 5
-    upd_rank = float(vi.updates_per_sweep) * float(sum(sweeps))
+    info = {"A": 7 if vi.model == "xyd" else 5, "W": vi.W, "H": vi.H, "S": vi.S, "B": vi.B, "model": vi.model,
+            "updates_per_sweep": vi.updates_per_sweep, "kernel": vi.kernel_name, "persistent": vi.persistent}
+    vi.close()
+    upd_rank = float(info["updates_per_sweep"]) * float(sum(sweeps))
+    collectives = None
+    if reducer is not None:
+        dev_ms = reducer.collect()
+        collectives = {"allreduces_per_solve": reducer.calls / args.steps,
+                       "host_reads_per_solve": reducer.host_reads / args.steps,
+                       "allreduce_us_per_solve_rank0": dev_ms * 1000.0 / args.steps,
+                       "protocol_host_us_per_solve_rank0": reducer.wall_s * 1e6 / args.steps,
+                       "note": "device time of the RCCL all-reduces (events on the protocol stream, includes "
+                               "waiting for the slowest rank) and host time of the one read per solve"}
     if dist is not None:
-        t = torch.tensor([elapsed, upd_rank], dtype=torch.float64, device=red_dev)
-        tmax = t[0:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        usum = t[1:2].clone()
-        dist.all_reduce(usum, op=dist.ReduceOp.SUM)
-        elapsed_max, upd_total = float(tmax.item()), float(usum.item())
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
+        u = torch.tensor([upd_rank], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(u, op=dist.ReduceOp.SUM)
+        elapsed_max, upd_total = float(t.item()), float(u.item())
     else:
         elapsed_max, upd_total = elapsed, upd_rank
+    return {"elapsed_max": elapsed_max, "upd_total": upd_total, "sweeps": sweeps, "kern_ms": kern_ms,
+            "launches": launches, "primed": primed, "info": info, "collectives": collectives}
 
-    if rank != 0:
-        vi.close()
-        if dist is not None:
-            dist.barrier()
-            dist.destroy_process_group()
-        return
 
-    tsize = 4 if args.dtype == "f32" else 8
-    bpu = algorithmic_bytes_per_update(tsize, A)
-    HW = vi.W * vi.H
-    bytes_alg = upd_rank * bpu
-    avg_launch_s = (kern_ms / 1000.0) / max(launches, 1)
-    achieved = bytes_alg / max(launches, 1) / avg_launch_s / 1e9 if launches else 0.0
-    comp_bytes = compulsory_bytes_per_sweep(vi.S, HW, tsize) * vi.B * (sum(sweeps))
-    persistent = vi.persistent
-    kernel_name = vi.kernel_name
-    key = f"{args.workload}/{args.method}/{args.mapping}/{args.dtype}"
-    roofline = {
-        "bound": "hbm", "kernel": kernel_name,
-        "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-        "traffic": load_traffic(key, args.steps / max(launches, 1)),
-        "launches": launches, "avg_launch_us": avg_launch_s * 1e6,
-        "alg_bytes_per_launch": bytes_alg / max(launches, 1),
-        "alg_bytes_per_update": bpu,
-        "compulsory_gbs": comp_bytes / max(launches, 1) / avg_launch_s / 1e9 if launches else 0.0,
-        "note": ("algorithmic bytes per SURVEY 8(d): (sizeof V + 1 + sizeof V / A) per (s,a) update; "
-                 "compulsory = 2*S*sizeof V + W*H per grid-sweep"),
-    }
-    if args.workload == "empty16":
-        roofline["regime"] = ("single 8 KiB grid on one workgroup: latency/LDS bound, HBM-roofline fraction "
-                              "is not meaningful here (SURVEY 8(d) caveats); see roofline_hbm")
-    if persistent:
-        roofline["launch_note"] = ("lone grid: one resident vi_serve_kernel launch serves every timed solve "
-                                   "(host posts a request word, the workgroup solves and publishes), so the "
-                                   "launch spans the timed region including host turnaround")
-    out = {
-        "metric": METRIC,
-        "value": upd_total / elapsed_max,
-        "unit": "updates/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": elapsed_max * 1000.0 / args.steps,
-        "higher_is_better": True,
-        "scaling": "strong" if spec["sharded"] else "weak",
-        "vs_baseline": None,
-        "dtype": args.dtype,
-        "data": f"synthetic: {spec['env_id']} grids from the reference-exact host generator "
-                f"({'seed 0 replicated' if spec['replicate'] else 'seeds ' + str(lo) + '..'})",
-        "config": {
-            "workload": args.workload, "env_id": spec["env_id"], "grids_per_gpu": hi - lo,
-            "global_grids": (hi - lo) * world if not spec["sharded"] else spec["global_grids"],
-            "states_per_grid": vi.S, "actions": A, "gamma": args.gamma, "tol": args.tol,
-            "method": args.method, "mapping": args.mapping,
-            "parallelism": (f"shard{world} + RCCL dV all-reduce" if sharded else
-                            ("replicas only" if spec["replicate"] else f"independent batches x{world}")),
-        },
-        "sweeps": int(sweeps[-1]),
-        "roofline": roofline,
-    }
-    vi.close()
+def host_info():
+    """The CPU the baseline runs on: nproc / affinity (the whole machine on the GPU box) and the
+    cores this process is allotted (OMP_NUM_THREADS: the pool's per-GPU CPU share), lscpu model."""
+    import subprocess
 
-    if world == 1 and not args.no_hbm and args.workload == "empty16":
-        out["roofline_hbm"] = hbm_side_measurement(args)
-    if world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(cells, vi.model, args.gamma, args.tol, args.dtype, args.cpu_budget)
-        out["cpu_baseline_all_cores"] = cpu_baseline(
-            cells, vi.model, args.gamma, args.tol, args.dtype, max(2.0, args.cpu_budget / 4),
-            nthreads=min(16, os.cpu_count() or 1))
-    print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    aff = len(os.sched_getaffinity(0))
+    cores = aff
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        cores = max(1, min(aff, int(os.environ["OMP_NUM_THREADS"])))
+    model = ""
+    try:
+        for line in subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout.splitlines():
+            if line.startswith("Model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    nproc = os.cpu_count()
+    try:
+        nproc = int(subprocess.run(["nproc"], capture_output=True, text=True, timeout=10).stdout.strip())
+    except Exception:
+        pass
+    return {"nproc": nproc, "affinity_cpus": aff, "cores_used": cores, "cpu_model": model,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def numpy_baseline(cells, model, gamma, tol, dtype, budget_s):
+    """oracle/numpy_vi.py (numpy Jacobi restatement, single thread) on the same sample."""
+    from oracle.numpy_vi import NumpyVI
+
+    sample = cells[: min(len(cells), 32)]
+    n = NumpyVI(0 if model == "xyd" else 1, sample, gamma, tol, dtype)
+    solves, upd, k = 0, 0, 0
+    t0 = time.perf_counter()
+    while True:
+        r = n.solve()
+        k = r["sweeps"]
+        upd += n.B * n.S * n.A * k
+        solves += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    el = time.perf_counter() - t0
+    return {"value": upd / el, "unit": "updates/s", "cores": 1, "kind": "port",
+            "sample": f"{solves} full solves of {n.B} grid(s) ({k} sweeps each, {dtype}), oracle/numpy_vi.py "
+                      f"(vectorised numpy Jacobi over the oracle's transition tables), {el:.1f} s"}
 
 
 def _max_over_ranks(dist, red_dev, elapsed, units):
@@ -547,14 +666,31 @@ def gen_cpu_baseline(env, budget_s):
             "sample": f"{n} host reset(seed) generations (numpy PCG64, envs.py), {el:.1f} s"}
 
 
+VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9  # MI355X_MICROARCH.md: 4 SIMD-32 per CU, one wave64 VALU op per 2 cycles
+
+
+def load_sq(key):
+    """Per-launch SQ counters of a kernel from the committed PMC passes (profiles/sq_counters.json,
+    tools/pmc_sq.sh): VALU / LDS instructions, wave cycles, busy cycles."""
+    p = os.path.join(ROOT, "profiles", "sq_counters.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f).get(key)
+
+
 def hbm_side_measurement(args, n_solves=3):
-    """Per-sweep HBM kernel on SURVEY 8(d) config R (Empty-16x16 x 65536, 537 MB of V > MALL)."""
+    """Both batched kernels on SURVEY 8(d) config R (Empty-16x16 x 65536: 537 MB of fp32 V > the
+    256 MB MALL).  `frac` is an HBM fraction of MEASURED bytes (PMC traffic per launch, else the
+    kernel's compulsory bytes per launch) -- never the algorithmic figure, which counts every
+    LDS-served neighbour gather as an HBM read and is reported apart as alg_equiv_gbs."""
     import torch
 
     import minigrid_dynamicprogramming_amd as mg
 
     cells, _ = make_cells(WORKLOADS["empty16x65536"], 0, 1)
     res = {}
+    tsize = 4 if args.dtype == "f32" else 8
     for method in ("sweep", "fused"):
         vi = mg.ValueIteration(cells, gamma=args.gamma, tol=args.tol, dtype=args.dtype, method=method,
                                mapping=args.mapping)
@@ -565,17 +701,34 @@ def hbm_side_measurement(args, n_solves=3):
         ks = [vi.solve() for _ in range(n_solves)]
         el = time.perf_counter() - t0
         ms, n = vi.kernel_time()
-        tsize = 4 if args.dtype == "f32" else 8
         upd = vi.updates_per_sweep * sum(ks)
         bpu = algorithmic_bytes_per_update(tsize, 7)
         avg = ms / 1000.0 / max(n, 1)
-        ach = upd * bpu / max(n, 1) / avg / 1e9
-        comp = compulsory_bytes_per_sweep(vi.S, vi.W * vi.H, tsize) * vi.B * sum(ks) / max(n, 1) / avg / 1e9
-        res[method] = {"kernel": vi.kernel_name,
-                       "updates_per_s": upd / el, "sweeps": ks[-1], "launches": n, "avg_launch_us": avg * 1e6,
-                       "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                       "compulsory_gbs": comp, "compulsory_frac": comp / HBM_PEAK_GBS,
-                       "traffic": load_traffic(f"empty16x65536/{method}/{args.mapping}/{args.dtype}", n_solves / max(n, 1))}
+        info = {"B": vi.B, "S": vi.S, "W": vi.W, "H": vi.H}
+        if method == "sweep":  # one timed launch per sweep (the pi pass is not timed)
+            comp = compulsory_bytes_per_sweep(vi.S, vi.W * vi.H, tsize) * vi.B
+        else:  # one launch per solve; V lives in LDS between sweeps
+            comp = compulsory_bytes_per_solve(info, tsize, "fused", ks[-1])
+        key = f"empty16x65536/{method}/{args.mapping}/{args.dtype}"
+        traffic = load_traffic(key, n_solves / max(n, 1))
+        meas = traffic if traffic else comp
+        r = {"kernel": vi.kernel_name, "updates_per_s": upd / el, "sweeps": ks[-1], "launches": n,
+             "avg_launch_us": avg * 1e6, "bound": "hbm" if method == "sweep" else "valu/lds (not hbm)",
+             "achieved": meas / avg / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": meas / avg / 1e9 / HBM_PEAK_GBS, "achieved_basis": "pmc traffic" if traffic else "compulsory bytes",
+             "traffic": traffic, "compulsory_bytes_per_launch": comp,
+             "compulsory_frac": comp / avg / 1e9 / HBM_PEAK_GBS,
+             "alg_equiv_gbs": upd * bpu / max(n, 1) / avg / 1e9,
+             "alg_note": "SURVEY 8(d) algorithmic bytes / launch time: every neighbour gather counted as an HBM "
+                         "read although LDS serves it; an equivalent rate, not an HBM fraction"}
+        sq = load_sq(f"{key}/{vi.kernel_name}")
+        if sq and sq.get("valu_insts_per_launch"):
+            lane_ops = sq["valu_insts_per_launch"] * 64.0 / avg
+            r["valu"] = {"achieved": lane_ops, "peak": VALU_PEAK_LANE_OPS, "unit": "lane-ops/s",
+                         "frac": lane_ops / VALU_PEAK_LANE_OPS, "source": sq.get("source")}
+            if sq.get("lds_insts_per_launch"):
+                r["lds_insts_per_launch"] = sq["lds_insts_per_launch"]
+        res[method] = r
         vi.close()
     res["workload"] = "empty16x65536"
     return res

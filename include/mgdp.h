@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MGDP_ABI_VERSION 3
+#define MGDP_ABI_VERSION 4
 
 enum {
     MGDP_OK = 0,
@@ -143,6 +143,20 @@ int mgdp_vi_run_to(mgdp_vi *vi, int32_t k_target, double *dv_out);
 int mgdp_vi_sweep(mgdp_vi *vi, double *dv_out);
 /* Extract pi from the last sweep and publish sweeps/converged for mgdp_vi_get_*. */
 int mgdp_vi_finish(mgdp_vi *vi, int32_t sweeps);
+
+/* The same protocol with no host round trip between its steps (fused method, no horizon / lava
+ * options; distributed.py drives it over RCCL).  d_pub / d_k are caller-owned DEVICE int64 buffers
+ * ordered on the handle's stream (mgdp_vi_set_stream):
+ *   mgdp_vi_reset -> mgdp_vi_run_local_dev(p) -> all-reduce(MAX) p[0] on the stream
+ *   -> mgdp_vi_run_to_dev(p, p + 4) -> all-reduce(MAX) p[5] -> ONE host read of p[0] (K), p[5]
+ *   -> mgdp_vi_set_result(K, dv) -> (rare fallback: mgdp_vi_sweep + host all-reduces) -> finish.
+ * A launch writes d_pub[0..3] = {max sweeps over the shard's grids, max|dV| as IEEE-754 bits
+ * (non-negative doubles order like their bits), min sweeps, launch epoch}; both calls only enqueue. */
+int mgdp_vi_run_local_dev(mgdp_vi *vi, int64_t *d_pub);
+/* Every grid to exactly the sweep *d_k (read on the device when the launch starts). */
+int mgdp_vi_run_to_dev(mgdp_vi *vi, const int64_t *d_k, int64_t *d_pub);
+/* Hand the all-reduced K and dV back to the handle (every grid is at sweep K). */
+int mgdp_vi_set_result(mgdp_vi *vi, int32_t k, double dv);
 
 /* Results (host).  V: B*S of float or double per dtype; pi: B*S int8 (-1 = absorbing state). */
 int mgdp_vi_get_values(mgdp_vi *vi, void *V);

@@ -80,6 +80,9 @@ SIGNATURES = {
     "mgdp_vi_run_to": (ctypes.c_int, [_P, _I32, _DP]),
     "mgdp_vi_sweep": (ctypes.c_int, [_P, _DP]),
     "mgdp_vi_finish": (ctypes.c_int, [_P, _I32]),
+    "mgdp_vi_run_local_dev": (ctypes.c_int, [_P, _P]),
+    "mgdp_vi_run_to_dev": (ctypes.c_int, [_P, _P, _P]),
+    "mgdp_vi_set_result": (ctypes.c_int, [_P, _I32, ctypes.c_double]),
     "mgdp_vi_get_values": (ctypes.c_int, [_P, _P]),
     "mgdp_vi_get_policy": (ctypes.c_int, [_P, _P]),
     "mgdp_vi_get_dv_trace": (ctypes.c_int, [_P, _P, _I32]),
@@ -143,7 +146,7 @@ def load():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.mgdp_abi_version() != 3:
+    if L.mgdp_abi_version() != 4:
         raise MgdpError("libmgdp ABI version mismatch")
     _lib = L
     return L

@@ -245,29 +245,35 @@ struct FusedK { static constexpr auto fn = vi_fused_kernel<T, MODEL, SLIP, MAP, 
 template <typename T, int MODEL, bool SLIP, int MAP, int WP>
 struct ServeK { static constexpr auto fn = vi_serve_kernel<T, MODEL, SLIP, MAP, WP>; };
 
+// pub: where the launch's {kmax, dV bits, kmin, epoch} go (default: the host-mapped words the host
+// polls; the multi-GPU device protocol passes a device buffer it all-reduces); k_dev: the target
+// sweep read from device memory instead of k_target (mgdp_vi_run_to_dev).
 template <typename T, int MODEL, bool SLIP, int MAP>
-int launch_fused_t(mgdp_vi *vi, int k_target) {
+int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr, const long long *k_dev = nullptr) {
     if (vi->opts) return launch_opts<T>(vi, k_target);
+    if (!pub) pub = vi->d_hout;
     const Geo g = make_geo(vi);
     const Smem L = smem_layout(vi->Ss, vi->HWp, sizeof(T), vi->nbuf);
     auto kern = pick_wave<FusedK, T, MODEL, SLIP, MAP>(vi);
-    if constexpr (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL)
+    if constexpr (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL) {
         if (vi->cpt == 2) kern = FusedK<T, MODEL, SLIP, MAP, -2>::fn;
         else if (vi->cpt == 4) kern = FusedK<T, MODEL, SLIP, MAP, -4>::fn;
-    if constexpr (MODEL == MGDP_MODEL_DOORKEY && MAP == MGDP_MAP_CELL && !SLIP)
+    }
+    if constexpr (MODEL == MGDP_MODEL_DOORKEY && MAP == MGDP_MAP_CELL && !SLIP) {
         if (vi->dk1t) kern = FusedK<T, MODEL, SLIP, MAP, kWpDk1t>::fn;
+    }
     if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
     TimedPair tp;
     if (int rc = timed_begin(vi, -1, &tp)) return rc;
     hipExtLaunchKernelGGL(kern, dim3(vi->d.B), dim3(vi->fused_block), L.total(), vi->stream, tp.a, tp.b, 0, g,
                        make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv,
-                       vi->d_dvenv, vi->d_red, vi->d_ticket, vi->d_hout, k_target, vi->fresh,
-                       vi->d.B <= kInKernelReduceMaxB ? 1 : 0, ++vi->epoch);
+                       vi->d_dvenv, vi->d_red, vi->d_ticket, pub, k_target, vi->fresh,
+                       vi->d.B <= kInKernelReduceMaxB ? 1 : 0, ++vi->epoch, k_dev);
     MGDP_HIP(hipGetLastError());
     vi->fresh = 0;
     if (vi->d.B > kInKernelReduceMaxB) {
         hipLaunchKernelGGL(vi_reduce_kernel, dim3(1), dim3(1024), 0, vi->stream, vi->d_kenv, vi->d_dvenv, vi->d.B,
-                           vi->d_hout, vi->epoch);
+                           pub, vi->epoch);
         MGDP_HIP(hipGetLastError());
     }
     return 0;
@@ -361,7 +367,9 @@ int dispatch(mgdp_vi *vi, Args... args) {
 
 template <typename T, int MODEL, bool SLIP, int MAP>
 struct FusedF {
-    static int run(mgdp_vi *vi, int k_target) { return launch_fused_t<T, MODEL, SLIP, MAP>(vi, k_target); }
+    static int run(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr, const long long *k_dev = nullptr) {
+        return launch_fused_t<T, MODEL, SLIP, MAP>(vi, k_target, pub, k_dev);
+    }
 };
 template <typename T, int MODEL, bool SLIP, int MAP>
 struct ServeF {
@@ -856,6 +864,40 @@ int mgdp_vi_run_to(mgdp_vi *vi, int32_t k_target, double *dv_out) {
         return 0;
     }
     return sweep_run(vi, k_target, true, dv_out);
+}
+
+// Multi-GPU device protocol (distributed.py): the two launches of a sharded solve are enqueued on
+// the handle's stream with their results in a caller-owned device buffer, so the all-reduces
+// between them (RCCL, ordered on the same stream) need no host round trip; the host reads K and dV
+// once at the end and hands them back with mgdp_vi_set_result.
+int mgdp_vi_run_local_dev(mgdp_vi *vi, int64_t *d_pub) {
+    MGDP_CHECK(vi && d_pub, MGDP_E_INVALID, "null argument");
+    MGDP_CHECK(vi->cells_loaded, MGDP_E_INVALID, "no cells loaded");
+    MGDP_CHECK(vi->d.method == MGDP_METHOD_FUSED && !vi->opts, MGDP_E_UNSUPPORTED,
+               "the device protocol runs the fused method without horizon / lava options");
+    DeviceGuard guard(vi->d.device);
+    if (int rc = server_stop(vi)) return rc;
+    vi->k_done_valid = false;
+    return dispatch<FusedF>(vi, -1, reinterpret_cast<unsigned long long *>(d_pub), (const long long *)nullptr);
+}
+
+int mgdp_vi_run_to_dev(mgdp_vi *vi, const int64_t *d_k, int64_t *d_pub) {
+    MGDP_CHECK(vi && d_k && d_pub, MGDP_E_INVALID, "null argument");
+    MGDP_CHECK(vi->d.method == MGDP_METHOD_FUSED && !vi->opts, MGDP_E_UNSUPPORTED,
+               "the device protocol runs the fused method without horizon / lava options");
+    MGDP_CHECK(!vi->fresh, MGDP_E_INVALID, "mgdp_vi_run_to_dev before mgdp_vi_run_local_dev");
+    DeviceGuard guard(vi->d.device);
+    vi->k_done_valid = false;
+    return dispatch<FusedF>(vi, 0, reinterpret_cast<unsigned long long *>(d_pub), reinterpret_cast<const long long *>(d_k));
+}
+
+int mgdp_vi_set_result(mgdp_vi *vi, int32_t k, double dv) {
+    MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
+    MGDP_CHECK(k >= 0 && k <= vi->d.max_sweeps, MGDP_E_INVALID, "sweep %d out of range", k);
+    vi->k_min = vi->k_max = vi->k_done = k;
+    vi->dv_red = dv;
+    vi->k_done_valid = true;
+    return 0;
 }
 
 int mgdp_vi_sweep(mgdp_vi *vi, double *dv_out) {

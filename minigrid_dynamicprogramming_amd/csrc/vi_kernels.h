@@ -146,10 +146,13 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
                 unsigned long long *__restrict__ host_out, int k_target, int fresh, int in_kernel_reduce,
-                unsigned int epoch) {
+                unsigned int epoch, const long long *__restrict__ k_target_dev) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
     T *slots = reinterpret_cast<T *>(smem + L.slots_off());
+    // multi-GPU protocol (mgdp_vi_run_to_dev): the target sweep is the all-reduced K in device
+    // memory, written by a collective ordered before this launch on the stream
+    if (k_target_dev) k_target = (int)*k_target_dev;
     int k;
     double dvl;
     const bool lone = in_kernel_reduce && gridDim.x == 1;

@@ -259,6 +259,34 @@ class ValueIteration:
         _lib.check(self.L.mgdp_vi_sweep(self.h, ctypes.byref(dv)), "mgdp_vi_sweep")
         return dv.value
 
+    # -- the same protocol with device-resident K / dV (distributed.py over RCCL): enqueue only
+    @property
+    def protocol_device(self):
+        """The torch device whose int64 buffers the *_dev steps read and write (None when this handle
+        runs the host protocol only: sweep method, horizon or NoDeath options)."""
+        if self.desc.method != _lib.METHOD_FUSED or self.horizon > 0 or self.desc.lava_mode != 0:
+            return None
+        import torch
+
+        return torch.device("cuda", self.desc.device)
+
+    def bind_stream(self, stream_ptr: int):
+        """Launch on this hipStream_t from now on (no-op when it already does)."""
+        if getattr(self, "_bound_stream", None) != int(stream_ptr):
+            _lib.check(self.L.mgdp_vi_set_stream(self.h, ctypes.c_void_p(int(stream_ptr))), "mgdp_vi_set_stream")
+            self._bound_stream = int(stream_ptr)
+
+    def run_local_dev(self, pub):
+        """pub: int64 CUDA tensor (or pointer) of 4 words <- {k max, dV bits, k min, epoch}."""
+        _lib.check(self.L.mgdp_vi_run_local_dev(self.h, _lib.ptr(pub)), "mgdp_vi_run_local_dev")
+
+    def run_to_dev(self, k, pub):
+        """Every grid to exactly the sweep held by the int64 device word k; results into pub."""
+        _lib.check(self.L.mgdp_vi_run_to_dev(self.h, _lib.ptr(k), _lib.ptr(pub)), "mgdp_vi_run_to_dev")
+
+    def set_result(self, k: int, dv: float):
+        _lib.check(self.L.mgdp_vi_set_result(self.h, int(k), float(dv)), "mgdp_vi_set_result")
+
     def finish(self, sweeps: int, dv: float):
         _lib.check(self.L.mgdp_vi_finish(self.h, int(sweeps)), "mgdp_vi_finish")
         self.sweeps, self.dv = int(sweeps), float(dv)

@@ -220,6 +220,7 @@ int orc_build_table(int model, int W, int H, const uint8_t *cells, int32_t *nxt,
         uint8_t *dn = (uint8_t *)malloc(BS * A);                                                  \
         T *Vn = (T *)malloc(sizeof(T) * BS);                                                      \
         if (!nxt || !rew || !dn || !Vn) { free(nxt); free(rew); free(dn); free(Vn); return -2; }  \
+        _Pragma("omp parallel for num_threads(nthreads) schedule(dynamic, 64)")                    \
         for (int b = 0; b < B; ++b)                                                               \
             orc_build_table(model, W, H, cells + (long long)b * W * H, nxt + (long long)b * S * A, \
                             rew + (long long)b * S * A, dn + (long long)b * S * A);               \

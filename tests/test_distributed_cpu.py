@@ -10,7 +10,8 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from minigrid_dynamicprogramming_amd.distributed import shard_range, solve_sharded
+from minigrid_dynamicprogramming_amd.distributed import (EmptyShard, Reducer, bits_to_double, double_to_bits,
+                                                         shard_range, solve_sharded)
 from oracle import oracle
 from tests.golden_util import cells_from_enc, load
 
@@ -46,6 +47,33 @@ class OracleShard:
         self.V, self.pi, self.sweeps = r["V"], r["pi"], k
 
 
+class DevOracleShard(OracleShard):
+    """The device-protocol steps of the shard (run_local_dev / run_to_dev / set_result) on CPU int64
+    tensors: the words a GPU launch would publish, all-reduced by gloo in place."""
+
+    @property
+    def protocol_device(self):
+        import torch
+
+        return torch.device("cpu")
+
+    def run_local_dev(self, pub):
+        pub[0] = self.run_local()
+        pub[1] = 0
+        pub[2] = 0
+        pub[3] = 1
+
+    def run_to_dev(self, k, pub):
+        kk = int(k[0])
+        pub[0] = kk
+        pub[1] = double_to_bits(self.run_to(kk))
+        pub[2] = kk
+        pub[3] = 2
+
+    def set_result(self, k, dv):
+        self.k = k
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -54,25 +82,32 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, cells, slip, out):
+def _worker(rank, world, port, cells, slip, out, device_proto=False, solves=1):
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     lo, hi = shard_range(len(cells), rank, world)
-    shard = OracleShard(cells[lo:hi], slip=slip)
-    res = solve_sharded(shard)
-    out[rank] = (res["sweeps"], res["allreduces"], shard.V, shard.pi, lo, hi)
+    red = Reducer()  # built once, reused by every solve
+    if hi == lo:
+        shard = EmptyShard()
+    else:
+        shard = (DevOracleShard if device_proto else OracleShard)(cells[lo:hi], slip=slip)
+    for _ in range(solves):
+        res = solve_sharded(shard, reducer=red)
+    V = getattr(shard, "V", None)
+    pi = getattr(shard, "pi", None)
+    out[rank] = (res["sweeps"], res["allreduces"], V, pi, lo, hi, res["host_reads"], red.calls)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def run_world(cells, world, slip=None):
+def run_world(cells, world, slip=None, device_proto=False, solves=1):
     port = _free_port()
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, port, cells, slip, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, port, cells, slip, out, device_proto, solves), nprocs=world, join=True)
     return dict(out)
 
 
@@ -91,16 +126,59 @@ def test_two_rank_gloo_matches_global_loop(slip):
     cells = np.stack([cells_from_enc(e) for e in g["enc"][:12]])
     ref = oracle.value_iteration(0, cells, slip_p=slip)
     out = run_world(cells, 2, slip)
-    for rank, (k, nred, V, pi, lo, hi) in out.items():
+    for rank, (k, nred, V, pi, lo, hi, reads, _) in out.items():
         assert k == ref["sweeps"]
         assert nred == 2  # one all-reduce for K, one for dV: the contraction holds in fp64
+        assert reads == 2  # host protocol: each all-reduce is read back
         np.testing.assert_array_equal(V, ref["V"][lo:hi])
         np.testing.assert_array_equal(pi, ref["pi"][lo:hi])
 
 
+@pytest.mark.parametrize("world,n", [(2, 12), (4, 13), (8, 13), (8, 5)])
+def test_device_protocol_uneven_shards_one_host_read(world, n):
+    """The device protocol (K / dV stay in int64 tensors, all-reduced in place) over uneven shards,
+    including ranks with no grids (8 ranks, 5 grids): equal to one global loop, two all-reduces and
+    ONE host read per solve, and the reducer reused across solves."""
+    g = load("grids_fourrooms.npz")
+    cells = np.stack([cells_from_enc(e) for e in g["enc"][:n]])
+    ref = oracle.value_iteration(0, cells)
+    out = run_world(cells, world, device_proto=True, solves=2)
+    assert len(out) == world
+    for rank, (k, nred, V, pi, lo, hi, reads, total_calls) in out.items():
+        assert k == ref["sweeps"], (rank, k)
+        assert nred == 2 and reads == 1
+        assert total_calls == 4  # two solves on one reducer
+        if hi > lo:
+            np.testing.assert_array_equal(V, ref["V"][lo:hi])
+            np.testing.assert_array_equal(pi, ref["pi"][lo:hi])
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_host_protocol_uneven_shards(world):
+    g = load("grids_lava11n5.npz")
+    cells = np.stack([cells_from_enc(e) for e in g["enc"][:11]])
+    ref = oracle.value_iteration(0, cells, slip_p=0.9)
+    out = run_world(cells, world, slip=0.9)
+    for rank, (k, nred, V, pi, lo, hi, reads, _) in out.items():
+        assert k == ref["sweeps"]
+        np.testing.assert_array_equal(V, ref["V"][lo:hi])
+        np.testing.assert_array_equal(pi, ref["pi"][lo:hi])
+
+
+def test_bits_round_trip_and_order():
+    xs = [0.0, 5e-324, 1e-12, 9.99e-7, 1e-6, 0.5, 1.0]
+    bits = [double_to_bits(x) for x in xs]
+    assert bits == sorted(bits)  # non-negative doubles order like their bits: MAX over bits is MAX
+    assert [bits_to_double(b) for b in bits] == xs
+
+
 class _FakeReducer:
     def __init__(self):
+        import torch
+
         self.calls = 0
+        self.host_reads = 0
+        self.device = torch.device("cpu")
 
     def max(self, x):
         self.calls += 1
@@ -133,3 +211,44 @@ def test_fallback_loop_finds_global_stopping_sweep():
     s = _NonMonotoneShard()
     res = solve_sharded(s, reducer=_FakeReducer())
     assert res["sweeps"] == 5 and res["converged"] and s.final[0] == 5
+
+
+class _FakeDeviceReducer(_FakeReducer):
+    """One rank's reducer on the device path: MAX over one rank is the identity."""
+
+    def __init__(self):
+        import torch
+
+        super().__init__()
+        self.torch = torch
+        self.stream = None
+        self.proto = torch.zeros(8, dtype=torch.int64)
+        self.wall_s = 0.0
+
+    def max(self, x):
+        self.host_reads += 1
+        return super().max(x)
+
+    def max_(self, t):
+        self.calls += 1
+
+
+class _NonMonotoneDevShard(_NonMonotoneShard):
+    protocol_device = property(lambda self: __import__("torch").device("cpu"))
+
+    def run_local_dev(self, pub):
+        pub[0] = self.run_local()
+
+    def run_to_dev(self, k, pub):
+        pub[1] = double_to_bits(self.run_to(int(k[0])))
+
+    def set_result(self, k, dv):
+        self.k = k
+
+
+def test_device_protocol_fallback_loop():
+    s = _NonMonotoneDevShard()
+    red = _FakeDeviceReducer()
+    res = solve_sharded(s, reducer=red)
+    assert res["sweeps"] == 5 and res["converged"] and s.final[0] == 5
+    assert res["allreduces"] == 4 and res["host_reads"] == 3  # 1 device read + 2 fallback sweeps

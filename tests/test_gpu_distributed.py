@@ -55,3 +55,73 @@ def test_two_ranks_match_single_device(env_id, slip, method):
         assert nred >= 2
         np.testing.assert_array_equal(V, ref.V[lo:hi])
         np.testing.assert_array_equal(pi, ref.pi[lo:hi])
+
+
+_DEVICE_PROTO = r"""
+import os, sys
+import torch  # first: PyTorch-ROCm and libmgdp share libamdhip64.so.7, the first one loaded serves both
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import minigrid_dynamicprogramming_amd as mg
+from minigrid_dynamicprogramming_amd import gen
+from minigrid_dynamicprogramming_amd.distributed import Reducer, bits_to_double, solve_sharded
+
+mode = sys.argv[2]
+env_id, B, dtype = sys.argv[3], int(sys.argv[4]), sys.argv[5]
+cells = gen.generate(env_id, 0, B, enc=False, cells=True, agent=False)["cells"]
+ref = mg.ValueIteration(cells, dtype=dtype)
+k_ref = ref.solve()
+V_ref, pi_ref = ref.values(), ref.policy()
+ref.close()
+vi = mg.ValueIteration(cells, dtype=dtype)
+if mode == "steps":
+    # the C entry points alone, on a torch stream: K and dV stay in device memory between launches
+    s = torch.cuda.Stream()
+    vi.bind_stream(s.cuda_stream)
+    p = torch.zeros(8, dtype=torch.int64, device="cuda")
+    with torch.cuda.stream(s):
+        for rep in range(3):
+            vi.reset()
+            vi.run_local_dev(p[0:4])
+            vi.run_to_dev(p[0:1], p[4:8])
+            h = p.tolist()
+            k, dv = h[0], bits_to_double(h[5])
+            assert k == k_ref and h[4] == k and h[6] == k and dv < 1e-6, (h, k_ref)
+            vi.set_result(k, dv)
+            vi.finish(k, dv)
+            assert np.array_equal(vi.values(), V_ref) and np.array_equal(vi.policy(), pi_ref)
+else:
+    import torch.distributed as dist
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))  # RCCL, one rank
+    red = Reducer(timing=True)
+    for rep in range(3):
+        res = solve_sharded(vi, reducer=red)
+        assert res["sweeps"] == k_ref and res["allreduces"] == 2 and res["host_reads"] == 1, res
+        assert np.array_equal(vi.values(), V_ref) and np.array_equal(vi.policy(), pi_ref)
+    torch.cuda.synchronize()
+    print("allreduce device ms", red.collect(), "calls", red.calls)
+    dist.destroy_process_group()
+vi.close()
+print("device protocol ok")
+"""
+
+
+@pytest.mark.parametrize("mode", ["steps", "rccl1"])
+@pytest.mark.parametrize("env_id,B,dtype", [("MiniGrid-LavaCrossingS11N5-v0", 2048, "f32"),
+                                            ("MiniGrid-FourRooms-v0", 300, "f64"),
+                                            ("MiniGrid-DoorKey-16x16-v0", 700, "f32"),
+                                            ("MiniGrid-Empty-16x16-v0", 1, "f32")])
+def test_device_protocol(mode, env_id, B, dtype):
+    """mgdp_vi_run_local_dev / run_to_dev / set_result: K and dV in a device buffer, read once.
+    "steps": the entry points on a torch stream; "rccl1": distributed.solve_sharded over a one-rank
+    RCCL group (the all-reduces are real RCCL collectives ordered on the protocol stream).  Batches
+    on both sides of the in-kernel-reduce limit (512) and a lone grid; equal to a one-device solve."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "-c", _DEVICE_PROTO, root, mode, env_id, str(B), dtype], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "device protocol ok" in r.stdout, r.stdout + r.stderr

@@ -128,28 +128,6 @@ def test_full_size_replicas_property():
         vi.close()
 
 
-def test_full_size_lava_batch_subset_vs_oracle():
-    # BASELINE configs[3]: LavaCrossingS11N5 x 65536 grids (one GPU's worth here); the global sweep
-    # count is the max of the per-grid counts; a sampled subset is checked bit-exactly.
-    env = mg.make("MiniGrid-LavaCrossingS11N5-v0")
-    B = 65536
-    cells = np.stack([env.generate(seed=s)[0][..., 0].T for s in range(B)]).astype(np.uint8)
-    vi = mg.ValueIteration(cells, dtype="f32")
-    k = vi.solve()
-    V = vi.values()
-    pi = vi.policy()
-    vi.close()
-    rng = np.random.default_rng(0)
-    idx = rng.choice(B, 48, replace=False)
-    per = [oracle.value_iteration(0, cells[i], dtype="f32")["sweeps"] for i in idx]
-    assert k >= max(per)
-    # deterministic grids stop at an exact fixed point (dV == 0), so every grid's V/pi after k
-    # sweeps equals its own fixed point: the subset solved alone must agree bit for bit
-    o = oracle.value_iteration(0, cells[idx], dtype="f32")
-    np.testing.assert_array_equal(V[idx], o["V"])
-    np.testing.assert_array_equal(pi[idx], o["pi"])
-
-
 def test_invalid_grids_raise():
     bad = np.full((1, 5, 5), 2, np.uint8)
     bad[0, 2, 2] = 6  # ball: outside the XYD model

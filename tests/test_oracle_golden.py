@@ -174,3 +174,24 @@ def test_oracle_finite_horizon_vs_reference_rewards(name):
         np.testing.assert_array_equal(o["V"][0], t[f"V_{tag}"])
         np.testing.assert_array_equal(o["pi"][0], t[f"pi0_{tag}"])
         np.testing.assert_array_equal(o["pi_t"][:, 0], t[f"pi_{tag}"])
+
+
+@pytest.mark.parametrize("name", table_names())
+def test_numpy_restatement_matches_golden_and_oracle(name):
+    """oracle/numpy_vi.py (the single-thread numpy CPU baseline) against the reference-derived
+    golden V*/pi*/sweeps and bit-for-bit against the C oracle in both dtypes."""
+    from oracle.numpy_vi import NumpyVI
+
+    t = load(f"table_{name}.npz")
+    model = int(t["model"])
+    cells = cells_from_enc(t["enc"])
+    r = NumpyVI(model, cells, dtype="f64").solve()
+    assert r["sweeps"] == int(t["sweeps"])
+    np.testing.assert_array_equal(r["pi"][0], t["pi"])
+    np.testing.assert_allclose(r["V"][0], t["V"], rtol=0, atol=1e-12)
+    for dtype in ("f32", "f64"):
+        r = NumpyVI(model, cells, dtype=dtype).solve()
+        o = oracle.value_iteration(model, cells, dtype=dtype)
+        assert r["sweeps"] == o["sweeps"]
+        np.testing.assert_array_equal(r["V"], o["V"])
+        np.testing.assert_array_equal(r["pi"], o["pi"])
