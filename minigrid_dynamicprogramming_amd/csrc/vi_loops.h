@@ -520,6 +520,11 @@ __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> 
     const int HW = geo.HWs;  // LDS stride: every thread (idle ones too) owns a slot, so LDS writes need no mask
     const int k_start = k;
     const DkTopo tp = pre ? *pre : dk_topo_soa(cl, geo, cc);  // pre: see fused_fast_xyd_soa
+    // Value sweeps use dk_step_fast, specialised per wave (a uniform branch) on whether any of
+    // its cells has a goal ahead (bit 0) or a key / door ahead or under it (bit 1).
+    const DkFast tpf = dk_fast_topo(tp, HW);
+    const uint32_t cls = dk_fast_class(tpf);
+    const uint32_t wcls = (__builtin_amdgcn_ballot_w64(cls & 1u) ? 1u : 0u) | (__builtin_amdgcn_ballot_w64(cls & 2u) ? 2u : 0u);
     T own[16];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -536,17 +541,21 @@ __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> 
         uint4 fl = make_uint4(0u, 0u, 0u, 0u);  // the previous sweep's flags (all 16 bytes: no branch on the wave count)
         if (LOCAL) fl = *reinterpret_cast<const uint4 *>(flags + (parity ^ 1) * 16);
         V4<T> nbs[4];
-        dk_load_nb(tp, Vin, nbs);
         uint32_t pk[4];
         const T rg = HMODE ? rgoal[k_target - 1 - k] : (T)1;
         T d;
-        if (HMODE == 2) {
+        if (HMODE != 2) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) nbs[q] = *reinterpret_cast<const V4<T> *>(Vin + tpf.nb[q]);
+            if (wcls == 0u) d = dk_step_fast<T, HMODE != 0, false, false>(tpf, cf, in, nbs, outv, rg);
+            else if (wcls == 1u) d = dk_step_fast<T, HMODE != 0, true, false>(tpf, cf, in, nbs, outv, rg);
+            else d = dk_step_fast<T, HMODE != 0, true, true>(tpf, cf, in, nbs, outv, rg);
+        } else {
+            dk_load_nb(tp, Vin, nbs);
             d = dk_step<T, true, true>(tp, cf, in, nbs, outv, pk, rg);
             if (own_cell)
                 *reinterpret_cast<uint4 *>(pit + (long long)(k_target - 1 - k) * pit_stride + c * 16) =
                     make_uint4(pk[0], pk[1], pk[2], pk[3]);
-        } else {
-            d = dk_step<T, false, HMODE != 0>(tp, cf, in, nbs, outv, pk, rg);
         }
         if (LOCAL) {
             asm volatile("" ::"v"(d));  // keep the arithmetic ahead of the test (no sinking past it)

@@ -363,6 +363,88 @@ __device__ __forceinline__ T dk_step(const DkTopo &tp, const Coef<T> &cf, const 
     return dv;
 }
 
+// Select-light value sweep of the DoorKey model (value-only form of dk_step, bit-identical).
+// Invalid states hold +0 in every tile (absorbing, never written otherwise) and V >= +0, so:
+//  * forward reads the front group whenever the front is walkable for SOME (has_key, door_open)
+//    -- a door or key front's non-walkable states are exactly its invalid, +0 states -- and a
+//    front forward never reads (wall, goal, lava, or any front of an absorbing cell) points at
+//    cell 0's group, a border cell that stays +0: no per-state select, max(., +0) is a no-op;
+//  * pickup (key ahead, has_key 0) and toggle (door ahead) add one candidate state each, +0 where
+//    the front is neither (one select per state, only in waves with such a cell: KD);
+//  * a cell walkable for only some (has_key, door_open) -- the door and key cells themselves --
+//    zeroes its invalid states (one select per state, same waves); an absorbing cell's own
+//    values, front read and goal flag are +0, so it yields +0 with no select;
+//  * max(fl(g*M), tq) is needed only in waves with a goal ahead of some cell (GOAL).
+// Every dropped candidate equals V[S] or is +0 <= V[S], and max is exact and order-free, so
+// V' and the |dV| test are those of dk_step's per-state form.  ~4.5 VALU per state in plain waves
+// (no key, door or goal next to any cell: most of a 16x16 grid) instead of ~11.
+struct DkFast {
+    uint32_t walk;   // as DkTopo
+    uint32_t f[4];   // bit 4 goal ahead (walkable own cell only), 6 key ahead, 7 door ahead
+    int nb[4];       // direction-major LDS index of the group forward reads (cell 0's when none)
+};
+__device__ __forceinline__ DkFast dk_fast_topo(const DkTopo &tp, int HWs) {  // tp: soa indices
+    DkFast q;
+    q.walk = tp.walk;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t f = tp.f[d];
+        const bool reads = tp.walk != 0u && !(f & 48u) && (f & 15u) != 0u;
+        q.nb[d] = reads ? tp.nb[d] : d * HWs * 4;
+        q.f[d] = tp.walk != 0u ? (f & (16u | 64u | 128u)) : 0u;
+    }
+    return q;
+}
+// wave class bits: 1 = some cell has a goal ahead, 2 = some cell has a key / door ahead or is one
+__device__ __forceinline__ uint32_t dk_fast_class(const DkFast &q) {
+    uint32_t goal = 0, kd = (q.walk != 0u && q.walk != 15u) ? 1u : 0u;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        goal |= (q.f[d] & 16u) ? 1u : 0u;
+        kd |= (q.f[d] & 192u) ? 1u : 0u;
+    }
+    return goal | (kd << 1);
+}
+
+template <typename T, bool FH, bool GOAL, bool KD>
+__device__ __forceinline__ T dk_step_fast(const DkFast &tp, const Coef<T> &cf, const T (&own)[16],
+                                          const V4<T> (&nbs)[4], T (&outv)[16], T rg = (T)1) {
+    T df[16];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t f = tp.f[d];
+        const bool key = f & 64u, door = f & 128u;
+        const T tqd = (f & 16u) ? (FH ? rg : (T)1) : (T)0;
+#pragma unroll
+        for (int hk = 0; hk < 2; ++hk) {
+#pragma unroll
+            for (int dop = 0; dop < 2; ++dop) {
+                const int hd = hk * 2 + dop, l = d * 4 + hd;
+                const T xS = own[l];
+                T M = vmax(vmax(own[((d + 3) & 3) * 4 + hd], own[((d + 1) & 3) * 4 + hd]), vmax(xS, nbs[d].v[hd]));
+                if (KD) {
+                    // pickup -> (d, 1, dop); toggle -> close (dop 1: (d, hk, 0)) / unlock (hk 1, dop 0: (d, 1, 1))
+                    T cand = (T)0;
+                    if (!hk) cand = key ? own[d * 4 + 2 + dop] : cand;
+                    if (dop) cand = door ? own[d * 4 + hk * 2] : cand;
+                    else if (hk) cand = door ? own[d * 4 + 3] : cand;
+                    M = vmax(M, cand);
+                }
+                T best = cf.g * M;
+                if (GOAL) best = vmax(best, tqd);
+                if (KD) best = ((tp.walk >> hd) & 1u) ? best : (T)0;
+                outv[l] = best;
+                df[l] = vabs(best - xS);
+            }
+        }
+    }
+    // max is exact and order-free: a three-input tree (v_max3) over the 16 differences
+    const T a = vmax(vmax(df[0], df[1]), df[2]), b = vmax(vmax(df[3], df[4]), df[5]);
+    const T c = vmax(vmax(df[6], df[7]), df[8]), e = vmax(vmax(df[9], df[10]), df[11]);
+    const T h = vmax(vmax(df[12], df[13]), df[14]);
+    return vmax(vmax(vmax(a, b), c), vmax(vmax(e, h), df[15]));
+}
+
 // LDS/HBM wrappers: read own values from Vin, update, write V and/or pi.
 template <typename T, bool SLIP, bool WRITE_V, bool WRITE_PI>
 __device__ __forceinline__ T xyd_update(const XydTopo<T> &tp, const Coef<T> &cf, const T *Vin, T *Vout,
