@@ -40,6 +40,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s peak
 
 WORKLOADS = {
     "empty16": dict(env_id="MiniGrid-Empty-16x16-v0", per_gpu=1, replicate=True, sharded=False),
+    # a stream of distinct lone grids: every step solves the next of 64 FourRooms seeds, handed to the
+    # resident server from HBM with the request (mgdp_vi_load_cells_device), no drain or relaunch
+    "fourrooms1": dict(env_id="MiniGrid-FourRooms-v0", per_gpu=1, distinct=64, replicate=False, sharded=False),
     "empty16x65536": dict(env_id="MiniGrid-Empty-16x16-v0", per_gpu=65536, replicate=True, sharded=False),
     "fourrooms4096": dict(env_id="MiniGrid-FourRooms-v0", per_gpu=4096, replicate=False, sharded=False),
     "lava65536": dict(env_id="MiniGrid-LavaCrossingS11N5-v0", global_grids=65536, replicate=False, sharded=True),
@@ -91,6 +94,8 @@ def make_cells(spec, rank, world):
     env = make(spec["env_id"])
     if spec.get("sharded"):
         lo, hi = shard_range(spec["global_grids"], rank, world)
+    elif spec.get("distinct"):
+        lo, hi = rank * spec["distinct"], (rank + 1) * spec["distinct"]
     else:
         lo, hi = rank * spec["per_gpu"], (rank + 1) * spec["per_gpu"]
     if spec.get("replicate"):
@@ -105,8 +110,9 @@ def make_cells(spec, rank, world):
     return cells, (lo, hi)
 
 
-def cpu_baseline(cells, model, gamma, tol, dtype, budget_s=8.0, nthreads=1):
-    """Time the oracle (oracle/, a C restatement of the same algorithm) on a bounded sample."""
+def cpu_baseline(cells, model, gamma, tol, dtype, budget_s=8.0, nthreads=1, lone=False):
+    """Time the oracle (oracle/, a C restatement of the same algorithm) on a bounded sample.
+    lone: the workload solves its grids one at a time (each its own stopping sweep)."""
     import threading
 
     from oracle import oracle
@@ -118,16 +124,19 @@ def cpu_baseline(cells, model, gamma, tol, dtype, budget_s=8.0, nthreads=1):
     # A lone-grid workload gives each OpenMP thread 64 states per sweep, so a threaded solve times
     # fork/join, not the cores: run one independent single-threaded solve loop per thread instead
     # (ctypes drops the GIL inside the oracle call).
-    replicated = nthreads > 1 and len(sample) < nthreads
+    replicated = nthreads > 1 and (len(sample) < nthreads or lone)
     loops = nthreads if replicated else 1
     per_call = 1 if replicated else nthreads
     counts = [[0, 0, 0] for _ in range(loops)]  # updates, solves, sweeps
     t0 = time.perf_counter()
 
     def loop(c):
+        i = 0
         while True:
-            r = oracle.value_iteration(model_id, sample, gamma, tol, dtype=dtype, nthreads=per_call)
-            c[0] += len(sample) * S * A * r["sweeps"]
+            g = sample[i % len(sample)][None] if lone else sample
+            i += 1
+            r = oracle.value_iteration(model_id, g, gamma, tol, dtype=dtype, nthreads=per_call)
+            c[0] += len(g) * S * A * r["sweeps"]
             c[1] += 1
             c[2] = r["sweeps"]
             if time.perf_counter() - t0 >= budget_s:
@@ -145,9 +154,11 @@ def cpu_baseline(cells, model, gamma, tol, dtype, budget_s=8.0, nthreads=1):
     updates = sum(c[0] for c in counts)
     solves = sum(c[1] for c in counts)
     how = f", {loops} threads each solving its own replica" if replicated else ""
+    what = (f"{solves} lone-grid solves cycling over {len(sample)} distinct grids" if lone else
+            f"{solves} full solves of {len(sample)} grid(s)")
     return {"value": updates / el, "unit": "updates/s", "cores": nthreads, "kind": "port",
-            "sample": f"{solves} full solves of {len(sample)} grid(s) of the same workload "
-                      f"({counts[0][2]} sweeps each, {dtype}{how}), oracle/mgdp_oracle.c, {el:.1f} s"}
+            "sample": f"{what} of the same workload ({counts[0][2]} sweeps in the last, {dtype}{how}), "
+                      f"oracle/mgdp_oracle.c, {el:.1f} s"}
 
 
 def load_traffic(key, solves_per_launch):
@@ -244,7 +255,7 @@ def main():
     # solves inside the timed launches: the K timed solves plus the priming solve a resident
     # server's launch also spans
     solves_in_launches = args.steps + m["primed"]
-    upd_per_solve = float(vi_info["updates_per_sweep"]) * m["sweeps"][-1]
+    upd_per_solve = float(vi_info["updates_per_sweep"]) * float(np.mean(m["sweeps"]))
     alg_bytes_launch = upd_per_solve * solves_in_launches * bpu / max(launches, 1)
     achieved = alg_bytes_launch / avg_launch_s / 1e9 if launches else 0.0
     comp_launch = compulsory_bytes_per_solve(vi_info, tsize, args.method, m["sweeps"][-1]) * solves_in_launches / max(launches, 1)
@@ -301,6 +312,7 @@ def main():
         },
         "sweeps": int(m["sweeps"][-1]),
         "roofline": roofline,
+        **({"sweeps_mean": float(np.mean(m["sweeps"])), "distinct_grids": len(cells)} if spec.get("distinct") else {}),
     }
     if m.get("collectives"):
         out["collectives"] = m["collectives"]
@@ -315,10 +327,12 @@ def main():
         out["roofline_hbm"] = hbm_side_measurement(args)
     if world == 1 and not args.no_cpu:
         out["host"] = host_info()
-        out["cpu_baseline"] = cpu_baseline(cells, vi_info["model"], args.gamma, args.tol, args.dtype, args.cpu_budget)
+        lone = bool(spec.get("distinct"))
+        out["cpu_baseline"] = cpu_baseline(cells, vi_info["model"], args.gamma, args.tol, args.dtype, args.cpu_budget,
+                                           lone=lone)
         out["cpu_baseline_all_cores"] = cpu_baseline(
             cells, vi_info["model"], args.gamma, args.tol, args.dtype, max(2.0, args.cpu_budget / 4),
-            nthreads=out["host"]["cores_used"])
+            nthreads=out["host"]["cores_used"], lone=lone)
         out["cpu_baseline_numpy"] = numpy_baseline(cells, vi_info["model"], args.gamma, args.tol, args.dtype,
                                                    max(2.0, args.cpu_budget / 4))
     print(json.dumps(out), flush=True)
@@ -344,44 +358,79 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded):
     import minigrid_dynamicprogramming_amd as mg
     from minigrid_dynamicprogramming_amd.distributed import solve_sharded
 
-    vi = mg.ValueIteration(cells, gamma=args.gamma, tol=args.tol, dtype=dtype, method=args.method,
-                           mapping=args.mapping, device=local)
+    distinct = WORKLOADS[args.workload].get("distinct")
+    vi = mg.ValueIteration(cells[:1] if distinct else cells, gamma=args.gamma, tol=args.tol, dtype=dtype,
+                           method=args.method, mapping=args.mapping, device=local)
+    if distinct:
+        # the grids stay resident in HBM; step i hands grid i mod n to the solver (device pointer)
+        grids = torch.from_numpy(np.ascontiguousarray(cells)).to(f"cuda:{local}")
+        torch.cuda.synchronize()
+        base, hw, n_grids = grids.data_ptr(), cells.shape[1] * cells.shape[2], len(cells)
+        nxt = [0]
 
-    def one_solve():
+    def one_solve(last=False):
         if sharded:
             return solve_sharded(vi, reducer=reducer)["sweeps"]
-        return vi.solve()
+        if distinct:
+            vi.load_device(base + (nxt[0] % n_grids) * hw)
+            nxt[0] += 1
+        return vi.solve(last)
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        one_solve()
-    # Enabling launch timing drains the stream (and asks a resident lone-grid server to leave), so
-    # the timed launches start after it; a persistent handle then gets one untimed priming solve,
-    # which relaunches the server (its launch is now timed), so the timed region holds no relaunch
-    # and its length does not depend on --steps.
+    # Warmup runs the timed sequence itself, edges included: timing on, W solves, then the same
+    # end-of-region teardown (a resident lone-grid server leaves, stream and device drained), so
+    # no first-time cost of that path lands in the timed region.
+    vi.enable_timing(True)
+    for i in range(args.warmup):
+        one_solve(last=i == args.warmup - 1)
+    vi.synchronize()
+    torch.cuda.synchronize()
+    # Re-enabling timing drops the warmup's launches; a persistent handle then gets untimed
+    # priming solves, which relaunch the server (its launch is timed from here), so the timed
+    # region holds no relaunch and its length does not depend on --steps.
     vi.enable_timing(True)
     if reducer is not None:
         reducer.collect()
         reducer.reset_counters()
     barrier()
     torch.cuda.synchronize()
+    # (16 of them: the first solves after the relaunch also run while the GPU clocks ramp back up
+    # from the drain, measured 3-4 us slower each)
     primed = 0
+    pstamps = [time.perf_counter()]
     if vi.persistent:
-        one_solve()
-        primed = 1
+        for _ in range(16):
+            one_solve()
+            primed += 1
+            pstamps.append(time.perf_counter())
+    stamps = [] if os.environ.get("MGDP_BENCH_STAMPS") else None  # diagnostics: where the region's time goes
     t0 = time.perf_counter()
     sweeps = []
-    for _ in range(args.steps):
-        sweeps.append(one_solve())
+    for i in range(args.steps):
+        # the last solve dismisses a resident lone-grid server (mgdp_vi_solve_last) instead of the
+        # synchronize below telling it to leave
+        sweeps.append(one_solve(last=i == args.steps - 1))
+        if stamps is not None:
+            stamps.append(time.perf_counter())
     # make the last solve final: a resident lone-grid server is told to leave (it exits within a
     # poll) and the stream drained; a device synchronize alone would wait out the server's idle limit
     vi.synchronize()
+    if stamps is not None:
+        stamps.append(time.perf_counter())
     torch.cuda.synchronize()
+    if stamps is not None:
+        stamps.append(time.perf_counter())
     barrier()
     elapsed = time.perf_counter() - t0
+    if stamps is not None:
+        us = [(b - a) * 1e6 for a, b in zip([t0] + stamps[:-1], stamps)]
+        log(json.dumps({"stamps_us": {"prime": [round((b - a) * 1e6, 2) for a, b in zip(pstamps[:-1], pstamps[1:])],
+                                      "gap": round((t0 - pstamps[-1]) * 1e6, 2),
+                                      "solves": [round(x, 2) for x in us[:-2]], "vi_sync": round(us[-2], 2),
+                                      "dev_sync": round(us[-1], 2), "region": round(elapsed * 1e6, 2)}}))
     kern_ms, launches = vi.kernel_time()
     vi.enable_timing(False)
     info = {"A": 7 if vi.model == "xyd" else 5, "W": vi.W, "H": vi.H, "S": vi.S, "B": vi.B, "model": vi.model,

@@ -111,9 +111,13 @@ int mgdp_vi_destroy(mgdp_vi *vi);
 /* Launch on this hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL = own stream. */
 int mgdp_vi_set_stream(mgdp_vi *vi, void *hip_stream);
 /* Upload B*H*W row-major OBJECT_TO_IDX cell codes (host).  Validates them against the model:
- * MGDP_E_UNSUPPORTED if a cell type is outside the model or a border cell is walkable. */
+ * MGDP_E_UNSUPPORTED if a cell type is outside the model or a border cell is walkable.  With a
+ * persistent lone-grid server resident (see mgdp_vi_solve) the grid is staged in host-mapped
+ * memory and handed to the server with the next request: no stream drain, no relaunch. */
 int mgdp_vi_load_cells(mgdp_vi *vi, const uint8_t *cells);
-/* Same from device memory (already validated by the caller); async on the handle's stream. */
+/* Same from device memory (already validated by the caller).  The bytes must be complete before
+ * the call and unchanged until the next solve returns: a resident lone-grid server reads them
+ * itself with the next request; otherwise they are copied on the handle's stream. */
 int mgdp_vi_load_cells_device(mgdp_vi *vi, const uint8_t *d_cells);
 
 /* Whole solve on one device: V_0 = 0, sweeps until the global rule stops.  Synchronous.
@@ -122,6 +126,9 @@ int mgdp_vi_load_cells_device(mgdp_vi *vi, const uint8_t *d_cells);
  * call that uses the stream, after 100 us without a request, or after 2 s.  MGDP_PERSISTENT=0 in
  * the environment (read at create) turns it off. */
 int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *converged_out);
+/* mgdp_vi_solve, after which a persistent lone-grid server leaves at once instead of idling out
+ * (the caller has no further solve for now); the next solve relaunches it.  Same results. */
+int mgdp_vi_solve_last(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *converged_out);
 /* *on = 1 if mgdp_vi_solve on this handle goes through the persistent server. */
 int mgdp_vi_persistent(const mgdp_vi *vi, int32_t *on);
 /* Name of the kernel mgdp_vi_kernel_time times on this handle (as rocprofv3 lists it): vi_serve_kernel,

@@ -75,6 +75,7 @@ SIGNATURES = {
     "mgdp_vi_load_cells": (ctypes.c_int, [_P, _P]),
     "mgdp_vi_load_cells_device": (ctypes.c_int, [_P, _P]),
     "mgdp_vi_solve": (ctypes.c_int, [_P, _I32P, _DP, _I32P]),
+    "mgdp_vi_solve_last": (ctypes.c_int, [_P, _I32P, _DP, _I32P]),
     "mgdp_vi_reset": (ctypes.c_int, [_P]),
     "mgdp_vi_run_local": (ctypes.c_int, [_P, _I32P]),
     "mgdp_vi_run_to": (ctypes.c_int, [_P, _I32, _DP]),

@@ -108,6 +108,14 @@ struct mgdp_vi {
     unsigned long long serve_life_ticks = 200000000; // 2 s
     int serve_pollers = 1;  // waves polling the request word (MGDP_SERVE_POLLERS; 1 measured 0.2-0.4 us faster than 4)
     std::chrono::steady_clock::time_point serve_last{};  // host time of the last served result
+    // A new lone grid for a resident server: the bytes wait at pending_src (host-mapped staging
+    // h_stage, or the caller's device memory) and the next request carries kServeNewCells; a server
+    // stop before that copies them into d_cells instead.
+    uint8_t *h_stage = nullptr;   // pinned, mapped: W*H bytes (B == 1 handles)
+    uint8_t *d_stage = nullptr;   // its device alias
+    unsigned long long pending_src = 0;
+    bool last_req = false;        // the request being posted is the server's last (mgdp_vi_solve_last)
+    bool exiting = false;         // a server told to leave after its last request may still be on the stream
 };
 
 namespace {
@@ -262,6 +270,10 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
     if constexpr (MODEL == MGDP_MODEL_DOORKEY && MAP == MGDP_MAP_CELL && !SLIP) {
         if (vi->dk1t) kern = FusedK<T, MODEL, SLIP, MAP, kWpDk1t>::fn;
     }
+    if constexpr (MAP == MGDP_MAP_CELL) {  // one cell per thread, direction-major: the stripped variant
+        if (kern == FusedK<T, MODEL, SLIP, MAP, 0>::fn && !vi->pair && !vi->quad && vi->HW <= vi->fused_block)
+            kern = FusedK<T, MODEL, SLIP, MAP, kWpSoa>::fn;
+    }
     if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
     TimedPair tp;
     if (int rc = timed_begin(vi, -1, &tp)) return rc;
@@ -405,6 +417,7 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
                 if (tagged && relaunches < 4) {
                     ++relaunches;
                     DeviceGuard guard(vi->d.device);  // the served fast path of mgdp_vi_solve holds none
+                    __atomic_store_n(vi->h_out + 11, 0ull, __ATOMIC_RELEASE);
                     if (int rc = dispatch<ServeF>(vi, vi->epoch - 1u)) return rc;
                     continue;
                 }
@@ -448,13 +461,57 @@ bool serve_eligible(const mgdp_vi *vi) {
            (vi->HW <= vi->cpt * vi->fused_block || vi->wave_p) && !vi->pair && !vi->quad;
 }
 // Ask a resident server to leave and drain the stream.  Every entry point that enqueues other
-// work on the stream, or reads results, calls this first.
-int server_stop(mgdp_vi *vi) {
-    if (!vi->serving) return 0;
-    __atomic_store_n(vi->h_out + 4, kServeQuit, __ATOMIC_RELEASE);
-    vi->serving = false;
-    MGDP_HIP(hipStreamSynchronize(vi->stream));
+// work on the stream, or reads results, calls this first.  A grid handed over for the next request
+// but not yet served goes to d_cells here, so every other launch sees it.
+// drain = false (mgdp_vi_synchronize): wait for the server's exit word -- its V / pi stores are
+// then complete and visible, and nothing else is queued behind it -- instead of the stream's
+// completion signal, which a later device synchronize still observes.
+int server_stop(mgdp_vi *vi, bool drain = true) {
+    if (vi->serving) {
+        __atomic_store_n(vi->h_out + 4, kServeQuit, __ATOMIC_RELEASE);
+        vi->serving = false;
+        if (drain) {
+            MGDP_HIP(hipStreamSynchronize(vi->stream));
+            vi->exiting = false;
+        } else {
+            const volatile unsigned long long *h = vi->h_out;
+            for (uint64_t spin = 0; h[11] == 0; ++spin) {
+                if ((spin & 1023) == 1023) {  // a server that never started or faulted: the stream says
+                    const hipError_t q = hipStreamQuery(vi->stream);
+                    if (q == hipSuccess) break;
+                    if (q != hipErrorNotReady) return hip_fail(q, "persistent server", __FILE__, __LINE__);
+                }
+            }
+            std::atomic_thread_fence(std::memory_order_acquire);
+        }
+    }
+    if (vi->pending_src) {
+        MGDP_HIP(hipMemcpyAsync(vi->d_cells, reinterpret_cast<const void *>(vi->pending_src), vi->HW, hipMemcpyDefault,
+                                vi->stream));
+        MGDP_HIP(hipStreamSynchronize(vi->stream));
+        vi->pending_src = 0;
+    }
     return 0;
+}
+// Post the next request word: epoch, plus kServeNewCells and the tagged source word when a new
+// grid is pending (source first, then the request, both release stores: x86 keeps them in order).
+void post_request(mgdp_vi *vi) {
+    ++vi->epoch;
+    unsigned long long w = (unsigned long long)vi->epoch;
+    if (vi->last_req) w |= kServeLast;
+    if (vi->pending_src) {
+        __atomic_store_n(vi->h_out + 12, vi->pending_src | ((w & 0xffffull) << 48), __ATOMIC_RELEASE);
+        w |= kServeNewCells;
+        vi->pending_src = 0;
+    }
+    __atomic_store_n(vi->h_out + 4, w, __ATOMIC_RELEASE);
+}
+// Hand a new lone grid to a resident server (no drain): true if it was taken.
+bool serve_handoff(mgdp_vi *vi, const void *src) {
+    const unsigned long long a = (unsigned long long)(uintptr_t)src;
+    if (!vi->serving || !serve_eligible(vi) || (a >> 48) != 0) return false;
+    vi->pending_src = a;
+    return true;
 }
 // Post request `epoch` (the server serves any request word != the last epoch it served) and make
 // sure a server is resident; reduce_env then waits for the published result.
@@ -466,9 +523,9 @@ int serve_request(mgdp_vi *vi) {
         if (idle_us * 100.0 > 0.5 * (double)vi->serve_idle_ticks)
             if (int rc = server_stop(vi)) return rc;
     }
-    ++vi->epoch;
-    __atomic_store_n(vi->h_out + 4, (unsigned long long)vi->epoch, __ATOMIC_RELEASE);
+    post_request(vi);
     if (!vi->serving) {
+        __atomic_store_n(vi->h_out + 11, 0ull, __ATOMIC_RELEASE);  // the exit word of this launch
         if (int rc = dispatch<ServeF>(vi, vi->epoch - 1u)) return rc;
         vi->serving = true;
     }
@@ -691,6 +748,10 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     if (e == hipSuccess) e = hipHostMalloc((void **)&vi->h_out, 16 * sizeof(unsigned long long),
                                            hipHostMallocMapped | hipHostMallocCoherent);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&vi->d_hout, vi->h_out, 0);
+    if (e == hipSuccess && d.B == 1) {
+        e = hipHostMalloc((void **)&vi->h_stage, (size_t)vi->HWp, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&vi->d_stage, vi->h_stage, 0);
+    }
     if (e == hipSuccess) {
         e = hipStreamCreateWithFlags(&vi->stream, hipStreamNonBlocking);
         vi->own_stream = e == hipSuccess;
@@ -748,6 +809,7 @@ int mgdp_vi_destroy(mgdp_vi *vi) {
     (void)hipFree(vi->d_rgoal);
     (void)hipFree(vi->d_pi_t);
     if (vi->h_out) (void)hipHostFree(vi->h_out);
+    if (vi->h_stage) (void)hipHostFree(vi->h_stage);
     if (vi->own_stream) (void)hipStreamDestroy(vi->stream);
     delete vi;
     return 0;
@@ -771,6 +833,16 @@ int mgdp_vi_set_stream(mgdp_vi *vi, void *s) {
 int mgdp_vi_load_cells(mgdp_vi *vi, const uint8_t *cells) {
     MGDP_CHECK(vi && cells, MGDP_E_INVALID, "null argument");
     if (int rc = validate_cells(vi->d, cells)) return rc;
+    // a resident lone-grid server takes the grid with its next request: staged in host memory
+    // (a solve is synchronous, so the server is not reading the staging buffer now)
+    if (vi->h_stage && vi->serving && serve_eligible(vi)) {
+        std::memcpy(vi->h_stage, cells, vi->HW);
+        if (serve_handoff(vi, vi->d_stage)) {
+            vi->cells_loaded = true;
+            vi->k_done_valid = false;
+            return 0;
+        }
+    }
     DeviceGuard guard(vi->d.device);
     if (int rc = server_stop(vi)) return rc;
     std::vector<uint8_t> pad((size_t)vi->d.B * vi->HWp, 0);
@@ -784,6 +856,11 @@ int mgdp_vi_load_cells(mgdp_vi *vi, const uint8_t *cells) {
 
 int mgdp_vi_load_cells_device(mgdp_vi *vi, const uint8_t *d_cells) {
     MGDP_CHECK(vi && d_cells, MGDP_E_INVALID, "null argument");
+    if (serve_handoff(vi, d_cells)) {  // the resident server reads the bytes with its next request
+        vi->cells_loaded = true;
+        vi->k_done_valid = false;
+        return 0;
+    }
     DeviceGuard guard(vi->d.device);
     if (int rc = server_stop(vi)) return rc;
     MGDP_HIP(hipMemcpy2DAsync(vi->d_cells, vi->HWp, d_cells, vi->HW, vi->HW, vi->d.B, hipMemcpyDeviceToDevice, vi->stream));
@@ -937,8 +1014,7 @@ int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *con
             vi->cur = 0;
             vi->k_done = 0;
             vi->k_done_valid = false;
-            ++vi->epoch;
-            __atomic_store_n(vi->h_out + 4, (unsigned long long)vi->epoch, __ATOMIC_RELEASE);
+            post_request(vi);
             vi->fresh = 0;
             int32_t k = 0;
             if (int rc = reduce_env(vi, &k, nullptr)) return rc;
@@ -983,6 +1059,18 @@ int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *con
     if (dv_out) *dv_out = dv;
     if (converged_out) *converged_out = vi->converged;
     return 0;
+}
+
+int mgdp_vi_solve_last(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *converged_out) {
+    MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
+    vi->last_req = true;
+    const int rc = mgdp_vi_solve(vi, sweeps_out, dv_out, converged_out);
+    vi->last_req = false;
+    if (vi->serving) {  // the request carried kServeLast: the server is leaving (or already gone)
+        vi->serving = false;
+        vi->exiting = true;
+    }
+    return rc;
 }
 
 int mgdp_vi_persistent(const mgdp_vi *vi, int32_t *on) {
@@ -1050,6 +1138,12 @@ int mgdp_vi_device_buffers(mgdp_vi *vi, void **d_V, void **d_pi) {
 int mgdp_vi_synchronize(mgdp_vi *vi) {
     MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
     DeviceGuard guard(vi->d.device);
+    if (vi->serving && !vi->pending_src) return server_stop(vi, false);  // the server is the stream's last work
+    if (vi->exiting && !vi->pending_src) {  // a server leaving after its last request: its exit word
+        vi->exiting = false;
+        vi->serving = true;  // (server_stop's quit word is harmless: it is leaving anyway)
+        return server_stop(vi, false);
+    }
     if (int rc = server_stop(vi)) return rc;
     MGDP_HIP(hipStreamSynchronize(vi->stream));
     return 0;

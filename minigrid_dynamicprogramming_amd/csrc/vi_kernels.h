@@ -6,6 +6,10 @@
 
 namespace mgdp {
 constexpr int kWpDk1t = -100;  // vi_fused_kernel variant tag: batched DoorKey on one LDS tile
+// vi_fused_kernel variant tag: the direction-major one-thread-per-cell path alone.  The generic
+// variant (WP = 0) also holds the cell-major, pair and quad loops, and a kernel's VGPR budget is
+// that of its hungriest path: stripping them is what sets the batched kernels' occupancy.
+constexpr int kWpSoa = -200;
 template <typename T, int MODEL> struct TopoOf { using type = XydTopo<T>; };
 template <typename T> struct TopoOf<T, MGDP_MODEL_DOORKEY> { using type = DkTopo; };
 
@@ -33,9 +37,10 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     // WP == kWpDk1t: batched DoorKey on one LDS tile (fused_fast_dk_1t); other WP < 0: -WP cells per
     // thread on the batched XYD direction-major path (fused_fast_xyd_soa_xn)
     constexpr bool DK1T = WP == kWpDk1t;
-    constexpr int CPT = WP < 0 && !DK1T ? -WP : 1;
+    constexpr bool SOA_ONLY = WP < 0;  // every negative tag runs the direction-major path alone
+    constexpr int CPT = WP < 0 && !DK1T && WP != kWpSoa ? -WP : 1;
     const bool fast = MAP == MGDP_MAP_CELL && geo.HW <= CPT * (int)blockDim.x;
-    const bool soa = fast && !geo.pair && !geo.quad;
+    const bool soa = SOA_ONLY || (fast && !geo.pair && !geo.quad);
     if (!SERVED) copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
     if (!soa) {
         // cell-major paths use the first S entries of each (Ss-sized) tile
@@ -97,7 +102,8 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
         }
         return true;  // V and pi were written by their owner threads
     }
-    if constexpr (SERVED) return true;
+    if constexpr (SERVED || SOA_ONLY) return true;
+    else {
     if (fast && MODEL == MGDP_MODEL_XYD && geo.pair) {
         int vf = 0;
         if (k_target < 0) fused_fast_xyd2<T, SLIP, true>(geo, cf, cl, V0, pis, slots, flags, k, k_target, vf, dvl, done);
@@ -136,6 +142,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
         dvenv[e] = dvl;
     }
     return true;
+    }
 }
 
 // WP > 0: the one-wave lone-grid variant (fused_wave_xyd), 64 threads, so its WP cells per lane
@@ -162,52 +169,72 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
 }
 
 // Persistent solver for a lone grid: one workgroup stays resident and serves solve requests posted
-// in host-mapped memory, removing the launch and dispatch latency from every solve.  The cells
-// cannot change while it is resident (every other entry point stops it first), so they are staged
-// in LDS once.  Lane 0 of every wave polls the request word (relaxed system-scope loads, the waves
-// staggered by s_sleep so a new request is seen a fraction of a round trip after it lands) and
-// also watches the LDS word another wave may already have set.  By default only wave 0 polls
+// in host-mapped memory, removing the launch and dispatch latency from every solve.  The grid is
+// staged in LDS (and its topology resolved) at launch and again whenever a request carries
+// kServeNewCells: the request's source word (host_cmd[8], tagged with the request's low 16 bits, so
+// a source written before the request can never be paired with an older one) names the new grid's
+// W*H bytes -- host-mapped staging or device memory --, which the workgroup reads with
+// system-scope loads (coherent with the host and with every XCD's L2), copies into LDS and into
+// the handle's HBM cells (so a later non-served launch sees the same grid).  Lane 0 of every
+// polling wave reads the request word (relaxed system-scope loads, the waves staggered by s_sleep)
+// and also watches the LDS word another wave may already have set.  By default only wave 0 polls
 // (`pollers` = 1; the others wait at the barrier): with four staggered pollers the barrier also
-// waited for the other waves' in-flight PCIe reads (measured 0.2-0.4 us per solve slower).  Request r (!= the last served)
-// runs a fresh fused solve whose {k, dV} is published tagged with r.  Every wave leaves on the quit
-// word, after `idle_ticks` without a request or after `life_ticks` in total (s_memrealtime,
-// 100 MHz); the host relaunches the server if a request finds it gone.
+// waited for the other waves' in-flight PCIe reads (measured 0.2-0.4 us per solve slower).  Request
+// r (!= the last served) runs a fresh fused solve whose {k, dV} is published tagged with r.  Every
+// wave leaves on the quit word, after `idle_ticks` without a request or after `life_ticks` in total
+// (s_memrealtime, 100 MHz); the host relaunches the server if a request finds it gone.
 constexpr unsigned long long kServeQuit = ~0ull;
+constexpr unsigned long long kServeNewCells = 1ull << 62;
+constexpr unsigned long long kServeLast = 1ull << 61;  // request flag: leave after serving it
+constexpr unsigned long long kServeSrcMask = (1ull << 48) - 1;
 
 template <typename T, int MODEL, bool SLIP, int MAP, int WP = 0>
 __global__ void __launch_bounds__(WP > 0 ? 64 : 1024)
-vi_serve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
+vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict__ V,
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ host_out, const unsigned long long *__restrict__ host_cmd,
                 unsigned long long served, unsigned long long idle_ticks, unsigned long long life_ticks, int pollers) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    __shared__ unsigned long long s_cmd;
+    __shared__ unsigned long long s_cmd, s_src;
     const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
-    copy16(smem + L.cells_off(), cells, geo.HWp);
+    uint8_t *cl = reinterpret_cast<uint8_t *>(smem + L.cells_off());
+    copy16(cl, cells, geo.HWp);
     if (threadIdx.x == 0) s_cmd = served;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     unsigned long long t_last = t_start;
     __syncthreads();
-    // the cells stay put while the server is resident: resolve this thread's cell topology once
+    // the grid stays put between kServeNewCells requests: resolve this thread's cell topology once
     typename TopoOf<T, MODEL>::type topo;
-    if constexpr (WP == 0) {
-        const uint8_t *cl = reinterpret_cast<const uint8_t *>(smem + L.cells_off());
-        const int cc = (int)threadIdx.x < geo.HW ? (int)threadIdx.x : 0;
-        if constexpr (MODEL == MGDP_MODEL_XYD) topo = xyd_topo_soa<T>(cl, geo, cc);
-        else topo = dk_topo_soa(cl, geo, cc);
-    }
+    auto resolve = [&]() {
+        if constexpr (WP == 0) {
+            const int cc = (int)threadIdx.x < geo.HW ? (int)threadIdx.x : 0;
+            if constexpr (MODEL == MGDP_MODEL_XYD) topo = xyd_topo_soa<T>(cl, geo, cc);
+            else topo = dk_topo_soa(cl, geo, cc);
+        }
+    };
+    resolve();
     while (true) {
         if (lane == 0 && wave < pollers) {  // the other waves wait at the barrier
             for (int i = 0; i < wave; ++i) __builtin_amdgcn_s_sleep(8);  // stagger the pollers
             while (true) {
-                const unsigned long long cmd = __hip_atomic_load(host_cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                unsigned long long cmd = __hip_atomic_load(host_cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                const unsigned long long now = __builtin_amdgcn_s_memrealtime();
                 if (cmd != served) {
+                    if (cmd != kServeQuit && (cmd & kServeNewCells)) {
+                        // the host wrote the source word before the request word; its tag proves it
+                        // belongs to this request (a stale read is simply repeated)
+                        unsigned long long src = __hip_atomic_load(host_cmd + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        while ((src >> 48) != (cmd & 0xffffull)) {
+                            if (__builtin_amdgcn_s_memrealtime() - t_start > life_ticks) { cmd = kServeQuit; break; }
+                            src = __hip_atomic_load(host_cmd + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        }
+                        __hip_atomic_store(&s_src, src & kServeSrcMask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
                     __hip_atomic_store(&s_cmd, cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     break;
                 }
                 if (__hip_atomic_load(&s_cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != served) break;
-                const unsigned long long now = __builtin_amdgcn_s_memrealtime();
                 if (now - t_last > idle_ticks || now - t_start > life_ticks) {
                     __hip_atomic_store(&s_cmd, kServeQuit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     break;
@@ -222,6 +249,16 @@ vi_serve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
         if (threadIdx.x == 0)
             __hip_atomic_store(host_out + 8, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #endif
+        if (cmd & kServeNewCells) {  // restage the grid named by the request
+            const uint8_t *src = reinterpret_cast<const uint8_t *>(s_src);
+            for (int i = threadIdx.x; i < geo.HW; i += blockDim.x) {
+                const uint8_t b = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                cl[i] = b;
+                cells[i] = b;
+            }
+            __syncthreads();
+            resolve();
+        }
         int k;
         double dvl;
         if (!fused_grid<T, MODEL, SLIP, MAP, true, WP>(geo, cf, cells, V, pi, kenv, dvenv, host_out, -1, 1, true,
@@ -229,6 +266,7 @@ vi_serve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
             threadIdx.x == 0)
             publish_tagged(host_out, k, dvl, (unsigned int)cmd);
         served = cmd;
+        if (cmd & kServeLast) break;
         t_last = __builtin_amdgcn_s_memrealtime();
         // Every wave is past s_cmd and the LDS tiles before the next request: an LDS-only barrier.
         // The V / pi stores of this solve stay in flight while the next request is polled (a
@@ -236,6 +274,11 @@ vi_serve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
         // has drained the stream.
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
+    // Leaving: every wave's V / pi stores complete, then one system-scope release tells the host
+    // (server_stop without a drain waits for this word instead of the stream's completion signal).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(host_out + 11, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // The fused solve with the SURVEY 8(f) item-3 options (ND = NoDeath lava, HMODE = finite horizon

@@ -178,6 +178,7 @@ class ValueIteration:
         self.horizon = int(horizon)
         self.desc = d
         self._solve_args = None
+        self._load_dev_fn = None
         h = ctypes.c_void_p()
         _lib.check(self.L.mgdp_vi_create(ctypes.byref(d), ctypes.byref(h)), "mgdp_vi_create")
         self.h = h
@@ -214,6 +215,20 @@ class ValueIteration:
         self.converged = False
         self.dv = float("nan")
 
+    def load_device(self, cells_ptr: int):
+        """Install new grids from device memory (mgdp_vi_load_cells_device): B*H*W row-major type
+        codes at `cells_ptr` (e.g. a torch uint8 tensor's data_ptr()), complete before the call and
+        unchanged until the next solve returns.  A resident lone-grid server takes the grid with
+        its next request, so this makes no HIP call; the bytes are not validated here."""
+        if self._load_dev_fn is None:
+            self._load_dev_fn = _lib.raw_fn("mgdp_vi_load_cells_device")
+        rc = self._load_dev_fn(self.h, ctypes.c_void_p(int(cells_ptr)))
+        if rc:
+            _lib.check(rc, "mgdp_vi_load_cells_device")
+        self.sweeps = 0
+        self.converged = False
+        self.dv = float("nan")
+
     def close(self):
         if getattr(self, "h", None):
             self.L.mgdp_vi_destroy(self.h)
@@ -227,13 +242,16 @@ class ValueIteration:
             pass
 
     # -- single-device solve
-    def solve(self) -> int:
+    def solve(self, last: bool = False) -> int:
+        """Whole solve (mgdp_vi_solve).  last=True (mgdp_vi_solve_last): a resident lone-grid server
+        leaves right after this solve instead of idling out; the next solve relaunches it."""
         if self._solve_args is None:  # reused ctypes arguments: nothing converted or allocated per solve
             self._out = (ctypes.c_int32(0), ctypes.c_double(0), ctypes.c_int32(0))
             self._solve_args = (ctypes.c_void_p(self.h.value if isinstance(self.h, ctypes.c_void_p) else self.h),) + \
                 tuple(ctypes.byref(o) for o in self._out)
             self._solve_fn = _lib.raw_fn("mgdp_vi_solve")
-        rc = self._solve_fn(*self._solve_args)
+            self._solve_last_fn = _lib.raw_fn("mgdp_vi_solve_last")
+        rc = (self._solve_last_fn if last else self._solve_fn)(*self._solve_args)
         if rc:
             _lib.check(rc, "mgdp_vi_solve")
         k, dv, conv = self._out

@@ -1,0 +1,152 @@
+"""The resident lone-grid server taking a new grid with each request (vi_serve_kernel,
+kServeNewCells): load() / load_device() on a handle whose server is resident hand the grid over
+without draining the stream; every solve must equal the oracle's solve of that grid alone (sweeps,
+V and pi bit-exact), whatever path the grid took (host staging, device memory, or a server stop
+that copies a pending grid into the handle's cells)."""
+import numpy as np
+import pytest
+import torch
+
+import minigrid_dynamicprogramming_amd as mg
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def family_cells(env_id, seeds):
+    env = mg.make(env_id)
+    return np.stack([np.ascontiguousarray(env.generate(seed=s)[0][..., 0].T) for s in seeds]).astype(np.uint8)
+
+
+def random_xyd(n, W, H, seed):
+    """Closed-border grids with random interior walls / lava and one goal (XYD model)."""
+    rng = np.random.default_rng(seed)
+    out = np.full((n, H, W), 2, np.uint8)  # wall
+    for i in range(n):
+        inner = rng.choice(np.array([1, 1, 1, 2, 9], np.uint8), size=(H - 2, W - 2))
+        out[i, 1:-1, 1:-1] = inner
+        gy, gx = rng.integers(1, H - 1), rng.integers(1, W - 1)
+        out[i, gy, gx] = 8  # goal
+    return out
+
+
+def check(vi, cells_one, model_id, dtype):
+    k = vi.solve()
+    r = vi.result()
+    o = oracle.value_iteration(model_id, cells_one, dtype=dtype)
+    assert k == o["sweeps"], (k, o["sweeps"])
+    np.testing.assert_array_equal(r.pi, o["pi"])
+    np.testing.assert_array_equal(r.V, o["V"])
+
+
+def served_sequence(cells, model_id, dtype, via_device):
+    model = "xyd" if model_id == 0 else "doorkey"
+    vi = mg.ValueIteration(cells[:1], model=model, dtype=dtype)
+    try:
+        assert vi.persistent
+        dev = torch.from_numpy(cells).cuda() if via_device else None
+        torch.cuda.synchronize()
+        hw = cells.shape[1] * cells.shape[2]
+        sweeps = []
+        for i in range(len(cells)):
+            if via_device:
+                vi.load_device(dev.data_ptr() + i * hw)
+            else:
+                vi.load(cells[i:i + 1])
+            sweeps.append(vi.solve())
+            o = oracle.value_iteration(model_id, cells[i:i + 1], dtype=dtype)
+            assert sweeps[-1] == o["sweeps"], (i, sweeps[-1], o["sweeps"])
+            if i % 5 == 4:  # reading V/pi stops the server: the next load goes the stop-and-copy way
+                r = vi.result()
+                np.testing.assert_array_equal(r.V, o["V"])
+                np.testing.assert_array_equal(r.pi, o["pi"])
+        r = vi.result()
+        o = oracle.value_iteration(model_id, cells[-1:], dtype=dtype)
+        np.testing.assert_array_equal(r.V, o["V"])
+        np.testing.assert_array_equal(r.pi, o["pi"])
+        return sweeps
+    finally:
+        vi.close()
+
+
+@pytest.mark.parametrize("via_device", [False, True])
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_fourrooms_distinct_seeds(dtype, via_device):
+    cells = family_cells("MiniGrid-FourRooms-v0", range(24))
+    sweeps = served_sequence(cells, 0, dtype, via_device)
+    assert len(set(sweeps)) > 1  # the grids really differ
+
+
+@pytest.mark.parametrize("via_device", [False, True])
+def test_lava_distinct_seeds(via_device):
+    cells = family_cells("MiniGrid-LavaCrossingS11N5-v0", range(16))
+    served_sequence(cells, 0, "f32", via_device)
+
+
+@pytest.mark.parametrize("via_device", [False, True])
+def test_doorkey_distinct_seeds(via_device):
+    cells = family_cells("MiniGrid-DoorKey-8x8-v0", range(12))
+    served_sequence(cells, 1, "f64", via_device)
+
+
+@pytest.mark.parametrize("W,H", [(8, 8), (7, 9)])
+def test_one_wave_server_distinct_grids(W, H):
+    # <= 64 cells: the one-wave server variant (fused_wave_xyd); grids may be unsolvable (V = 0)
+    cells = random_xyd(12, W, H, seed=W * 100 + H)
+    served_sequence(cells, 0, "f32", via_device=False)
+
+
+def test_pending_grid_survives_a_stop_before_its_solve():
+    cells = family_cells("MiniGrid-FourRooms-v0", [3, 4])
+    vi = mg.ValueIteration(cells[:1], dtype="f32")
+    try:
+        check(vi, cells[:1], 0, "f32")
+        vi.solve()  # server resident
+        vi.load(cells[1:2])  # handed over, not yet served
+        vi.synchronize()  # the stop copies the pending grid into the handle's cells
+        check(vi, cells[1:2], 0, "f32")
+        vi.load(cells[0:1])
+        vi.enable_timing(True)  # another stop path
+        check(vi, cells[0:1], 0, "f32")
+        vi.enable_timing(False)
+    finally:
+        vi.close()
+
+
+def test_sweep_and_batched_paths_after_served_grids():
+    # a handle whose server took new grids, then re-used on the non-served path (run_local/run_to)
+    cells = family_cells("MiniGrid-FourRooms-v0", [5, 6, 7])
+    vi = mg.ValueIteration(cells[:1], dtype="f64")
+    try:
+        for i in range(3):
+            vi.load(cells[i:i + 1])
+            vi.solve()
+        vi.reset()
+        k = vi.run_local()
+        o = oracle.value_iteration(0, cells[2:3], dtype="f64")
+        assert k == o["sweeps"]
+    finally:
+        vi.close()
+
+
+def test_solve_last_dismisses_the_server_and_the_next_solve_relaunches():
+    cells = family_cells("MiniGrid-FourRooms-v0", range(6))
+    vi = mg.ValueIteration(cells[:1], dtype="f32")
+    try:
+        for i in range(6):
+            vi.load(cells[i:i + 1])
+            vi.solve(last=(i % 2 == 1))  # alternate: served, served-and-leave
+            if i % 3 == 2:
+                vi.synchronize()
+            o = oracle.value_iteration(0, cells[i:i + 1], dtype="f32")
+            assert vi.sweeps == o["sweeps"]
+        r = vi.result()
+        np.testing.assert_array_equal(r.V, o["V"])
+        np.testing.assert_array_equal(r.pi, o["pi"])
+        for _ in range(3):  # last solves back to back: each relaunches and dismisses
+            assert vi.solve(last=True) == o["sweeps"]
+        vi.synchronize()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(vi.result().V, o["V"])
+    finally:
+        vi.close()

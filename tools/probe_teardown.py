@@ -1,6 +1,7 @@
 """Where the lone-grid bench's fixed per-region cost goes: K served solves, then the end-of-region
 teardown (vi.synchronize(): quit word + stream drain, then torch.cuda.synchronize()), timed
-separately over many regions.  Run under different host-wait settings (ROC_ACTIVE_WAIT_TIMEOUT)."""
+separately over many regions.  Run under different host-wait settings (ROC_ACTIVE_WAIT_TIMEOUT,
+--spin: hipSetDeviceFlags(hipDeviceScheduleSpin) before torch touches the device)."""
 import json
 import os
 import sys
@@ -14,6 +15,11 @@ import minigrid_dynamicprogramming_amd as mg  # noqa: E402
 
 
 def main():
+    if "--spin" in sys.argv:
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        rc = hip.hipSetDeviceFlags(ctypes.c_uint(1))  # hipDeviceScheduleSpin
+        print(f"hipSetDeviceFlags(spin) -> {rc}", file=sys.stderr)
     enc, _ = mg.make("MiniGrid-Empty-16x16-v0").generate(seed=0)
     cells = np.ascontiguousarray(enc[:, :, 0].T)[None]
     torch.cuda.set_device(0)
@@ -47,6 +53,7 @@ def main():
                "p90_us": float(np.percentile(v, 90)) * 1e6} for k, v in rows.items()}
     out["env"] = {k: os.environ.get(k) for k in ("ROC_ACTIVE_WAIT_TIMEOUT",)}
     out["timing"] = timing
+    out["spin"] = "--spin" in sys.argv
     print(json.dumps(out))
     vi.close()
 
