@@ -167,7 +167,8 @@ class Ball(WorldObj):
 
 
 class Box(WorldObj):
-    """Box; the HIP step models an empty box (toggling it leaves an empty cell)."""
+    """Box; the HIP step models an empty box (toggling it leaves an empty cell).  Grid.set refuses a
+    box that holds an object."""
 
     def __init__(self, color, contains: WorldObj | None = None):
         super().__init__("box", color)
@@ -202,6 +203,13 @@ class Grid:
         if v is None:
             t, c, s = OBJECT_TO_IDX["empty"], 0, 0
         else:
+            if getattr(v, "contains", None) is not None:
+                # the grid is (type, colour, state) per cell, in HBM one byte per cell: a Box holding
+                # an object (world_object.py:272-294, toggle replaces the box by its contents)
+                # cannot be expressed, and no target family places one -- refuse it rather than
+                # step a different env
+                raise NotImplementedError("Box(contains=...) is not modelled: boxes are stepped as "
+                                          "empty (toggle leaves an empty cell); see DESIGN.md")
             t, c, s = v.encode()
         self.type[j, i], self.color[j, i], self.state[j, i] = t, c, s
         if self._owner is not None:

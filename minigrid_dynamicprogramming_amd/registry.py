@@ -34,7 +34,10 @@ def register(id: str, entry_point: str, kwargs: dict | None = None):
     if HAVE_GYMNASIUM:  # pragma: no cover
         import gymnasium
 
-        gymnasium.register(id=id, entry_point=entry_point, kwargs=dict(kwargs or {}))
+        # idempotent: gymnasium's plugin loader calls register_minigrid_envs (the pyproject.toml
+        # entry point) after this module's import already registered the ids
+        if id not in gymnasium.registry:
+            gymnasium.register(id=id, entry_point=entry_point, kwargs=dict(kwargs or {}))
 
 
 def make(id: str, **kwargs):
@@ -44,6 +47,9 @@ def make(id: str, **kwargs):
 
 
 def register_minigrid_envs():
+    """Register the target families' ids (here and, when importable, with gymnasium).  Also the
+    gymnasium.envs entry point (pyproject.toml), like the reference's
+    minigrid.__init__:register_minigrid_envs; calling it again is harmless."""
     ep = "minigrid_dynamicprogramming_amd.envs:"
     # LavaCrossing / SimpleCrossing, minigrid/__init__.py:34-83
     for s, n in ((9, 1), (9, 2), (9, 3), (11, 5)):

@@ -13,7 +13,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmgdp_oracle.so")
+# MGDP_ORACLE_LIB: an alternative build of the same source (the sanitizer build, oracle/Makefile asan)
+LIB_PATH = os.environ.get("MGDP_ORACLE_LIB") or os.path.join(HERE, "libmgdp_oracle.so")
 
 _lib = None
 

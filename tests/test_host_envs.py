@@ -105,3 +105,17 @@ def test_grid_api_round_trip():
     assert door.is_locked and not door.is_open and door.encode() == (4, 4, 2)
     with pytest.raises(AssertionError):
         g.get(8, 0)
+
+
+def test_box_with_contents_is_refused():
+    # world_object.py:272-294: Box.toggle replaces the box by its contents, which the one-byte cell
+    # code cannot hold; an empty box is modelled (toggle -> empty cell)
+    import pytest
+
+    from minigrid_dynamicprogramming_amd.core import Ball, Box, Grid
+
+    g = Grid(5, 5)
+    g.set(2, 2, Box("red"))
+    assert g.get(2, 2).type == "box"
+    with pytest.raises(NotImplementedError):
+        g.set(2, 3, Box("red", contains=Ball("blue")))

@@ -14,7 +14,8 @@ SRC = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 OUT = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_traffic.json"
 # run -> (bench key, kernel, solves per launch for a persistent server launch or None)
 RUNS = {
-    "empty16": ("empty16/fused/cell/f32", "vi_serve_kernel", 20),
+    # --steps 20 --warmup 0: the timed launch serves the 16 priming solves and the 20 timed ones
+    "empty16": ("empty16/fused/cell/f32", "vi_serve_kernel", 36),
     "empty16x65536_sweep": ("empty16x65536/sweep/cell/f32", "vi_sweep_pipe_kernel", None),
     "empty16x65536_fused": ("empty16x65536/fused/cell/f32", "vi_fused_kernel", None),
     "doorkey65536_fused": ("doorkey65536/fused/cell/f32", "vi_fused_kernel", None),
@@ -25,6 +26,7 @@ RUNS = {
     "step_doorkey16x65536": ("step_doorkey16x65536/step", "envs_step_kernel", None),
     "step_fourrooms65536": ("step_fourrooms65536/step", "envs_step_kernel", None),
     "step_lava65536": ("step_lava65536/step", "envs_step_kernel", None),
+    "step_doorkey16x1m": ("step_doorkey16x1m/step", "envs_step_kernel", None),
     "gen_lava65536": ("gen_lava65536/gen", "gen_grids_kernel", None),
     "gen_fourrooms65536": ("gen_fourrooms65536/gen", "gen_grids_kernel", None),
     "gen_doorkey16x65536": ("gen_doorkey16x65536/gen", "gen_grids_kernel", None),

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/pmc
 mkdir -p $OUT
 prof() { name=$1; ctr=$2; shift 2
-  timeout -k 10 600 rocprofv3 --pmc $ctr --kernel-trace -T -d $OUT/${name}_${ctr} -o run --output-format csv -- python3 bench.py "$@" --no-cpu --no-hbm > $OUT/${name}_${ctr}.log 2>&1 || { echo "$name $ctr failed"; exit 1; }; }
+  timeout -k 10 600 rocprofv3 --pmc $ctr --kernel-trace -T -d $OUT/${name}_${ctr} -o run --output-format csv -- python3 bench.py "$@" --no-cpu --no-hbm --no-f64 > $OUT/${name}_${ctr}.log 2>&1 || { echo "$name $ctr failed"; exit 1; }; }
 for c in FETCH_SIZE WRITE_SIZE; do
   prof empty16 $c --steps 20 --warmup 0
   prof empty16x65536_sweep $c --workload empty16x65536 --method sweep --steps 2 --warmup 1
