@@ -274,6 +274,13 @@ def main():
                  "(fused/served: cells in + V and pi out once per solve; sweep: 2*S*sizeof V + W*H per "
                  "grid-sweep); traffic = PMC HBM bytes per launch (profiles/pmc_traffic.json)"),
     }
+    sq = load_sq(f"{key}/{vi_info['kernel']}")
+    if sq and sq.get("valu_insts_per_launch") and launches:
+        # the batched fused kernel keeps V in LDS: its limits are issue / LDS / latency, not HBM
+        lane_ops = sq["valu_insts_per_launch"] * 64.0 / avg_launch_s
+        roofline["valu"] = {"achieved": lane_ops, "peak": VALU_PEAK_LANE_OPS, "unit": "lane-ops/s",
+                            "frac": lane_ops / VALU_PEAK_LANE_OPS, "lds_array_busy": sq.get("lds_array_busy"),
+                            "wave_split": sq.get("wave_split"), "source": sq.get("source")}
     if args.workload == "empty16":
         roofline["regime"] = ("single 4 KiB V grid on one resident workgroup: latency bound (barrier + LDS round trip "
                               "per sweep, host hand-off per solve); HBM is not the limit here (SURVEY 8(d) "

@@ -8,7 +8,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmgdp.so")
+# MGDP_LIB: an alternative build of the same sources (tools/ experiments with compile-time knobs)
+LIB_PATH = os.environ.get("MGDP_LIB") or os.path.join(HERE, "libmgdp.so")
 
 MGDP_OK = 0
 MGDP_E_INVALID = -1

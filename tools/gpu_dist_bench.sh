@@ -11,4 +11,5 @@ run() { name=$1; port=$2; shift 2
 run empty16 29511 --steps 20 --warmup 2
 run lava65536 29512 --workload lava65536 --steps 3 --warmup 1
 run doorkey65536 29513 --workload doorkey65536 --steps 2 --warmup 1
+run fourrooms1 29514 --workload fourrooms1 --steps 50 --warmup 5
 echo all ok
