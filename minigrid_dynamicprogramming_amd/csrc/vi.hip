@@ -91,6 +91,8 @@ struct mgdp_vi {
     int wave_p = 0;               // lone XYD grid on one wave: cells per lane (fused_wave_xyd)
     int cpt = 1;                  // batched XYD fused path: cells per thread (MGDP_CPT; 2 = fused_fast_xyd_soa_x2)
     int dk1t = 0;                 // batched fp32 DoorKey on one LDS tile (MGDP_DK_1T; fused_fast_dk_1t)
+    int pair2 = 1;                // batched plain XYD with cpt 2: adjacent-cell pairs (MGDP_PAIR2=0: fused_fast_xyd_soa_xn)
+    int wave2 = 0;                // batched plain XYD on one wave per grid: cells per lane P (fused_wave2_xyd; 0 = off)
     int sweep_block = 256;
     int sweep_m = 1;              // grids staged per workgroup iteration (measured: m>1 no faster)
     int sweep_pipe = 2;           // register-pipelined sweep kernel: grids fetched ahead (0 = staged kernel)
@@ -266,6 +268,21 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
     if constexpr (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL) {
         if (vi->cpt == 2) kern = FusedK<T, MODEL, SLIP, MAP, -2>::fn;
         else if (vi->cpt == 4) kern = FusedK<T, MODEL, SLIP, MAP, -4>::fn;
+        if constexpr (!SLIP) {  // two adjacent cells per thread, compile-time plane stride
+            if (vi->cpt == 2 && vi->pair2 && vi->HWs == 2 * vi->fused_block && vi->HWs % 128 == 0 && vi->HWs <= 1024) {
+                switch (vi->HWs / 128) {
+                case 1: kern = FusedK<T, MODEL, SLIP, MAP, kWpPair - 1>::fn; break;
+                case 2: kern = FusedK<T, MODEL, SLIP, MAP, kWpPair - 2>::fn; break;
+                case 3: kern = FusedK<T, MODEL, SLIP, MAP, kWpPair - 3>::fn; break;
+                case 4: kern = FusedK<T, MODEL, SLIP, MAP, kWpPair - 4>::fn; break;
+                case 5: kern = FusedK<T, MODEL, SLIP, MAP, kWpPair - 5>::fn; break;
+                case 6: kern = FusedK<T, MODEL, SLIP, MAP, kWpPair - 6>::fn; break;
+                case 7: kern = FusedK<T, MODEL, SLIP, MAP, kWpPair - 7>::fn; break;
+                case 8: kern = FusedK<T, MODEL, SLIP, MAP, kWpPair - 8>::fn; break;
+                default: break;
+                }
+            }
+        }
     }
     if constexpr (MODEL == MGDP_MODEL_DOORKEY && MAP == MGDP_MAP_CELL && !SLIP) {
         if (vi->dk1t) kern = FusedK<T, MODEL, SLIP, MAP, kWpDk1t>::fn;
@@ -274,10 +291,26 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
         if (kern == FusedK<T, MODEL, SLIP, MAP, 0>::fn && !vi->pair && !vi->quad && vi->HW <= vi->fused_block)
             kern = FusedK<T, MODEL, SLIP, MAP, kWpSoa>::fn;
     }
-    if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
+    int smem = L.total();
+    if constexpr (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL && !SLIP) {
+        if (vi->wave2) {
+            switch (vi->wave2) {
+            case 1: kern = FusedK<T, MODEL, SLIP, MAP, kWpWave2 - 1>::fn; break;
+            case 2: kern = FusedK<T, MODEL, SLIP, MAP, kWpWave2 - 2>::fn; break;
+            case 3: kern = FusedK<T, MODEL, SLIP, MAP, kWpWave2 - 3>::fn; break;
+            case 4: kern = FusedK<T, MODEL, SLIP, MAP, kWpWave2 - 4>::fn; break;
+            case 5: kern = FusedK<T, MODEL, SLIP, MAP, kWpWave2 - 5>::fn; break;
+            case 6: kern = FusedK<T, MODEL, SLIP, MAP, kWpWave2 - 6>::fn; break;
+            case 7: kern = FusedK<T, MODEL, SLIP, MAP, kWpWave2 - 7>::fn; break;
+            default: kern = FusedK<T, MODEL, SLIP, MAP, kWpWave2 - 8>::fn; break;
+            }
+            smem = wave2_smem_bytes(vi->HWp, vi->d.W, vi->wave2, (int)sizeof(T));
+        }
+    }
+    if (smem > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
     TimedPair tp;
     if (int rc = timed_begin(vi, -1, &tp)) return rc;
-    hipExtLaunchKernelGGL(kern, dim3(vi->d.B), dim3(vi->fused_block), L.total(), vi->stream, tp.a, tp.b, 0, g,
+    hipExtLaunchKernelGGL(kern, dim3(vi->d.B), dim3(vi->fused_block), smem, vi->stream, tp.a, tp.b, 0, g,
                        make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv,
                        vi->d_dvenv, vi->d_red, vi->d_ticket, pub, k_target, vi->fresh,
                        vi->d.B <= kInKernelReduceMaxB ? 1 : 0, ++vi->epoch, k_dev);
@@ -685,7 +718,9 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
         // default is P = 1 (grids of <= 64 cells); MGDP_WAVE=8 enables the rest (tests cover them).
         int wave_max = 1;
         if (const char *ev = std::getenv("MGDP_WAVE")) wave_max = std::atoi(ev);
-        if (d.B == 1 && d.model == MGDP_MODEL_XYD && d.method == MGDP_METHOD_FUSED && !vi->pair && !vi->quad &&
+        int wave_batch = 0;  // MGDP_WAVE_BATCH=1: batches on the one-wave path too (measurement knob)
+        if (const char *ev = std::getenv("MGDP_WAVE_BATCH")) wave_batch = std::atoi(ev);
+        if ((d.B == 1 || wave_batch) && d.model == MGDP_MODEL_XYD && d.method == MGDP_METHOD_FUSED && !vi->pair && !vi->quad &&
             !vi->opts && vi->HW <= 64 * std::min(wave_max, 8)) {
             int P = 1;
             while (64 * P < vi->HW) P *= 2;
@@ -700,12 +735,27 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
         if (const char *ev = std::getenv("MGDP_CPT")) cpt = std::atoi(ev);
         int lone_cpt = 1;  // a lone grid (latency) keeps one cell per thread unless MGDP_LONE_CPT=2
         if (const char *ev = std::getenv("MGDP_LONE_CPT")) lone_cpt = std::atoi(ev) == 2 ? 2 : 1;
-        if (d.B == 1) cpt = vi->wave_p ? 1 : lone_cpt;
+        if (vi->wave_p) cpt = 1;
+        else if (d.B == 1) cpt = lone_cpt;
         if ((cpt == 2 || cpt == 4) && d.model == MGDP_MODEL_XYD && d.method == MGDP_METHOD_FUSED &&
             !vi->pair && !vi->quad && !vi->opts && vi->HW <= 1024) {
             vi->cpt = cpt;
             vi->fused_block = (int)round_up((vi->HW + cpt - 1) / cpt, 64);
             vi->HWs = cpt * vi->fused_block;
+            vi->Ss = vi->S / vi->HW * vi->HWs;
+        }
+        if (const char *ev = std::getenv("MGDP_PAIR2")) vi->pair2 = std::atoi(ev) != 0;
+        // Batched deterministic XYD grids: one wave per grid, no workgroup barrier (fused_wave2_xyd)
+        // up to MGDP_WAVE2 cells per lane (0 disables it).
+        int wave2_max = 8;
+        if (const char *ev = std::getenv("MGDP_WAVE2")) wave2_max = std::atoi(ev);
+        const int P2 = (vi->HW + 63) / 64;
+        if (d.B > 1 && d.model == MGDP_MODEL_XYD && d.method == MGDP_METHOD_FUSED && d.slip_p < 0.0 && !vi->pair &&
+            !vi->quad && !vi->opts && !vi->wave_p && P2 <= std::min(wave2_max, 8)) {
+            vi->wave2 = P2;
+            vi->cpt = 1;
+            vi->fused_block = 64;
+            vi->HWs = (int)round_up(vi->HW, 64);
             vi->Ss = vi->S / vi->HW * vi->HWs;
         }
         int dk1t = 0;

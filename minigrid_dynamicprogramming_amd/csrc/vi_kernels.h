@@ -10,6 +10,14 @@ constexpr int kWpDk1t = -100;  // vi_fused_kernel variant tag: batched DoorKey o
 // variant (WP = 0) also holds the cell-major, pair and quad loops, and a kernel's VGPR budget is
 // that of its hungriest path: stripping them is what sets the batched kernels' occupancy.
 constexpr int kWpSoa = -200;
+// Tags -301 .. -308: batched deterministic XYD, two adjacent cells per thread, plane stride
+// HWS = 128 * (-tag - 300) known at compile time (fused_pair_xyd).
+constexpr int kWpPair = -300;
+__host__ __device__ constexpr bool wp_is_pair(int wp) { return wp <= kWpPair - 1 && wp >= kWpPair - 8; }
+// Tags -401 .. -408: batched deterministic XYD, one wave per grid, P = -tag - 400 cells per lane
+// (fused_wave2_xyd, its own compact LDS layout).
+constexpr int kWpWave2 = -400;
+__host__ __device__ constexpr bool wp_is_wave2(int wp) { return wp <= kWpWave2 - 1 && wp >= kWpWave2 - 8; }
 template <typename T, int MODEL> struct TopoOf { using type = XydTopo<T>; };
 template <typename T> struct TopoOf<T, MGDP_MODEL_DOORKEY> { using type = DkTopo; };
 
@@ -34,11 +42,32 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     const bool work = k_target < 0 ? (!(k > 0 && dvl < geo.tol) && k < geo.max_sweeps) : (k < k_target);
     if (!work) return false;
     const long long vb = (long long)e * geo.S;
+    if constexpr (wp_is_wave2(WP)) {  // its own LDS layout (wave2_*): cells, then the N/S tile
+        static_assert(MODEL == MGDP_MODEL_XYD && !SLIP && MAP == MGDP_MAP_CELL && !SERVED, "wave2: batched plain XYD");
+        constexpr int P = kWpWave2 - WP;
+        uint8_t *cl2 = smem + 256;
+        copy16(cl2, cells + (long long)e * geo.HWp, geo.HWp);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its LDS writes are ordered
+        T *tile = reinterpret_cast<T *>(smem + wave2_tile_off(geo.HWp));
+        auto done2 = [&](int kk, double dv) {
+            if (lone && threadIdx.x == 0)
+                publish(host_out, (unsigned long long)kk, (unsigned long long)__double_as_longlong(dv),
+                        (unsigned long long)kk, epoch);
+        };
+        if (k_target < 0) fused_wave2_xyd<T, true, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
+        else fused_wave2_xyd<T, false, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
+        if (threadIdx.x == 0) {
+            kenv[e] = k;
+            dvenv[e] = dvl;
+        }
+        return true;
+    }
     // WP == kWpDk1t: batched DoorKey on one LDS tile (fused_fast_dk_1t); other WP < 0: -WP cells per
     // thread on the batched XYD direction-major path (fused_fast_xyd_soa_xn)
     constexpr bool DK1T = WP == kWpDk1t;
     constexpr bool SOA_ONLY = WP < 0;  // every negative tag runs the direction-major path alone
-    constexpr int CPT = WP < 0 && !DK1T && WP != kWpSoa ? -WP : 1;
+    constexpr bool PAIR2 = wp_is_pair(WP);
+    constexpr int CPT = PAIR2 ? 2 : (WP < 0 && !DK1T && WP != kWpSoa ? -WP : 1);
     const bool fast = MAP == MGDP_MAP_CELL && geo.HW <= CPT * (int)blockDim.x;
     const bool soa = SOA_ONLY || (fast && !geo.pair && !geo.quad);
     if (!SERVED) copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
@@ -79,7 +108,12 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
         return true;
     }
     if (SERVED || soa) {  // served lone grids are always on this path (serve_eligible): no other code in the server
-        if constexpr (MODEL == MGDP_MODEL_DOORKEY && DK1T) {
+        if constexpr (PAIR2) {
+            static_assert(MODEL == MGDP_MODEL_XYD && !SLIP && MAP == MGDP_MAP_CELL, "pair path: plain XYD");
+            constexpr int HWS = 128 * (kWpPair - WP);
+            if (k_target < 0) fused_pair_xyd<T, true, HWS>(geo, cf, cl, V0, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+            else fused_pair_xyd<T, false, HWS>(geo, cf, cl, V0, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+        } else if constexpr (MODEL == MGDP_MODEL_DOORKEY && DK1T) {
             if (k_target < 0) fused_fast_dk_1t<T, true>(geo, cf, cl, V0, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
             else fused_fast_dk_1t<T, false>(geo, cf, cl, V0, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
         } else if constexpr (MODEL == MGDP_MODEL_XYD && CPT > 1) {
@@ -153,7 +187,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
 #define MGDP_XN_WPE 1
 #endif
 template <typename T, int MODEL, bool SLIP, int MAP, int WP = 0>
-__global__ void __launch_bounds__(WP > 0 ? 64 : 1024) __attribute__((amdgpu_waves_per_eu(WP == -2 ? MGDP_XN_WPE : 1)))
+__global__ void __launch_bounds__(WP > 0 || wp_is_wave2(WP) ? 64 : 1024) __attribute__((amdgpu_waves_per_eu(WP == -2 ? MGDP_XN_WPE : 1)))
 vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
@@ -161,7 +195,7 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
                 unsigned int epoch, const long long *__restrict__ k_target_dev) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
-    T *slots = reinterpret_cast<T *>(smem + L.slots_off());
+    T *slots = reinterpret_cast<T *>(smem + (wp_is_wave2(WP) ? 0 : L.slots_off()));
     // multi-GPU protocol (mgdp_vi_run_to_dev): the target sweep is the all-reduced K in device
     // memory, written by a collective ordered before this launch on the stream
     if (k_target_dev) k_target = (int)*k_target_dev;

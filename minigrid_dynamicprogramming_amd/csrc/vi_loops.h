@@ -415,6 +415,331 @@ __device__ __forceinline__ void fused_fast_xyd_soa_xn(const Geo &geo, const Coef
     }
 }
 
+// Batched deterministic XYD grids, two ADJACENT cells per thread (c0 = 2t, c0 + 1) and a
+// compile-time plane stride HWS (= 2 * blockDim): the direction-major tiles then hold a thread's two
+// values of a plane side by side, so each plane is one ds_write_b64 and its two front reads one
+// ds_read2_b32, and every LDS address is one of three per-thread bases (the thread's slot, and
+// that slot +-W rows) plus an immediate.  Forward reads the GEOMETRIC front cell: a front the
+// agent cannot enter (wall, door, key, goal, lava) is an invalid state whose V is +0 in every tile
+// (absorbing, V' = fl(0 * m) = +0), and V >= +0, so max(..., +0) is the identity and the value
+// equals fused_fast_xyd_soa's (which reads the own state instead); a goal ahead still adds its
+// constant 1 (only in waves that have one).  Same rule, same flags, same pi pass (the per-action
+// form on the usual topology), bit-identical V, pi and sweep counts.
+template <typename T, bool LOCAL, int HWS, typename Done>
+__device__ __forceinline__ void fused_pair_xyd(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *V0,
+                                               T *slots, uint8_t *flags, const T *Vg, T *Vg_out, int8_t *pig,
+                                               int &k, int k_target, double &dvl, const Done &done) {
+    struct alignas(2 * sizeof(T)) P2 { T a, b; };
+    T *const V1 = V0 + 4 * HWS;  // smem_layout: V1 follows V0 (Ss = 4 * HWs)
+    const int c0 = 2 * (int)threadIdx.x;
+    const int lane = (int)threadIdx.x & 63;
+    const int W = geo.W;
+    const bool even_w = (W & 1) == 0;
+    T ge[2];
+    uint32_t goal = 0;  // bit 4j + d: a goal is ahead of cell c0 + j in direction d
+    T own[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int c = c0 + j;
+        const int cc = c < geo.HW ? c : 0;  // idle slots shadow cell 0 (a wall) and never write HBM
+        const bool valid = xyd_free(cl[cc]);
+        ge[j] = valid ? cf.g : (T)0;
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+            goal |= (uint32_t)(valid && cl[valid ? cc + geo.off[d] : cc] == T_GOAL) << (4 * j + d);
+        const V4<T> x = k == 0 ? V4<T>{{(T)0, (T)0, (T)0, (T)0}} : *reinterpret_cast<const V4<T> *>(Vg + cc * 4);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) own[j][d] = x.v[d];
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) *reinterpret_cast<P2 *>(V0 + d * HWS + c0) = P2{own[0][d], own[1][d]};
+    const bool goal_wave = __builtin_amdgcn_ballot_w64(goal != 0u) != 0ull;
+    const int k_start = k;
+    __syncthreads();
+    int parity = 0;
+    T diff = (T)0;
+    // `out` is assigned only when the sweep commits, so after the loop the other register set
+    // still holds V_{k-1} (the pi pass needs its planes 0 / 2, which the tiles keep only at edges)
+    auto sweep = [&](const T *Vin, T *Vout, const T (&in)[2][4], T (&out)[2][4]) -> bool {
+        if (LOCAL ? k >= geo.max_sweeps : k >= k_target) return false;
+        uint4 fl = make_uint4(0u, 0u, 0u, 0u);
+        if (LOCAL) fl = *reinterpret_cast<const uint4 *>(flags + (parity ^ 1) * 16);
+        // geometric fronts: +1, +W, -1, -W in planes 0..3.  East / west stay in registers: the pair
+        // holds each other's, the lanes beside it hold the rest (DPP wave shifts); only the two
+        // wave-edge lanes read them from the tile, which the lanes at the other side of the edge
+        // wrote (below).  North / south: one 8-byte read per plane when W is even (aligned,
+        // conflict-free), two 4-byte reads otherwise.
+        T F[2][4];
+        F[0][0] = in[1][0];
+        F[1][2] = in[0][2];
+        F[1][0] = dpp_mov<0x130>(in[0][0]);  // wave_shl:1 -- lane i gets lane i+1's
+        F[0][2] = dpp_mov<0x138>(in[1][2]);  // wave_shr:1 -- lane i gets lane i-1's
+        if (lane == 63) F[1][0] = Vin[0 * HWS + c0 + 2];
+        if (lane == 0) F[0][2] = Vin[2 * HWS + c0 - 1];
+        if (even_w) {
+            const P2 s = *reinterpret_cast<const P2 *>(Vin + 1 * HWS + c0 + W);
+            const P2 n = *reinterpret_cast<const P2 *>(Vin + 3 * HWS + c0 - W);
+            F[0][1] = s.a; F[1][1] = s.b;
+            F[0][3] = n.a; F[1][3] = n.b;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                F[j][1] = Vin[1 * HWS + c0 + j + W];
+                F[j][3] = Vin[3 * HWS + c0 + j - W];
+            }
+        }
+        T d = (T)0;
+        T o[2][4];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const T m02 = vmax(in[j][0], in[j][2]), m13 = vmax(in[j][1], in[j][3]);
+            const T m[4] = {vmax(vmax(in[j][0], m13), F[j][0]), vmax(vmax(in[j][1], m02), F[j][1]),
+                            vmax(vmax(in[j][2], m13), F[j][2]), vmax(vmax(in[j][3], m02), F[j][3])};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[j][q] = ge[j] * m[q];
+        }
+        if (goal_wave) {  // max(fl(g * m), 1): the goal's reward (uniform branch: few waves have one)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) o[j][q] = ((goal >> (4 * j + q)) & 1u) ? vmax(o[j][q], (T)1) : o[j][q];
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) d = vmax(d, vabs(o[j][q] - in[j][q]));
+        if (LOCAL) {
+            asm volatile("" ::"v"(d));
+            if (k > k_start && (fl.x | fl.y | fl.z | fl.w) == 0u) return false;
+        }
+        diff = d;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) out[j][q] = o[j][q];
+        *reinterpret_cast<P2 *>(Vout + 1 * HWS + c0) = P2{out[0][1], out[1][1]};
+        *reinterpret_cast<P2 *>(Vout + 3 * HWS + c0) = P2{out[0][3], out[1][3]};
+        if (lane == 0) Vout[0 * HWS + c0] = out[0][0];           // read by the previous wave's lane 63
+        if (lane == 63) Vout[2 * HWS + c0 + 1] = out[1][2];      // read by the next wave's lane 0
+        if (LOCAL) flag_write(diff >= cf.tol, flags, parity);
+        __syncthreads();
+        parity ^= 1;
+        ++k;
+        return true;
+    };
+    T alt[2][4], prev[2][4];
+    int cur = 0;
+    while (true) {
+        if (!sweep(V0, V1, own, alt)) {
+            cur = 0;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) prev[j][q] = alt[j][q];
+            break;
+        }
+        if (!sweep(V1, V0, alt, own)) {
+            cur = 1;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    prev[j][q] = own[j][q];
+                    own[j][q] = alt[j][q];
+                }
+            break;
+        }
+    }
+    // V_{k-1}'s tile: complete planes 0 / 2 (nobody reads it until the pi pass; block_max's
+    // barrier orders these writes before it)
+    T *Vp = cur ? V0 : V1;
+    *reinterpret_cast<P2 *>(Vp + 0 * HWS + c0) = P2{prev[0][0], prev[1][0]};
+    *reinterpret_cast<P2 *>(Vp + 2 * HWS + c0) = P2{prev[0][2], prev[1][2]};
+    dvl = (double)block_max(diff, slots, 0);
+    done(k, dvl);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int c = c0 + j;
+        if (c < geo.HW) {
+            const XydTopo<T> tp = xyd_topo_soa<T>(cl, geo, c);
+            V4<T> op, tmp;
+            T nbv[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) op.v[q] = Vp[q * HWS + c];
+            xyd_load_nb(tp, Vp, nbv);
+            uint32_t pk;
+            xyd_step<T, false, true>(tp, cf, op, nbv, tmp, pk);
+            *reinterpret_cast<uint32_t *>(pig + c * 4) = pk;
+            *reinterpret_cast<V4<T> *>(Vg_out + c * 4) = V4<T>{{own[j][0], own[j][1], own[j][2], own[j][3]}};
+        }
+    }
+}
+
+// Batched deterministic XYD grids, ONE wave per grid (cells j*64 + lane, j < P), no workgroup
+// barrier: a wave's LDS instructions execute in issue order, so one tile suffices -- sweep k reads
+// its north / south fronts (V_{k-1}) and only then overwrites them with V_k.  East / west fronts
+// never touch LDS: cell c +- 1 is the neighbouring lane of the same block (DPP wave rotates), or
+// at a block edge the other end of the next / previous block (the same rotate of that block's
+// register); the first and last cell of the grid are border walls, whose fronts do not matter.
+// The tile keeps only planes 1 (read at c + W) and 3 (read at c - W), with zero pads of padw
+// cells on both sides, so it is 2 * 64 * P values per grid instead of two 4-plane tiles -- a
+// Empty-16 grid needs 2.3 KB of LDS, not 8.5.  Forward reads the geometric front as in
+// fused_pair_xyd (invalid states hold +0); the stop rule is the wave's ballot.  Same backups,
+// rule and pi pass as fused_fast_xyd_soa: bit-identical V, pi and sweep counts.
+// LDS: [slots 256 B][cells HWp][tile: pad | plane 3 (64P) | plane 1 (64P) | pad] (wave2_* below).
+__host__ __device__ inline int wave2_padw(int W) { return (W + 15) / 16 * 16; }
+__host__ __device__ inline int wave2_tile_off(int HWp) { return 256 + (HWp + 15) / 16 * 16; }
+__host__ __device__ inline int wave2_smem_bytes(int HWp, int W, int P, int tsize) {
+    return wave2_tile_off(HWp) + (2 * 64 * P + 2 * wave2_padw(W)) * tsize;
+}
+template <typename T, bool LOCAL, int P, typename Done>
+__device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *tile,
+                                                const T *Vg, T *Vg_out, int8_t *pig, int &k, int k_target,
+                                                double &dvl, const Done &done) {
+    static_assert(P >= 1 && P <= 8, "goal bits: 4 per cell, 32 per lane");
+    const int lane = (int)threadIdx.x;
+    const int W = geo.W, padw = wave2_padw(W);
+    T *const N3 = tile + padw;           // plane 3 (V of direction 3) of cell c at N3[c]
+    T *const S1 = tile + padw + 64 * P;  // plane 1 of cell c at S1[c]
+    T ge[P];
+    uint32_t goal = 0;
+    T own[P][4];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const int c = j * 64 + lane;
+        const int cc = c < geo.HW ? c : 0;  // idle slots shadow cell 0 (a wall) and never write HBM
+        const bool valid = xyd_free(cl[cc]);
+        ge[j] = valid ? cf.g : (T)0;
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+            goal |= (uint32_t)(valid && cl[valid ? cc + geo.off[d] : cc] == T_GOAL) << (4 * j + d);
+        const V4<T> x = k == 0 ? V4<T>{{(T)0, (T)0, (T)0, (T)0}} : *reinterpret_cast<const V4<T> *>(Vg + cc * 4);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) own[j][d] = x.v[d];
+        N3[c] = own[j][3];
+        S1[c] = own[j][1];
+    }
+    for (int i = lane; i < padw; i += 64) {
+        tile[i] = (T)0;
+        tile[padw + 128 * P + i] = (T)0;
+    }
+    asm volatile("" ::: "memory");
+    const bool goal_wave = __builtin_amdgcn_ballot_w64(goal != 0u) != 0ull;
+    const int k_start = k;
+    bool more = true;
+    T diff = (T)0;
+    auto sweep = [&](const T (&in)[P][4], T (&out)[P][4]) -> bool {  // `out` written only on commit
+        T FS[P], FN[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            FS[j] = S1[j * 64 + lane + W];
+            FN[j] = N3[j * 64 + lane - W];
+        }
+        if (LOCAL) {
+            if (k >= geo.max_sweeps) return false;
+            if (k > k_start && !more) return false;
+        } else if (k >= k_target) {
+            return false;
+        }
+        T R[P], L[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            R[j] = dpp_mov<0x134>(in[j][0]);  // wave_rol:1 -- lane i gets lane (i+1) mod 64
+            L[j] = dpp_mov<0x13C>(in[j][2]);  // wave_ror:1 -- lane i gets lane (i-1) mod 64
+        }
+        T o[P][4];
+        T dm = (T)0;
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const T FE = (j + 1 < P && lane == 63) ? R[j + 1] : R[j];
+            const T FW = (j > 0 && lane == 0) ? L[j - 1] : L[j];
+            const T m02 = vmax(in[j][0], in[j][2]), m13 = vmax(in[j][1], in[j][3]);
+            const T m[4] = {vmax(vmax(in[j][0], m13), FE), vmax(vmax(in[j][1], m02), FS[j]),
+                            vmax(vmax(in[j][2], m13), FW), vmax(vmax(in[j][3], m02), FN[j])};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[j][q] = ge[j] * m[q];
+        }
+        if (goal_wave) {
+#pragma unroll
+            for (int j = 0; j < P; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) o[j][q] = ((goal >> (4 * j + q)) & 1u) ? vmax(o[j][q], (T)1) : o[j][q];
+        }
+#pragma unroll
+        for (int j = 0; j < P; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                dm = vmax(dm, vabs(o[j][q] - in[j][q]));
+                out[j][q] = o[j][q];
+            }
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            S1[j * 64 + lane] = o[j][1];
+            N3[j * 64 + lane] = o[j][3];
+        }
+        asm volatile("" ::: "memory");
+        diff = dm;
+        if (LOCAL) more = __ballot(dm >= cf.tol) != 0ull;
+        ++k;
+        return true;
+    };
+    T alt[P][4], prev[P][4];
+    while (true) {
+        if (!sweep(own, alt)) {
+#pragma unroll
+            for (int j = 0; j < P; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) prev[j][q] = alt[j][q];
+            break;
+        }
+        if (!sweep(alt, own)) {
+#pragma unroll
+            for (int j = 0; j < P; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    prev[j][q] = own[j][q];
+                    own[j][q] = alt[j][q];
+                }
+            break;
+        }
+    }
+    dvl = (double)wave_max(diff);
+    done(k, dvl);
+    // pi of the last sweep = argmax on V_{k-1} (`prev`), per action with the usual topology
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        S1[j * 64 + lane] = prev[j][1];
+        N3[j * 64 + lane] = prev[j][3];
+    }
+    asm volatile("" ::: "memory");
+    T R[P], L[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        R[j] = dpp_mov<0x134>(prev[j][0]);
+        L[j] = dpp_mov<0x13C>(prev[j][2]);
+    }
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const int c = j * 64 + lane;
+        const T front[4] = {(j + 1 < P && lane == 63) ? R[j + 1] : R[j], S1[c + W],
+                            (j > 0 && lane == 0) ? L[j - 1] : L[j], N3[c - W]};
+        if (c < geo.HW) {
+            const XydTopo<T> tp = xyd_topo<T>(cl, geo, c);
+            V4<T> op, tmp;
+            T nbv[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                op.v[d] = prev[j][d];
+                nbv[d] = (tp.nbi[d] >> 2) != c ? front[d] : prev[j][d];  // blocked / terminal: own state
+            }
+            uint32_t pk;
+            xyd_step<T, false, true>(tp, cf, op, nbv, tmp, pk);
+            *reinterpret_cast<uint32_t *>(pig + c * 4) = pk;
+            *reinterpret_cast<V4<T> *>(Vg_out + c * 4) = V4<T>{{own[j][0], own[j][1], own[j][2], own[j][3]}};
+        }
+    }
+}
+
 // Lone XYD grid on ONE wave, P cells per lane (cell j*64 + lane, same direction-major tiles with
 // HWs = 64*P).  A wave's LDS instructions execute in issue order, so the writes of sweep k are
 // seen by the reads of sweep k+1 without a workgroup barrier, and the stopping rule is the wave's
