@@ -329,12 +329,29 @@ int launch_serve_t(mgdp_vi *vi, unsigned int served) {
     const Geo g = make_geo(vi);
     const Smem L = smem_layout(vi->Ss, vi->HWp, sizeof(T), vi->nbuf);
     auto kern = pick_wave<ServeK, T, MODEL, SLIP, MAP>(vi);
-    if constexpr (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL)
+    int smem = L.total();
+    if constexpr (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL) {
         if (vi->cpt == 2) kern = ServeK<T, MODEL, SLIP, MAP, -2>::fn;
-    if (L.total() > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total()));
+        if constexpr (!SLIP) {
+            if (vi->wave2) {
+                switch (vi->wave2) {
+                case 1: kern = ServeK<T, MODEL, SLIP, MAP, kWpWave2 - 1>::fn; break;
+                case 2: kern = ServeK<T, MODEL, SLIP, MAP, kWpWave2 - 2>::fn; break;
+                case 3: kern = ServeK<T, MODEL, SLIP, MAP, kWpWave2 - 3>::fn; break;
+                case 4: kern = ServeK<T, MODEL, SLIP, MAP, kWpWave2 - 4>::fn; break;
+                case 5: kern = ServeK<T, MODEL, SLIP, MAP, kWpWave2 - 5>::fn; break;
+                case 6: kern = ServeK<T, MODEL, SLIP, MAP, kWpWave2 - 6>::fn; break;
+                case 7: kern = ServeK<T, MODEL, SLIP, MAP, kWpWave2 - 7>::fn; break;
+                default: kern = ServeK<T, MODEL, SLIP, MAP, kWpWave2 - 8>::fn; break;
+                }
+                smem = wave2_smem_bytes(vi->HWp, vi->d.W, vi->wave2, (int)sizeof(T));
+            }
+        }
+    }
+    if (smem > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
     TimedPair tp;
     if (int rc = timed_begin(vi, -1, &tp)) return rc;
-    hipExtLaunchKernelGGL(kern, dim3(1), dim3(vi->fused_block), L.total(), vi->stream, tp.a, tp.b, 0, g,
+    hipExtLaunchKernelGGL(kern, dim3(1), dim3(vi->fused_block), smem, vi->stream, tp.a, tp.b, 0, g,
                           make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv, vi->d_dvenv,
                           vi->d_hout, vi->d_hout + 4, (unsigned long long)served, vi->serve_idle_ticks,
                           vi->serve_life_ticks, vi->serve_pollers);
@@ -491,7 +508,7 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
 // Persistent solver hand-off (lone grid on the one-thread-per-cell fused path).
 bool serve_eligible(const mgdp_vi *vi) {
     return vi->persistent && !vi->opts && vi->d.method == MGDP_METHOD_FUSED && vi->d.B == 1 && vi->d.mapping == MGDP_MAP_CELL &&
-           (vi->HW <= vi->cpt * vi->fused_block || vi->wave_p) && !vi->pair && !vi->quad;
+           (vi->HW <= vi->cpt * vi->fused_block || vi->wave_p || vi->wave2) && !vi->pair && !vi->quad;
 }
 // Ask a resident server to leave and drain the stream.  Every entry point that enqueues other
 // work on the stream, or reads results, calls this first.  A grid handed over for the next request
@@ -750,7 +767,9 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
         int wave2_max = 8;
         if (const char *ev = std::getenv("MGDP_WAVE2")) wave2_max = std::atoi(ev);
         const int P2 = (vi->HW + 63) / 64;
-        if (d.B > 1 && d.model == MGDP_MODEL_XYD && d.method == MGDP_METHOD_FUSED && d.slip_p < 0.0 && !vi->pair &&
+        int lone_wave2 = 0;  // MGDP_LONE_WAVE2=1: the lone served grid on one wave too
+        if (const char *ev = std::getenv("MGDP_LONE_WAVE2")) lone_wave2 = std::atoi(ev);
+        if ((d.B > 1 || lone_wave2) && d.model == MGDP_MODEL_XYD && d.method == MGDP_METHOD_FUSED && d.slip_p < 0.0 && !vi->pair &&
             !vi->quad && !vi->opts && !vi->wave_p && P2 <= std::min(wave2_max, 8)) {
             vi->wave2 = P2;
             vi->cpt = 1;
