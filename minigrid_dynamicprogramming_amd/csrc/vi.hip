@@ -252,6 +252,29 @@ auto pick_wave(const mgdp_vi *vi) -> decltype(K<T, MODEL, SLIP, MAP, 0>::fn) {
 }
 template <typename T, int MODEL, bool SLIP, int MAP, int WP>
 struct FusedK { static constexpr auto fn = vi_fused_kernel<T, MODEL, SLIP, MAP, WP>; };
+// The one-wave-per-grid instantiation for P cells per lane (XYD up to 8, DoorKey up to 4: its 16
+// states per cell fill the register file at P = 4); `dflt` if P is out of range.
+template <template <typename, int, bool, int, int> class K, typename T, int MODEL, bool SLIP, int MAP, typename F>
+F pick_wave2(int P, F dflt) {
+    constexpr int PMAX = MODEL == MGDP_MODEL_XYD ? 8 : 4;
+    switch (P) {
+    case 1: return K<T, MODEL, SLIP, MAP, kWpWave2 - 1>::fn;
+    case 2: return K<T, MODEL, SLIP, MAP, kWpWave2 - 2>::fn;
+    case 3: return K<T, MODEL, SLIP, MAP, kWpWave2 - 3>::fn;
+    case 4: return K<T, MODEL, SLIP, MAP, kWpWave2 - 4>::fn;
+    default: break;
+    }
+    if constexpr (PMAX > 4) {
+        switch (P) {
+        case 5: return K<T, MODEL, SLIP, MAP, kWpWave2 - 5>::fn;
+        case 6: return K<T, MODEL, SLIP, MAP, kWpWave2 - 6>::fn;
+        case 7: return K<T, MODEL, SLIP, MAP, kWpWave2 - 7>::fn;
+        case 8: return K<T, MODEL, SLIP, MAP, kWpWave2 - 8>::fn;
+        default: break;
+        }
+    }
+    return dflt;
+}
 template <typename T, int MODEL, bool SLIP, int MAP, int WP>
 struct ServeK { static constexpr auto fn = vi_serve_kernel<T, MODEL, SLIP, MAP, WP>; };
 
@@ -292,19 +315,10 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
             kern = FusedK<T, MODEL, SLIP, MAP, kWpSoa>::fn;
     }
     int smem = L.total();
-    if constexpr (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL && !SLIP) {
+    if constexpr (MAP == MGDP_MAP_CELL && !SLIP) {
         if (vi->wave2) {
-            switch (vi->wave2) {
-            case 1: kern = FusedK<T, MODEL, SLIP, MAP, kWpWave2 - 1>::fn; break;
-            case 2: kern = FusedK<T, MODEL, SLIP, MAP, kWpWave2 - 2>::fn; break;
-            case 3: kern = FusedK<T, MODEL, SLIP, MAP, kWpWave2 - 3>::fn; break;
-            case 4: kern = FusedK<T, MODEL, SLIP, MAP, kWpWave2 - 4>::fn; break;
-            case 5: kern = FusedK<T, MODEL, SLIP, MAP, kWpWave2 - 5>::fn; break;
-            case 6: kern = FusedK<T, MODEL, SLIP, MAP, kWpWave2 - 6>::fn; break;
-            case 7: kern = FusedK<T, MODEL, SLIP, MAP, kWpWave2 - 7>::fn; break;
-            default: kern = FusedK<T, MODEL, SLIP, MAP, kWpWave2 - 8>::fn; break;
-            }
-            smem = wave2_smem_bytes(vi->HWp, vi->d.W, vi->wave2, (int)sizeof(T));
+            kern = pick_wave2<FusedK, T, MODEL, SLIP, MAP>(vi->wave2, kern);
+            smem = wave2_smem_bytes(vi->HWp, vi->d.W, vi->wave2, (int)sizeof(T), MODEL == MGDP_MODEL_XYD ? 1 : 4);
         }
     }
     if (smem > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
@@ -334,16 +348,7 @@ int launch_serve_t(mgdp_vi *vi, unsigned int served) {
         if (vi->cpt == 2) kern = ServeK<T, MODEL, SLIP, MAP, -2>::fn;
         if constexpr (!SLIP) {
             if (vi->wave2) {
-                switch (vi->wave2) {
-                case 1: kern = ServeK<T, MODEL, SLIP, MAP, kWpWave2 - 1>::fn; break;
-                case 2: kern = ServeK<T, MODEL, SLIP, MAP, kWpWave2 - 2>::fn; break;
-                case 3: kern = ServeK<T, MODEL, SLIP, MAP, kWpWave2 - 3>::fn; break;
-                case 4: kern = ServeK<T, MODEL, SLIP, MAP, kWpWave2 - 4>::fn; break;
-                case 5: kern = ServeK<T, MODEL, SLIP, MAP, kWpWave2 - 5>::fn; break;
-                case 6: kern = ServeK<T, MODEL, SLIP, MAP, kWpWave2 - 6>::fn; break;
-                case 7: kern = ServeK<T, MODEL, SLIP, MAP, kWpWave2 - 7>::fn; break;
-                default: kern = ServeK<T, MODEL, SLIP, MAP, kWpWave2 - 8>::fn; break;
-                }
+                kern = pick_wave2<ServeK, T, MODEL, SLIP, MAP>(vi->wave2, kern);
                 smem = wave2_smem_bytes(vi->HWp, vi->d.W, vi->wave2, (int)sizeof(T));
             }
         }
@@ -773,6 +778,16 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
             !vi->quad && !vi->opts && !vi->wave_p && P2 <= std::min(wave2_max, 8)) {
             vi->wave2 = P2;
             vi->cpt = 1;
+            vi->fused_block = 64;
+            vi->HWs = (int)round_up(vi->HW, 64);
+            vi->Ss = vi->S / vi->HW * vi->HWs;
+        }
+        // Batched DoorKey grids the same way (fused_wave2_dk), up to MGDP_DK_WAVE2 cells per lane.
+        int dk_wave2_max = 0;
+        if (const char *ev = std::getenv("MGDP_DK_WAVE2")) dk_wave2_max = std::atoi(ev);
+        if (d.B > 1 && d.model == MGDP_MODEL_DOORKEY && d.method == MGDP_METHOD_FUSED && !vi->opts &&
+            P2 <= std::min(dk_wave2_max, 4)) {
+            vi->wave2 = P2;
             vi->fused_block = 64;
             vi->HWs = (int)round_up(vi->HW, 64);
             vi->Ss = vi->S / vi->HW * vi->HWs;

@@ -43,7 +43,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     if (!work) return false;
     const long long vb = (long long)e * geo.S;
     if constexpr (wp_is_wave2(WP)) {  // its own LDS layout (wave2_*): cells, then the N/S tile
-        static_assert(MODEL == MGDP_MODEL_XYD && !SLIP && MAP == MGDP_MAP_CELL, "wave2: plain XYD");
+        static_assert(!SLIP && MAP == MGDP_MAP_CELL, "wave2: plain XYD / DoorKey");
         constexpr int P = kWpWave2 - WP;
         uint8_t *cl2 = smem + 256;
         if (!SERVED) copy16(cl2, cells + (long long)e * geo.HWp, geo.HWp);  // a server staged them
@@ -57,8 +57,13 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
                         (unsigned long long)kk, epoch);
             }
         };
-        if (k_target < 0) fused_wave2_xyd<T, true, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
-        else fused_wave2_xyd<T, false, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
+        if constexpr (MODEL == MGDP_MODEL_XYD) {
+            if (k_target < 0) fused_wave2_xyd<T, true, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
+            else fused_wave2_xyd<T, false, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
+        } else {
+            if (k_target < 0) fused_wave2_dk<T, true, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
+            else fused_wave2_dk<T, false, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
+        }
         if (threadIdx.x == 0) {
             kenv[e] = k;
             dvenv[e] = dvl;
