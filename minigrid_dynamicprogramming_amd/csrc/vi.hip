@@ -64,6 +64,9 @@ struct mgdp_vi {
     double *d_dvenv = nullptr;
     unsigned long long *d_shards = nullptr;
     unsigned long long *d_red = nullptr;    // fused reduction shards [64][4]
+    unsigned long long *d_pub1 = nullptr;   // device copy of a run_local launch's {kmax, dV, kmin, epoch} (chained solve)
+    bool chain = true;                      // batched fused solve: run_local -> run_to(K from device memory), one host wait (MGDP_CHAIN=0: two)
+    int inkernel_max = kInKernelReduceMaxB; // batches up to this fold {k, dV} in the fused launch itself (MGDP_INKERNEL_MAX)
     unsigned int *d_ticket = nullptr;       // arrival ticket of the fused reduction
     unsigned long long *h_out = nullptr;    // host-mapped {kmax, dV bits, kmin, epoch, request}
     unsigned long long *d_hout = nullptr;   // device alias of h_out
@@ -207,10 +210,10 @@ int launch_opts_t(mgdp_vi *vi, int k_target) {
     hipExtLaunchKernelGGL(kern, dim3(vi->d.B), dim3(vi->fused_block), L.total(), vi->stream, tp.a, tp.b, 0, g,
                           make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv, vi->d_dvenv,
                           vi->d_red, vi->d_ticket, vi->d_hout, k_target, vi->fresh,
-                          vi->d.B <= kInKernelReduceMaxB ? 1 : 0, ++vi->epoch, (const T *)vi->d_rgoal, vi->d_pi_t);
+                          vi->d.B <= vi->inkernel_max ? 1 : 0, ++vi->epoch, (const T *)vi->d_rgoal, vi->d_pi_t);
     MGDP_HIP(hipGetLastError());
     vi->fresh = 0;
-    if (vi->d.B > kInKernelReduceMaxB) {
+    if (vi->d.B > vi->inkernel_max) {
         hipLaunchKernelGGL(vi_reduce_kernel, dim3(1), dim3(1024), 0, vi->stream, vi->d_kenv, vi->d_dvenv, vi->d.B,
                            vi->d_hout, vi->epoch);
         MGDP_HIP(hipGetLastError());
@@ -327,10 +330,10 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
     hipExtLaunchKernelGGL(kern, dim3(vi->d.B), dim3(vi->fused_block), smem, vi->stream, tp.a, tp.b, 0, g,
                        make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv,
                        vi->d_dvenv, vi->d_red, vi->d_ticket, pub, k_target, vi->fresh,
-                       vi->d.B <= kInKernelReduceMaxB ? 1 : 0, ++vi->epoch, k_dev);
+                       vi->d.B <= vi->inkernel_max ? 1 : 0, ++vi->epoch, k_dev);
     MGDP_HIP(hipGetLastError());
     vi->fresh = 0;
-    if (vi->d.B > kInKernelReduceMaxB) {
+    if (vi->d.B > vi->inkernel_max) {
         hipLaunchKernelGGL(vi_reduce_kernel, dim3(1), dim3(1024), 0, vi->stream, vi->d_kenv, vi->d_dvenv, vi->d.B,
                            pub, vi->epoch);
         MGDP_HIP(hipGetLastError());
@@ -816,6 +819,7 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     al((void **)&vi->d_dvenv, sizeof(double) * d.B);
     al((void **)&vi->d_shards, sizeof(unsigned long long) * 8 * (size_t)(d.max_sweeps + 1));
     al((void **)&vi->d_red, sizeof(unsigned long long) * (kRedShards * 4 + 2));
+    al((void **)&vi->d_pub1, sizeof(unsigned long long) * 4);
     if (d.horizon > 0) {
         al(&vi->d_rgoal, (size_t)d.horizon * vi->tsize);
         if (d.flags & MGDP_KEEP_POLICY_T) al((void **)&vi->d_pi_t, (size_t)d.horizon * BS);
@@ -847,6 +851,8 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     if (const char *ev = std::getenv("MGDP_SWEEP_GRID")) vi->sweep_grid = std::max(1, std::atoi(ev));
     if (const char *ev = std::getenv("MGDP_SWEEP_BLOCK")) vi->sweep_block = std::min(256, std::max(64, std::atoi(ev) / 64 * 64));
     if (const char *ev = std::getenv("MGDP_PERSISTENT")) vi->persistent = std::atoi(ev) != 0;
+    if (const char *ev = std::getenv("MGDP_CHAIN")) vi->chain = std::atoi(ev) != 0;
+    if (const char *ev = std::getenv("MGDP_INKERNEL_MAX")) vi->inkernel_max = std::max(0, std::atoi(ev));
     // DoorKey (64-128 B of V per thread) measured slower on the register pipeline (5.38 -> 3.3 TB/s
     // compulsory: the prefetch registers collide with the 16-state backup's), so it keeps the
     // staged kernel unless MGDP_SWEEP_PIPE asks otherwise.
@@ -890,6 +896,7 @@ int mgdp_vi_destroy(mgdp_vi *vi) {
     (void)hipFree(vi->d_dvenv);
     (void)hipFree(vi->d_shards);
     (void)hipFree(vi->d_red);
+    (void)hipFree(vi->d_pub1);
     (void)hipFree(vi->d_rgoal);
     (void)hipFree(vi->d_pi_t);
     if (vi->h_out) (void)hipHostFree(vi->h_out);
@@ -1130,9 +1137,21 @@ int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *con
     }
     if (int rc = mgdp_vi_reset(vi)) return rc;
     int32_t k = 0;
-    if (int rc = mgdp_vi_run_local(vi, &k)) return rc;
     double dv = 0.0;
-    if (int rc = mgdp_vi_run_to(vi, k, &dv)) return rc;
+    if (vi->chain && vi->d.method == MGDP_METHOD_FUSED && vi->d.horizon == 0 && !vi->opts && !serve_eligible(vi)) {
+        // The single-GPU form of the multi-GPU device protocol: run_local publishes {K, ...} to
+        // device memory and run_to(K) reads K there, enqueued back to back -- no host round trip
+        // and no launch gap between the two; the host waits once, for run_to's result.
+        DeviceGuard guard(vi->d.device);
+        if (int rc = server_stop(vi)) return rc;
+        if (int rc = dispatch<FusedF>(vi, -1, vi->d_pub1, (const long long *)nullptr)) return rc;
+        if (int rc = dispatch<FusedF>(vi, 0, (unsigned long long *)nullptr, (const long long *)vi->d_pub1)) return rc;
+        if (int rc = reduce_env(vi, &k, &dv)) return rc;
+        vi->k_done = k;
+    } else {
+        if (int rc = mgdp_vi_run_local(vi, &k)) return rc;
+        if (int rc = mgdp_vi_run_to(vi, k, &dv)) return rc;
+    }
     while (vi->d.horizon == 0 && !(dv < vi->d.tol) && k < vi->d.max_sweeps) {  // contraction broken by rounding: global rule
         if (int rc = mgdp_vi_sweep(vi, &dv)) return rc;
         ++k;
