@@ -255,11 +255,10 @@ auto pick_wave(const mgdp_vi *vi) -> decltype(K<T, MODEL, SLIP, MAP, 0>::fn) {
 }
 template <typename T, int MODEL, bool SLIP, int MAP, int WP>
 struct FusedK { static constexpr auto fn = vi_fused_kernel<T, MODEL, SLIP, MAP, WP>; };
-// The one-wave-per-grid instantiation for P cells per lane (XYD up to 8, DoorKey up to 4: its 16
-// states per cell fill the register file at P = 4); `dflt` if P is out of range.
+// The one-wave-per-grid instantiation for P cells per lane (1..8); `dflt` if P is out of range.
 template <template <typename, int, bool, int, int> class K, typename T, int MODEL, bool SLIP, int MAP, typename F>
 F pick_wave2(int P, F dflt) {
-    constexpr int PMAX = MODEL == MGDP_MODEL_XYD ? 8 : 4;
+    constexpr int PMAX = 8;
     switch (P) {
     case 1: return K<T, MODEL, SLIP, MAP, kWpWave2 - 1>::fn;
     case 2: return K<T, MODEL, SLIP, MAP, kWpWave2 - 2>::fn;
@@ -318,10 +317,10 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
             kern = FusedK<T, MODEL, SLIP, MAP, kWpSoa>::fn;
     }
     int smem = L.total();
-    if constexpr (MAP == MGDP_MAP_CELL && !SLIP) {
+    if constexpr (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL && !SLIP) {
         if (vi->wave2) {
             kern = pick_wave2<FusedK, T, MODEL, SLIP, MAP>(vi->wave2, kern);
-            smem = wave2_smem_bytes(vi->HWp, vi->d.W, vi->wave2, (int)sizeof(T), MODEL == MGDP_MODEL_XYD ? 1 : 4);
+            smem = wave2_smem_bytes(vi->HWp, vi->d.W, vi->wave2, (int)sizeof(T));
         }
     }
     if (smem > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
@@ -349,12 +348,6 @@ int launch_serve_t(mgdp_vi *vi, unsigned int served) {
     int smem = L.total();
     if constexpr (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL) {
         if (vi->cpt == 2) kern = ServeK<T, MODEL, SLIP, MAP, -2>::fn;
-        if constexpr (!SLIP) {
-            if (vi->wave2) {
-                kern = pick_wave2<ServeK, T, MODEL, SLIP, MAP>(vi->wave2, kern);
-                smem = wave2_smem_bytes(vi->HWp, vi->d.W, vi->wave2, (int)sizeof(T));
-            }
-        }
     }
     if (smem > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
     TimedPair tp;
@@ -516,7 +509,7 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
 // Persistent solver hand-off (lone grid on the one-thread-per-cell fused path).
 bool serve_eligible(const mgdp_vi *vi) {
     return vi->persistent && !vi->opts && vi->d.method == MGDP_METHOD_FUSED && vi->d.B == 1 && vi->d.mapping == MGDP_MAP_CELL &&
-           (vi->HW <= vi->cpt * vi->fused_block || vi->wave_p || vi->wave2) && !vi->pair && !vi->quad;
+           (vi->HW <= vi->cpt * vi->fused_block || vi->wave_p) && !vi->pair && !vi->quad;
 }
 // Ask a resident server to leave and drain the stream.  Every entry point that enqueues other
 // work on the stream, or reads results, calls this first.  A grid handed over for the next request
@@ -743,9 +736,7 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
         // default is P = 1 (grids of <= 64 cells); MGDP_WAVE=8 enables the rest (tests cover them).
         int wave_max = 1;
         if (const char *ev = std::getenv("MGDP_WAVE")) wave_max = std::atoi(ev);
-        int wave_batch = 0;  // MGDP_WAVE_BATCH=1: batches on the one-wave path too (measurement knob)
-        if (const char *ev = std::getenv("MGDP_WAVE_BATCH")) wave_batch = std::atoi(ev);
-        if ((d.B == 1 || wave_batch) && d.model == MGDP_MODEL_XYD && d.method == MGDP_METHOD_FUSED && !vi->pair && !vi->quad &&
+        if (d.B == 1 && d.model == MGDP_MODEL_XYD && d.method == MGDP_METHOD_FUSED && !vi->pair && !vi->quad &&
             !vi->opts && vi->HW <= 64 * std::min(wave_max, 8)) {
             int P = 1;
             while (64 * P < vi->HW) P *= 2;
@@ -775,22 +766,10 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
         int wave2_max = 8;
         if (const char *ev = std::getenv("MGDP_WAVE2")) wave2_max = std::atoi(ev);
         const int P2 = (vi->HW + 63) / 64;
-        int lone_wave2 = 0;  // MGDP_LONE_WAVE2=1: the lone served grid on one wave too
-        if (const char *ev = std::getenv("MGDP_LONE_WAVE2")) lone_wave2 = std::atoi(ev);
-        if ((d.B > 1 || lone_wave2) && d.model == MGDP_MODEL_XYD && d.method == MGDP_METHOD_FUSED && d.slip_p < 0.0 && !vi->pair &&
+        if (d.B > 1 && d.model == MGDP_MODEL_XYD && d.method == MGDP_METHOD_FUSED && d.slip_p < 0.0 && !vi->pair &&
             !vi->quad && !vi->opts && !vi->wave_p && P2 <= std::min(wave2_max, 8)) {
             vi->wave2 = P2;
             vi->cpt = 1;
-            vi->fused_block = 64;
-            vi->HWs = (int)round_up(vi->HW, 64);
-            vi->Ss = vi->S / vi->HW * vi->HWs;
-        }
-        // Batched DoorKey grids the same way (fused_wave2_dk), up to MGDP_DK_WAVE2 cells per lane.
-        int dk_wave2_max = 0;
-        if (const char *ev = std::getenv("MGDP_DK_WAVE2")) dk_wave2_max = std::atoi(ev);
-        if (d.B > 1 && d.model == MGDP_MODEL_DOORKEY && d.method == MGDP_METHOD_FUSED && !vi->opts &&
-            P2 <= std::min(dk_wave2_max, 4)) {
-            vi->wave2 = P2;
             vi->fused_block = 64;
             vi->HWs = (int)round_up(vi->HW, 64);
             vi->Ss = vi->S / vi->HW * vi->HWs;

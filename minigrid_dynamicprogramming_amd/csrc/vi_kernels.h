@@ -15,7 +15,7 @@ constexpr int kWpSoa = -200;
 constexpr int kWpPair = -300;
 __host__ __device__ constexpr bool wp_is_pair(int wp) { return wp <= kWpPair - 1 && wp >= kWpPair - 8; }
 // Tags -401 .. -408: batched deterministic XYD, one wave per grid, P = -tag - 400 cells per lane
-// (fused_wave2_xyd, its own compact LDS layout).
+// (fused_wave2_xyd, its own compact LDS layout; vi_fused_kernel only).
 constexpr int kWpWave2 = -400;
 __host__ __device__ constexpr bool wp_is_wave2(int wp) { return wp <= kWpWave2 - 1 && wp >= kWpWave2 - 8; }
 template <typename T, int MODEL> struct TopoOf { using type = XydTopo<T>; };
@@ -43,27 +43,19 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     if (!work) return false;
     const long long vb = (long long)e * geo.S;
     if constexpr (wp_is_wave2(WP)) {  // its own LDS layout (wave2_*): cells, then the N/S tile
-        static_assert(!SLIP && MAP == MGDP_MAP_CELL, "wave2: plain XYD / DoorKey");
+        static_assert(MODEL == MGDP_MODEL_XYD && !SLIP && MAP == MGDP_MAP_CELL && !SERVED, "wave2: batched plain XYD");
         constexpr int P = kWpWave2 - WP;
         uint8_t *cl2 = smem + 256;
-        if (!SERVED) copy16(cl2, cells + (long long)e * geo.HWp, geo.HWp);  // a server staged them
+        copy16(cl2, cells + (long long)e * geo.HWp, geo.HWp);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its LDS writes are ordered
         T *tile = reinterpret_cast<T *>(smem + wave2_tile_off(geo.HWp));
         auto done2 = [&](int kk, double dv) {
-            if (SERVED) {
-                if (threadIdx.x == 0) publish_tagged(host_out, kk, dv, epoch);
-            } else if (lone && threadIdx.x == 0) {
+            if (lone && threadIdx.x == 0)
                 publish(host_out, (unsigned long long)kk, (unsigned long long)__double_as_longlong(dv),
                         (unsigned long long)kk, epoch);
-            }
         };
-        if constexpr (MODEL == MGDP_MODEL_XYD) {
-            if (k_target < 0) fused_wave2_xyd<T, true, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
-            else fused_wave2_xyd<T, false, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
-        } else {
-            if (k_target < 0) fused_wave2_dk<T, true, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
-            else fused_wave2_dk<T, false, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
-        }
+        if (k_target < 0) fused_wave2_xyd<T, true, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
+        else fused_wave2_xyd<T, false, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
         if (threadIdx.x == 0) {
             kenv[e] = k;
             dvenv[e] = dvl;
@@ -236,7 +228,7 @@ constexpr unsigned long long kServeLast = 1ull << 61;  // request flag: leave af
 constexpr unsigned long long kServeSrcMask = (1ull << 48) - 1;
 
 template <typename T, int MODEL, bool SLIP, int MAP, int WP = 0>
-__global__ void __launch_bounds__(WP > 0 || wp_is_wave2(WP) ? 64 : 1024)
+__global__ void __launch_bounds__(WP > 0 ? 64 : 1024)
 vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict__ V,
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ host_out, const unsigned long long *__restrict__ host_cmd,
@@ -244,7 +236,7 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ unsigned long long s_cmd, s_src;
     const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
-    uint8_t *cl = reinterpret_cast<uint8_t *>(smem + (wp_is_wave2(WP) ? 256 : L.cells_off()));
+    uint8_t *cl = reinterpret_cast<uint8_t *>(smem + L.cells_off());
     copy16(cl, cells, geo.HWp);
     if (threadIdx.x == 0) s_cmd = served;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;

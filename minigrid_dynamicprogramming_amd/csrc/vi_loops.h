@@ -587,14 +587,10 @@ __device__ __forceinline__ void fused_pair_xyd(const Geo &geo, const Coef<T> &cf
 // fused_pair_xyd (invalid states hold +0); the stop rule is the wave's ballot.  Same backups,
 // rule and pi pass as fused_fast_xyd_soa: bit-identical V, pi and sweep counts.
 // LDS: [slots 256 B][cells HWp][tile: pad | plane 3 (64P) | plane 1 (64P) | pad] (wave2_* below).
-#ifndef MGDP_WAVE2_PK
-#define MGDP_WAVE2_PK 0  // packed-fp32 products and differences in fused_wave2_xyd (measured 6 % slower, off)
-#endif
 __host__ __device__ inline int wave2_padw(int W) { return (W + 15) / 16 * 16; }
 __host__ __device__ inline int wave2_tile_off(int HWp) { return 256 + (HWp + 15) / 16 * 16; }
-// grp: values per plane slot (XYD 1, DoorKey 4: the (has_key, door_open) group)
-__host__ __device__ inline int wave2_smem_bytes(int HWp, int W, int P, int tsize, int grp = 1) {
-    return wave2_tile_off(HWp) + (2 * 64 * P + 2 * wave2_padw(W)) * tsize * grp;
+__host__ __device__ inline int wave2_smem_bytes(int HWp, int W, int P, int tsize) {
+    return wave2_tile_off(HWp) + (2 * 64 * P + 2 * wave2_padw(W)) * tsize;
 }
 template <typename T, bool LOCAL, int P, typename Done>
 __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *tile,
@@ -665,15 +661,8 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
             const T m02 = vmax(in[j][0], in[j][2]), m13 = vmax(in[j][1], in[j][3]);
             const T m[4] = {vmax(vmax(in[j][0], m13), FE), vmax(vmax(in[j][1], m02), FS[j]),
                             vmax(vmax(in[j][2], m13), FW), vmax(vmax(in[j][3], m02), FN[j])};
-            if constexpr (sizeof(T) == 4 && MGDP_WAVE2_PK) {  // packed fp32 (v_pk_mul_f32): two products per issue slot
-                typedef float f2 __attribute__((ext_vector_type(2)));
-                const f2 g2 = {ge[j], ge[j]};
-                const f2 lo = f2{m[0], m[1]} * g2, hi = f2{m[2], m[3]} * g2;
-                o[j][0] = lo.x; o[j][1] = lo.y; o[j][2] = hi.x; o[j][3] = hi.y;
-            } else {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) o[j][q] = ge[j] * m[q];
-            }
+            for (int q = 0; q < 4; ++q) o[j][q] = ge[j] * m[q];
         }
 #pragma unroll
         for (int j = 0; j < P; ++j) {
@@ -684,15 +673,8 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
         }
 #pragma unroll
         for (int j = 0; j < P; ++j) {
-            if constexpr (sizeof(T) == 4 && MGDP_WAVE2_PK) {  // packed differences (v_pk_add_f32 with neg), exact as scalar
-                typedef float f2 __attribute__((ext_vector_type(2)));
-                const f2 dl = f2{o[j][0], o[j][1]} - f2{in[j][0], in[j][1]};
-                const f2 dh = f2{o[j][2], o[j][3]} - f2{in[j][2], in[j][3]};
-                dm = vmax(vmax(dm, vmax(vabs(dl.x), vabs(dl.y))), vmax(vabs(dh.x), vabs(dh.y)));
-            } else {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) dm = vmax(dm, vabs(o[j][q] - in[j][q]));
-            }
+            for (int q = 0; q < 4; ++q) dm = vmax(dm, vabs(o[j][q] - in[j][q]));
 #pragma unroll
             for (int q = 0; q < 4; ++q) out[j][q] = o[j][q];
         }
@@ -760,166 +742,6 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
             xyd_step<T, false, true>(tp, cf, op, nbv, tmp, pk);
             *reinterpret_cast<uint32_t *>(pig + c * 4) = pk;
             *reinterpret_cast<V4<T> *>(Vg_out + c * 4) = V4<T>{{own[j][0], own[j][1], own[j][2], own[j][3]}};
-        }
-    }
-}
-
-// Batched DoorKey grids, ONE wave per grid (cells j*64 + lane, j < P): fused_wave2_xyd's scheme
-// for the 16-state product model.  East / west front groups (4 (has_key, door_open) values each)
-// come from the neighbouring lanes by DPP wave rotates, north / south groups from one tile holding
-// planes 1 and 3 as 16-B groups (ds_read_b128 / ds_write_b128, consecutive lanes, conflict-free);
-// no barrier.  Forward reads the geometric front group: a front that is not walkable for a state
-// holds +0 there (walls, the goal, the door while closed, the key cell before pickup are invalid
-// states), and absorbing cells multiply by g = 0, so dk_step_fast's value form applies unchanged,
-// specialised per 64-cell block on its goal / key-door neighbours as in fused_fast_dk_soa.  The pi
-// pass runs dk_step's per-action form on V_{k-1} with the usual topology: bit-identical results.
-template <typename T, bool LOCAL, int P, typename Done>
-__device__ __forceinline__ void fused_wave2_dk(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *tile,
-                                               const T *Vg, T *Vg_out, int8_t *pig, int &k, int k_target,
-                                               double &dvl, const Done &done) {
-    const int lane = (int)threadIdx.x;
-    const int W = geo.W, padw = wave2_padw(W);
-    V4<T> *const N3 = reinterpret_cast<V4<T> *>(tile) + padw;           // plane-3 group of cell c
-    V4<T> *const S1 = reinterpret_cast<V4<T> *>(tile) + padw + 64 * P;  // plane-1 group of cell c
-    DkFast tf[P];
-    Coef<T> cfj[P];  // g = 0 for absorbing cells: their geometric front reads must not leak in
-    uint32_t cls[P];
-    T own[P][16];
-#pragma unroll
-    for (int j = 0; j < P; ++j) {
-        const int c = j * 64 + lane;
-        const int cc = c < geo.HW ? c : 0;  // idle slots shadow cell 0 (a wall) and never write HBM
-        const DkTopo tp = dk_topo(cl, geo, cc);
-        tf[j] = dk_fast_topo(tp, 0);
-        cfj[j] = cf;
-        cfj[j].g = tp.walk != 0u ? cf.g : (T)0;
-        const uint32_t cl1 = dk_fast_class(tf[j]);
-        cls[j] = (__builtin_amdgcn_ballot_w64(cl1 & 1u) ? 1u : 0u) | (__builtin_amdgcn_ballot_w64(cl1 & 2u) ? 2u : 0u);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const V4<T> x = k == 0 ? V4<T>{{(T)0, (T)0, (T)0, (T)0}} : *reinterpret_cast<const V4<T> *>(Vg + cc * 16 + 4 * q);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) own[j][4 * q + i] = x.v[i];
-        }
-        S1[c] = V4<T>{{own[j][4], own[j][5], own[j][6], own[j][7]}};
-        N3[c] = V4<T>{{own[j][12], own[j][13], own[j][14], own[j][15]}};
-    }
-    for (int i = lane; i < padw; i += 64) {
-        N3[i - padw] = V4<T>{{(T)0, (T)0, (T)0, (T)0}};
-        S1[64 * P + i] = V4<T>{{(T)0, (T)0, (T)0, (T)0}};
-    }
-    asm volatile("" ::: "memory");
-    const int k_start = k;
-    bool more = true;
-    T diff = (T)0;
-    auto rot = [&](const T (&x)[P][16], int j, int base, bool left, V4<T> &o) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o.v[i] = left ? dpp_mov<0x134>(x[j][base + i]) : dpp_mov<0x13C>(x[j][base + i]);
-    };
-    auto sweep = [&](const T (&in)[P][16], T (&out)[P][16]) -> bool {
-        V4<T> FS[P], FN[P];
-#pragma unroll
-        for (int j = 0; j < P; ++j) {
-            FS[j] = S1[j * 64 + lane + W];
-            FN[j] = N3[j * 64 + lane - W];
-        }
-        if (LOCAL) {
-            if (k >= geo.max_sweeps) return false;
-            if (k > k_start && !more) return false;
-        } else if (k >= k_target) {
-            return false;
-        }
-        T dm = (T)0;
-#pragma unroll
-        for (int j = 0; j < P; ++j) {
-            V4<T> nbs[4], Rn, Lp;
-            rot(in, j, 0, true, nbs[0]);   // east group: lane i+1's direction-0 values
-            rot(in, j, 8, false, nbs[2]);  // west group: lane i-1's direction-2 values
-            if (j + 1 < P) {
-                rot(in, j + 1, 0, true, Rn);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) nbs[0].v[i] = lane == 63 ? Rn.v[i] : nbs[0].v[i];
-            }
-            if (j > 0) {
-                rot(in, j - 1, 8, false, Lp);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) nbs[2].v[i] = lane == 0 ? Lp.v[i] : nbs[2].v[i];
-            }
-            nbs[1] = FS[j];
-            nbs[3] = FN[j];
-            T d;
-            if (cls[j] == 0u) d = dk_step_fast<T, false, false, false>(tf[j], cfj[j], in[j], nbs, out[j]);
-            else if (cls[j] == 1u) d = dk_step_fast<T, false, true, false>(tf[j], cfj[j], in[j], nbs, out[j]);
-            else d = dk_step_fast<T, false, true, true>(tf[j], cfj[j], in[j], nbs, out[j]);
-            dm = vmax(dm, d);
-        }
-#pragma unroll
-        for (int j = 0; j < P; ++j) {
-            S1[j * 64 + lane] = V4<T>{{out[j][4], out[j][5], out[j][6], out[j][7]}};
-            N3[j * 64 + lane] = V4<T>{{out[j][12], out[j][13], out[j][14], out[j][15]}};
-        }
-        asm volatile("" ::: "memory");
-        diff = dm;
-        if (LOCAL) more = __ballot(dm >= cf.tol) != 0ull;
-        ++k;
-        return true;
-    };
-    T alt[P][16], prev[P][16];
-    while (true) {
-        if (!sweep(own, alt)) {
-#pragma unroll
-            for (int j = 0; j < P; ++j)
-#pragma unroll
-                for (int q = 0; q < 16; ++q) prev[j][q] = alt[j][q];
-            break;
-        }
-        if (!sweep(alt, own)) {
-#pragma unroll
-            for (int j = 0; j < P; ++j)
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    prev[j][q] = own[j][q];
-                    own[j][q] = alt[j][q];
-                }
-            break;
-        }
-    }
-    dvl = (double)wave_max(diff);
-    done(k, dvl);
-    // pi of the last sweep = argmax on V_{k-1} (`prev`), per action with the usual topology
-#pragma unroll
-    for (int j = 0; j < P; ++j) {
-        S1[j * 64 + lane] = V4<T>{{prev[j][4], prev[j][5], prev[j][6], prev[j][7]}};
-        N3[j * 64 + lane] = V4<T>{{prev[j][12], prev[j][13], prev[j][14], prev[j][15]}};
-    }
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int j = 0; j < P; ++j) {
-        const int c = j * 64 + lane;
-        V4<T> nbs[4], Rn, Lp;
-        rot(prev, j, 0, true, nbs[0]);
-        rot(prev, j, 8, false, nbs[2]);
-        if (j + 1 < P) {
-            rot(prev, j + 1, 0, true, Rn);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) nbs[0].v[i] = lane == 63 ? Rn.v[i] : nbs[0].v[i];
-        }
-        if (j > 0) {
-            rot(prev, j - 1, 8, false, Lp);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) nbs[2].v[i] = lane == 0 ? Lp.v[i] : nbs[2].v[i];
-        }
-        nbs[1] = S1[c + W];
-        nbs[3] = N3[c - W];
-        if (c < geo.HW) {
-            const DkTopo tp = dk_topo(cl, geo, c);
-            T tmp[16];
-            uint32_t pk[4];
-            dk_step<T, true>(tp, cf, prev[j], nbs, tmp, pk);
-            *reinterpret_cast<uint4 *>(pig + c * 16) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                *reinterpret_cast<V4<T> *>(Vg_out + c * 16 + 4 * q) = V4<T>{{own[j][4 * q], own[j][4 * q + 1], own[j][4 * q + 2], own[j][4 * q + 3]}};
         }
     }
 }
