@@ -181,13 +181,8 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
 
 // WP > 0: the one-wave lone-grid variant (fused_wave_xyd), 64 threads, so its WP cells per lane
 // may use the whole register file.
-// MGDP_XN_WPE: minimum waves per SIMD asked of the batched two-cells-per-thread XYD variant (the
-// compiler then caps its VGPRs, spilling what does not fit); 1 = no constraint.
-#ifndef MGDP_XN_WPE
-#define MGDP_XN_WPE 1
-#endif
 template <typename T, int MODEL, bool SLIP, int MAP, int WP = 0>
-__global__ void __launch_bounds__(WP > 0 || wp_is_wave2(WP) ? 64 : 1024) __attribute__((amdgpu_waves_per_eu(WP == -2 ? MGDP_XN_WPE : 1)))
+__global__ void __launch_bounds__(WP > 0 || wp_is_wave2(WP) ? 64 : 1024)
 vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
