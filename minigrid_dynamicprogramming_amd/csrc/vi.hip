@@ -94,6 +94,7 @@ struct mgdp_vi {
     int wave_p = 0;               // lone XYD grid on one wave: cells per lane (fused_wave_xyd)
     int cpt = 1;                  // batched XYD fused path: cells per thread (MGDP_CPT; 2 = fused_fast_xyd_soa_x2)
     int dk1t = 0;                 // batched fp32 DoorKey on one LDS tile (MGDP_DK_1T; fused_fast_dk_1t)
+    int dkhalf = 0;               // batched DoorKey, states split by has_key over two threads (MGDP_DK_HALF; fused_dk_half)
     int pair2 = 1;                // batched plain XYD with cpt 2: adjacent-cell pairs (MGDP_PAIR2=0: fused_fast_xyd_soa_xn)
     int wave2 = 0;                // batched plain XYD on one wave per grid: cells per lane P (fused_wave2_xyd; 0 = off)
     int sweep_block = 256;
@@ -311,6 +312,19 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
     }
     if constexpr (MODEL == MGDP_MODEL_DOORKEY && MAP == MGDP_MAP_CELL && !SLIP) {
         if (vi->dk1t) kern = FusedK<T, MODEL, SLIP, MAP, kWpDk1t>::fn;
+        else if (vi->dkhalf) {
+            switch (vi->HWs / 64) {
+            case 1: kern = FusedK<T, MODEL, SLIP, MAP, kWpDkHalf - 1>::fn; break;
+            case 2: kern = FusedK<T, MODEL, SLIP, MAP, kWpDkHalf - 2>::fn; break;
+            case 3: kern = FusedK<T, MODEL, SLIP, MAP, kWpDkHalf - 3>::fn; break;
+            case 4: kern = FusedK<T, MODEL, SLIP, MAP, kWpDkHalf - 4>::fn; break;
+            case 5: kern = FusedK<T, MODEL, SLIP, MAP, kWpDkHalf - 5>::fn; break;
+            case 6: kern = FusedK<T, MODEL, SLIP, MAP, kWpDkHalf - 6>::fn; break;
+            case 7: kern = FusedK<T, MODEL, SLIP, MAP, kWpDkHalf - 7>::fn; break;
+            case 8: kern = FusedK<T, MODEL, SLIP, MAP, kWpDkHalf - 8>::fn; break;
+            default: return MGDP_E_INVALID;  // excluded at create (HW <= 512)
+            }
+        }
     }
     if constexpr (MAP == MGDP_MAP_CELL) {  // one cell per thread, direction-major: the stripped variant
         if (kern == FusedK<T, MODEL, SLIP, MAP, 0>::fn && !vi->pair && !vi->quad && vi->HW <= vi->fused_block)
@@ -780,6 +794,20 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
             !vi->opts && vi->HW <= vi->fused_block) {
             vi->dk1t = 1;
             vi->nbuf = 1;  // one V tile in LDS
+        }
+        // Batched DoorKey grids of <= 512 cells: each cell's 16 states over two threads split by
+        // has_key (fused_dk_half).  Default for fp64 only: measured on DoorKey-16 x 65536
+        // (profiles/r02_dk_half/), fp64 9.8e12 vs 2.8e12 updates/s (the one-thread-per-cell fp64
+        // loop spills: 138 VGPRs of scratch), fp32 1.89e13 vs 2.23e13 (the same 4 grids per CU,
+        // LDS-bound, with twice the LDS instructions).  MGDP_DK_HALF=0|1 forces it off / on.
+        int dkhalf = d.dtype == MGDP_F64 ? 1 : 0;
+        if (const char *ev = std::getenv("MGDP_DK_HALF")) dkhalf = std::atoi(ev) != 0;
+        if (dkhalf && !vi->dk1t && d.B > 1 && d.model == MGDP_MODEL_DOORKEY && d.method == MGDP_METHOD_FUSED &&
+            !vi->opts && vi->HW <= 512) {
+            vi->dkhalf = 1;
+            vi->HWs = (int)round_up(vi->HW, 64);
+            vi->Ss = vi->S / vi->HW * vi->HWs;
+            vi->fused_block = 2 * vi->HWs;
         }
     } else {
         int blk = d.B == 1 ? 1024 : 256;

@@ -18,6 +18,11 @@ __host__ __device__ constexpr bool wp_is_pair(int wp) { return wp <= kWpPair - 1
 // (fused_wave2_xyd, its own compact LDS layout; vi_fused_kernel only).
 constexpr int kWpWave2 = -400;
 __host__ __device__ constexpr bool wp_is_wave2(int wp) { return wp <= kWpWave2 - 1 && wp >= kWpWave2 - 8; }
+// vi_fused_kernel variant tag: batched DoorKey, a cell's states split over two threads by has_key
+// (fused_dk_half; workgroup = 2 * HWs threads)
+// Tags -501 .. -508: plane stride HWs = 64 * (-tag - 500) known at compile time.
+constexpr int kWpDkHalf = -500;
+__host__ __device__ constexpr bool wp_is_dkhalf(int wp) { return wp <= kWpDkHalf - 1 && wp >= kWpDkHalf - 8; }
 template <typename T, int MODEL> struct TopoOf { using type = XydTopo<T>; };
 template <typename T> struct TopoOf<T, MGDP_MODEL_DOORKEY> { using type = DkTopo; };
 
@@ -67,7 +72,8 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     constexpr bool DK1T = WP == kWpDk1t;
     constexpr bool SOA_ONLY = WP < 0;  // every negative tag runs the direction-major path alone
     constexpr bool PAIR2 = wp_is_pair(WP);
-    constexpr int CPT = PAIR2 ? 2 : (WP < 0 && !DK1T && WP != kWpSoa ? -WP : 1);
+    constexpr bool DKHALF = wp_is_dkhalf(WP);
+    constexpr int CPT = PAIR2 ? 2 : (WP < 0 && !DK1T && !DKHALF && WP != kWpSoa ? -WP : 1);
     const bool fast = MAP == MGDP_MAP_CELL && geo.HW <= CPT * (int)blockDim.x;
     const bool soa = SOA_ONLY || (fast && !geo.pair && !geo.quad);
     if (!SERVED) copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
@@ -113,6 +119,10 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
             constexpr int HWS = 128 * (kWpPair - WP);
             if (k_target < 0) fused_pair_xyd<T, true, HWS>(geo, cf, cl, V0, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
             else fused_pair_xyd<T, false, HWS>(geo, cf, cl, V0, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+        } else if constexpr (MODEL == MGDP_MODEL_DOORKEY && DKHALF) {
+            constexpr int HWS = 64 * (kWpDkHalf - WP);
+            if (k_target < 0) fused_dk_half<T, true, HWS>(geo, cf, cl, V0, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+            else fused_dk_half<T, false, HWS>(geo, cf, cl, V0, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
         } else if constexpr (MODEL == MGDP_MODEL_DOORKEY && DK1T) {
             if (k_target < 0) fused_fast_dk_1t<T, true>(geo, cf, cl, V0, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
             else fused_fast_dk_1t<T, false>(geo, cf, cl, V0, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);

@@ -935,6 +935,212 @@ __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> 
     }
 }
 
+// Batched DoorKey grids with each cell's 16 states split over two threads by has_key: the first
+// HWs threads (whole waves) own (cell, has_key 0), the next HWs threads (cell, has_key 1), 8 states
+// (dir, door_open) each.  Per thread that halves the values held per register set (own, the next
+// sweep's, the four front pairs), which is what capped fused_fast_dk_soa at 4 waves per SIMD
+// (107 VGPRs); the workgroup doubles to 2*HWs threads.  has_key is wave-uniform, so the half's
+// transition form is a uniform branch.  Only pickup (has_key 0, key ahead -> the same (dir,
+// door_open) with has_key 1) crosses the halves: it reads the other half's values of its own cell
+// from the input tile (same bits as that thread's registers), only in waves with a key / door.
+// LDS tiles: value (x, d, hk, dop) at ((hk*4 + d)*HWs + x)*2 + dop, so a thread's front pair and
+// own pairs are unit-stride 8-B accesses.  Same candidates per state as dk_step_fast / dk_step
+// (max is exact and order-free; the pi pass keeps dk_step's action order), so V, pi and the
+// stopping sweep are bit-identical.
+struct DkHalf {
+    uint32_t walk;  // as DkTopo
+    uint32_t fp;    // byte d: DkFast::f[d] (goal / key / door ahead), packed to save registers
+    int nb[4];      // LDS index of the front pair forward reads (cell 0's when none)
+};
+template <typename T, bool HK0, bool FH, bool GOAL, bool KD>
+__device__ __forceinline__ T dkh_step_fast(const DkHalf &tp, const Coef<T> &cf, const T (&own)[8], const T (&oth)[8],
+                                           const V2<T> (&nbs)[4], T (&outv)[8], T rg = (T)1) {
+    constexpr int hk = HK0 ? 0 : 1;
+    T dv = (T)0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t f = tp.fp >> (8 * d);
+        const bool key = f & 64u, door = f & 128u;
+        const T tqd = (f & 16u) ? (FH ? rg : (T)1) : (T)0;
+#pragma unroll
+        for (int dop = 0; dop < 2; ++dop) {
+            const int hd = hk * 2 + dop, l = d * 2 + dop;
+            const T xS = own[l];
+            T M = vmax(vmax(own[((d + 3) & 3) * 2 + dop], own[((d + 1) & 3) * 2 + dop]), vmax(xS, nbs[d].v[dop]));
+            if (KD) {  // pickup -> (d, 1, dop); toggle -> close (dop 1: (d, hk, 0)) / unlock (hk 1, dop 0: (d, 1, 1))
+                T cand = (T)0;
+                if (!hk) cand = key ? oth[l] : cand;
+                if (dop) cand = door ? own[d * 2] : cand;
+                else if (hk) cand = door ? own[d * 2 + 1] : cand;
+                M = vmax(M, cand);
+            }
+            T best = cf.g * M;
+            if (GOAL) best = vmax(best, tqd);
+            if (KD) best = ((tp.walk >> hd) & 1u) ? best : (T)0;
+            outv[l] = best;
+            dv = vmax(dv, vabs(best - xS));  // running max: two live temporaries, not eight
+        }
+    }
+    return dv;
+}
+
+// pi of one half (dk_step's WRITE_PI form restricted to has_key = hk): pk[d] = the 2 lanes' bytes
+template <typename T>
+__device__ __forceinline__ void dkh_pi(const DkTopo &tp, const Coef<T> &cf, int hk, const T (&own)[8], const T (&oth)[8],
+                                       const V2<T> (&nbs)[4], uint32_t (&pk)[4]) {
+    T gv[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) gv[l] = cf.g * own[l];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t f = tp.f[d];
+        const bool goal = f & 16u, lava = f & 32u, key = f & 64u, door = f & 128u;
+        pk[d] = 0;
+#pragma unroll
+        for (int dop = 0; dop < 2; ++dop) {
+            const int l = d * 2 + dop, hd = hk * 2 + dop;
+            const T qS = gv[l];
+            const T qL = gv[((d + 3) & 3) * 2 + dop];
+            const T qR = gv[((d + 1) & 3) * 2 + dop];
+            const T qM = ((f >> hd) & 1u) ? cf.g * nbs[d].v[dop] : qS;
+            const T qF = goal ? (T)1 : (lava ? (T)0 : qM);
+            const T qP = (!hk && key) ? cf.g * oth[l] : qS;
+            const T qD = dop ? gv[d * 2] : (hk ? gv[d * 2 + 1] : qS);
+            const T qT = door ? qD : qS;
+            T best = qL;
+            int arg = 0;
+            if (qR > best) { best = qR; arg = 1; }
+            if (qF > best) { best = qF; arg = 2; }
+            if (qP > best) { best = qP; arg = 3; }
+            if (qT > best) { best = qT; arg = 4; }
+            const bool valid = (tp.walk >> hd) & 1u;
+            pk[d] |= (uint32_t)(uint8_t)(valid ? arg : -1) << (8 * dop);
+        }
+    }
+}
+
+// HW: the plane stride geo.HWs (a multiple of 64, so has_key is uniform per wave) known at compile
+// time: every tile / plane offset is an instruction immediate, and a thread keeps one LDS address
+// per front cell instead of one per (tile, plane) pair.
+template <typename T, bool LOCAL, int HW, typename Done>
+__device__ __forceinline__ void fused_dk_half(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *V0,
+                                              T *slots, uint8_t *flags, const T *Vg, T *Vg_out, int8_t *pig, int &k,
+                                              int k_target, double &dvl, const Done &done) {
+    T *V1 = V0 + 16 * HW;  // = smem_layout's second tile (Ss = 16 * HWs)
+    const int hk = (int)threadIdx.x >= HW ? 1 : 0;
+    const int c = threadIdx.x - hk * HW;
+    const int cc = c < geo.HW ? c : 0;
+    const bool own_cell = c < geo.HW;
+    const int k_start = k;
+    auto tix = [&](int x, int d, int h) { return ((h * 4 + d) * HW + x) * 2; };
+    DkHalf tpf;  // front pair read by forward (cell 0's when none; see dk_fast_topo)
+    uint32_t cls;
+    {
+    const DkTopo tp = dk_topo(cl, geo, cc);  // (resolved again for the pi pass: fewer live registers)
+    DkFast q;
+    q.walk = tpf.walk = tp.walk;
+    tpf.fp = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t f = tp.f[d];
+        const bool reads = tp.walk != 0u && !(f & 48u) && (f & 15u) != 0u;
+        tpf.nb[d] = tix(reads ? (tp.nb[d] >> 4) : 0, d, hk);
+        q.f[d] = tp.walk != 0u ? (f & (16u | 64u | 128u)) : 0u;
+        tpf.fp |= q.f[d] << (8 * d);
+    }
+    cls = dk_fast_class(q);
+    }
+    const uint32_t wcls = (__builtin_amdgcn_ballot_w64(cls & 1u) ? 1u : 0u) | (__builtin_amdgcn_ballot_w64(cls & 2u) ? 2u : 0u);
+    T own[8];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const V2<T> x = k == 0 ? V2<T>{{(T)0, (T)0}} : *reinterpret_cast<const V2<T> *>(Vg + cc * 16 + d * 4 + hk * 2);
+        own[2 * d] = x.v[0];
+        own[2 * d + 1] = x.v[1];
+        *reinterpret_cast<V2<T> *>(V0 + tix(c, d, hk)) = x;
+    }
+    __syncthreads();
+    int cur = 0, parity = 0;
+    T diff = (T)0;
+    auto sweep = [&](const T *Vin, T *Vout, const T (&in)[8], T (&outv)[8]) -> bool {
+        if (LOCAL ? k >= geo.max_sweeps : k >= k_target) return false;
+        uint4 fl = make_uint4(0u, 0u, 0u, 0u);
+        if (LOCAL) fl = *reinterpret_cast<const uint4 *>(flags + (parity ^ 1) * 16);
+        V2<T> nbs[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) nbs[d] = *reinterpret_cast<const V2<T> *>(Vin + tpf.nb[d]);
+        T d;
+        if (wcls == 0u) {
+            const T (&none)[8] = in;  // unused without KD
+            d = hk ? dkh_step_fast<T, false, false, false, false>(tpf, cf, in, none, nbs, outv)
+                   : dkh_step_fast<T, true, false, false, false>(tpf, cf, in, none, nbs, outv);
+        } else if (wcls == 1u) {
+            const T (&none)[8] = in;
+            d = hk ? dkh_step_fast<T, false, false, true, false>(tpf, cf, in, none, nbs, outv)
+                   : dkh_step_fast<T, true, false, true, false>(tpf, cf, in, none, nbs, outv);
+        } else if (hk) {
+            d = dkh_step_fast<T, false, false, true, true>(tpf, cf, in, in, nbs, outv);
+        } else {
+            T oth[8];  // the has_key-1 half's V_k of this cell (pickup)
+#pragma unroll
+            for (int dd = 0; dd < 4; ++dd) {
+                const V2<T> x = *reinterpret_cast<const V2<T> *>(Vin + tix(c, dd, 1));
+                oth[2 * dd] = x.v[0];
+                oth[2 * dd + 1] = x.v[1];
+            }
+            d = dkh_step_fast<T, true, false, true, true>(tpf, cf, in, oth, nbs, outv);
+        }
+        if (LOCAL) {
+            asm volatile("" ::"v"(d));  // keep the arithmetic ahead of the test (no sinking past it)
+            if (k > k_start && (fl.x | fl.y | fl.z | fl.w) == 0u) return false;
+        }
+        diff = d;
+#pragma unroll
+        for (int dd = 0; dd < 4; ++dd)
+            *reinterpret_cast<V2<T> *>(Vout + tix(c, dd, hk)) = V2<T>{{outv[2 * dd], outv[2 * dd + 1]}};
+        if (LOCAL) flag_write(diff >= cf.tol, flags, parity);
+        __syncthreads();
+        parity ^= 1;
+        ++k;
+        return true;
+    };
+    T alt[8];
+    while (true) {
+        if (!sweep(V0, V1, own, alt)) { cur = 0; break; }
+        if (!sweep(V1, V0, alt, own)) {
+            cur = 1;
+#pragma unroll
+            for (int l = 0; l < 8; ++l) own[l] = alt[l];
+            break;
+        }
+    }
+    dvl = (double)block_max(diff, slots, 0);
+    done(k, dvl);
+    if (own_cell) {  // V_k (`own`) out first (frees its registers), then pi on V_{k-1} (buffer cur ^ 1)
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+            *reinterpret_cast<V2<T> *>(Vg_out + c * 16 + d * 4 + hk * 2) = V2<T>{{own[2 * d], own[2 * d + 1]}};
+        const DkTopo tp = dk_topo(cl, geo, cc);
+        const T *Vp = cur ? V0 : V1;
+        T op[8], oth[8];
+        V2<T> nbs[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const V2<T> x = *reinterpret_cast<const V2<T> *>(Vp + tix(c, d, hk));
+            const V2<T> y = *reinterpret_cast<const V2<T> *>(Vp + tix(c, d, 1));
+            op[2 * d] = x.v[0];
+            op[2 * d + 1] = x.v[1];
+            oth[2 * d] = y.v[0];
+            oth[2 * d + 1] = y.v[1];
+            nbs[d] = *reinterpret_cast<const V2<T> *>(Vp + tix(tp.nb[d] >> 4, d, hk));
+        }
+        uint32_t pk[4];
+        dkh_pi<T>(tp, cf, hk, op, oth, nbs, pk);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) *reinterpret_cast<uint16_t *>(pig + c * 16 + d * 4 + hk * 2) = (uint16_t)pk[d];
+    }
+}
+
 // Batched DoorKey grids on ONE LDS tile (fp32): the two 16 KB tiles of fused_fast_dk_soa cap a CU
 // at 4 resident 16x16 grids, one tile at 8.  A sweep reads the neighbours' V_k from the tile,
 // passes a barrier (every read is done), tests the previous sweep's stop flags (read before the

@@ -28,6 +28,10 @@ template <typename T>
 struct alignas(4 * sizeof(T)) V4 {
     T v[4];
 };
+template <typename T>
+struct alignas(2 * sizeof(T)) V2 {
+    T v[2];
+};
 
 __device__ __forceinline__ bool xyd_free(int t) { return t == T_EMPTY || t == T_FLOOR; }
 __device__ __forceinline__ bool dk_walk(int t, int hk, int dop) {
