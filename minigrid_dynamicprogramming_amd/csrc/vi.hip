@@ -280,6 +280,21 @@ F pick_wave2(int P, F dflt) {
 }
 template <typename T, int MODEL, bool SLIP, int MAP, int WP>
 struct ServeK { static constexpr auto fn = vi_serve_kernel<T, MODEL, SLIP, MAP, WP>; };
+// fused_dk_half variants by plane stride HWs = 64 * n (the host allows n <= 8)
+template <template <typename, int, bool, int, int> class K, typename T, int MODEL, bool SLIP, int MAP, typename F>
+F pick_dkhalf(int n, F dflt) {
+    switch (n) {
+    case 1: return K<T, MODEL, SLIP, MAP, kWpDkHalf - 1>::fn;
+    case 2: return K<T, MODEL, SLIP, MAP, kWpDkHalf - 2>::fn;
+    case 3: return K<T, MODEL, SLIP, MAP, kWpDkHalf - 3>::fn;
+    case 4: return K<T, MODEL, SLIP, MAP, kWpDkHalf - 4>::fn;
+    case 5: return K<T, MODEL, SLIP, MAP, kWpDkHalf - 5>::fn;
+    case 6: return K<T, MODEL, SLIP, MAP, kWpDkHalf - 6>::fn;
+    case 7: return K<T, MODEL, SLIP, MAP, kWpDkHalf - 7>::fn;
+    case 8: return K<T, MODEL, SLIP, MAP, kWpDkHalf - 8>::fn;
+    default: return dflt;
+    }
+}
 
 // pub: where the launch's {kmax, dV bits, kmin, epoch} go (default: the host-mapped words the host
 // polls; the multi-GPU device protocol passes a device buffer it all-reduces); k_dev: the target
@@ -312,19 +327,7 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
     }
     if constexpr (MODEL == MGDP_MODEL_DOORKEY && MAP == MGDP_MAP_CELL && !SLIP) {
         if (vi->dk1t) kern = FusedK<T, MODEL, SLIP, MAP, kWpDk1t>::fn;
-        else if (vi->dkhalf) {
-            switch (vi->HWs / 64) {
-            case 1: kern = FusedK<T, MODEL, SLIP, MAP, kWpDkHalf - 1>::fn; break;
-            case 2: kern = FusedK<T, MODEL, SLIP, MAP, kWpDkHalf - 2>::fn; break;
-            case 3: kern = FusedK<T, MODEL, SLIP, MAP, kWpDkHalf - 3>::fn; break;
-            case 4: kern = FusedK<T, MODEL, SLIP, MAP, kWpDkHalf - 4>::fn; break;
-            case 5: kern = FusedK<T, MODEL, SLIP, MAP, kWpDkHalf - 5>::fn; break;
-            case 6: kern = FusedK<T, MODEL, SLIP, MAP, kWpDkHalf - 6>::fn; break;
-            case 7: kern = FusedK<T, MODEL, SLIP, MAP, kWpDkHalf - 7>::fn; break;
-            case 8: kern = FusedK<T, MODEL, SLIP, MAP, kWpDkHalf - 8>::fn; break;
-            default: return MGDP_E_INVALID;  // excluded at create (HW <= 512)
-            }
-        }
+        else if (vi->dkhalf) kern = pick_dkhalf<FusedK, T, MODEL, SLIP, MAP>(vi->HWs / 64, kern);
     }
     if constexpr (MAP == MGDP_MAP_CELL) {  // one cell per thread, direction-major: the stripped variant
         if (kern == FusedK<T, MODEL, SLIP, MAP, 0>::fn && !vi->pair && !vi->quad && vi->HW <= vi->fused_block)
@@ -362,6 +365,9 @@ int launch_serve_t(mgdp_vi *vi, unsigned int served) {
     int smem = L.total();
     if constexpr (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL) {
         if (vi->cpt == 2) kern = ServeK<T, MODEL, SLIP, MAP, -2>::fn;
+    }
+    if constexpr (MODEL == MGDP_MODEL_DOORKEY && MAP == MGDP_MAP_CELL && !SLIP) {
+        if (vi->dkhalf) kern = pick_dkhalf<ServeK, T, MODEL, SLIP, MAP>(vi->HWs / 64, kern);
     }
     if (smem > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
     TimedPair tp;
@@ -796,13 +802,14 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
             vi->nbuf = 1;  // one V tile in LDS
         }
         // Batched DoorKey grids of <= 512 cells: each cell's 16 states over two threads split by
-        // has_key (fused_dk_half).  Default for fp64 only: measured on DoorKey-16 x 65536
-        // (profiles/r02_dk_half/), fp64 9.8e12 vs 2.8e12 updates/s (the one-thread-per-cell fp64
-        // loop spills: 138 VGPRs of scratch), fp32 1.89e13 vs 2.23e13 (the same 4 grids per CU,
-        // LDS-bound, with twice the LDS instructions).  MGDP_DK_HALF=0|1 forces it off / on.
-        int dkhalf = d.dtype == MGDP_F64 ? 1 : 0;
+        // has_key (fused_dk_half).  Default for fp64 and for lone grids: measured on DoorKey-16
+        // (profiles/r02_dk_half/), x 65536 fp64 9.9e12 vs 2.8e12 updates/s (the one-thread-per-cell
+        // fp64 loop spills: 138 VGPRs of scratch) but fp32 1.90e13 vs 2.22e13 (the same 4 grids per
+        // CU, LDS-bound, with twice the LDS instructions); a lone grid, served: fp32 26.1 vs
+        // 28.4 us, fp64 34.8 vs 85.0 us per solve.  MGDP_DK_HALF=0|1 forces it off / on.
+        int dkhalf = (d.dtype == MGDP_F64 || d.B == 1) ? 1 : 0;
         if (const char *ev = std::getenv("MGDP_DK_HALF")) dkhalf = std::atoi(ev) != 0;
-        if (dkhalf && !vi->dk1t && d.B > 1 && d.model == MGDP_MODEL_DOORKEY && d.method == MGDP_METHOD_FUSED &&
+        if (dkhalf && !vi->dk1t && d.model == MGDP_MODEL_DOORKEY && d.method == MGDP_METHOD_FUSED &&
             !vi->opts && vi->HW <= 512) {
             vi->dkhalf = 1;
             vi->HWs = (int)round_up(vi->HW, 64);

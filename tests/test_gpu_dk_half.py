@@ -72,3 +72,27 @@ def test_dk_half_protocol_continuation(monkeypatch):
         np.testing.assert_array_equal(vi.policy(), o["pi"])
     finally:
         vi.close()
+
+
+@pytest.mark.parametrize("persistent", ["0", "1"])
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_dk_half_lone_grid_served_and_launched(persistent, dtype, monkeypatch):
+    # a lone grid on the split loop: the resident server (grid per request included) or one launch
+    monkeypatch.setenv("MGDP_PERSISTENT", persistent)
+    monkeypatch.setenv("MGDP_DK_HALF", "1")
+    for size in (6, 16, 22):
+        cells = doorkey_cells(size, 4, seed0=100 + size)
+        vi = mg.ValueIteration(cells[:1], model="doorkey", dtype=dtype)
+        try:
+            assert vi.persistent == (persistent == "1")
+            for i in range(len(cells)):
+                vi.load(cells[i:i + 1])
+                k = vi.solve()
+                o = oracle.value_iteration(1, cells[i:i + 1], dtype=dtype)
+                assert k == o["sweeps"]
+                if i % 2:
+                    r = vi.result()
+                    np.testing.assert_array_equal(r.V, o["V"])
+                    np.testing.assert_array_equal(r.pi, o["pi"])
+        finally:
+            vi.close()
