@@ -399,12 +399,37 @@ vi_reduce_kernel(const int32_t *__restrict__ kenv, const double *__restrict__ dv
                  unsigned long long *__restrict__ host_out, unsigned int epoch) {
     __shared__ unsigned long long sk[16], sd[16], sn[16];
     unsigned long long km = 0, dm = 0, kn = 0x7fffffffull;
-    for (int i = threadIdx.x; i < B; i += blockDim.x) {
-        const unsigned long long k = (unsigned long long)kenv[i];
-        km = max(km, k);
-        kn = min(kn, k);
-        dm = max(dm, (unsigned long long)__double_as_longlong(dvenv[i]));
+    auto fold = [&](int k, double d) {
+        km = max(km, (unsigned long long)k);
+        kn = min(kn, (unsigned long long)k);
+        dm = max(dm, (unsigned long long)__double_as_longlong(d));
+    };
+    // 16-B loads, U of them in flight per thread before any is folded: one workgroup streaming
+    // 12 B per grid is latency-bound (the one-load-per-iteration loop took 24 us for 65536 grids)
+    constexpr int U = 4;
+    const int B4 = B / 4;  // kenv / dvenv come from hipMalloc: 16-B aligned
+    const int4 *k4 = reinterpret_cast<const int4 *>(kenv);
+    const double2 *d2 = reinterpret_cast<const double2 *>(dvenv);
+    const int step = (int)blockDim.x;
+    for (int base = threadIdx.x; base < B4; base += U * step) {
+        int4 kk[U];
+        double2 da[U], db[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = min(base + u * step, B4 - 1);  // clamped re-reads are harmless for max/min
+            kk[u] = k4[i];
+            da[u] = d2[2 * i];
+            db[u] = d2[2 * i + 1];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            fold(kk[u].x, da[u].x);
+            fold(kk[u].y, da[u].y);
+            fold(kk[u].z, db[u].x);
+            fold(kk[u].w, db[u].y);
+        }
     }
+    for (int i = 4 * B4 + (int)threadIdx.x; i < B; i += step) fold(kenv[i], dvenv[i]);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         km = max(km, (unsigned long long)__shfl_xor(km, o));
