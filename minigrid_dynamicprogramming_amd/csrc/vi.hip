@@ -68,6 +68,7 @@ struct mgdp_vi {
     bool chain = true;                      // batched fused solve: run_local -> run_to(K from device memory), one host wait (MGDP_CHAIN=0: two)
     int inkernel_max = kInKernelReduceMaxB; // batches up to this fold {k, dV} in the fused launch itself (MGDP_INKERNEL_MAX)
     unsigned int *d_ticket = nullptr;       // arrival ticket of the fused reduction
+    bool reduce_multi = true;               // B > inkernel_max: vi_reduce_multi_kernel (MGDP_REDUCE_MULTI)
     unsigned long long *h_out = nullptr;    // host-mapped {kmax, dV bits, kmin, epoch, request}
     unsigned long long *d_hout = nullptr;   // device alias of h_out
     int cur = 0;        // V buffer holding the current V (sweep method)
@@ -200,6 +201,17 @@ int timed_collect(mgdp_vi *vi) {
     return 0;
 }
 
+// {kmax, dV, kmin} of a launch too large to reduce in itself: kRedShards workgroups on the
+// fused reduction's idle shards (MGDP_REDUCE_MULTI=0: the one-workgroup kernel)
+inline void launch_reduce(mgdp_vi *vi, unsigned long long *pub) {
+    if (vi->reduce_multi)
+        hipLaunchKernelGGL(vi_reduce_multi_kernel, dim3(kRedShards), dim3(256), 0, vi->stream, vi->d_kenv, vi->d_dvenv,
+                           vi->d.B, vi->d_red, vi->d_ticket, pub, vi->epoch);
+    else
+        hipLaunchKernelGGL(vi_reduce_kernel, dim3(1), dim3(1024), 0, vi->stream, vi->d_kenv, vi->d_dvenv, vi->d.B,
+                           pub, vi->epoch);
+}
+
 template <typename T, int MODEL, bool SLIP, bool ND, int HMODE>
 int launch_opts_t(mgdp_vi *vi, int k_target) {
     const Geo g = make_geo(vi);
@@ -215,8 +227,7 @@ int launch_opts_t(mgdp_vi *vi, int k_target) {
     MGDP_HIP(hipGetLastError());
     vi->fresh = 0;
     if (vi->d.B > vi->inkernel_max) {
-        hipLaunchKernelGGL(vi_reduce_kernel, dim3(1), dim3(1024), 0, vi->stream, vi->d_kenv, vi->d_dvenv, vi->d.B,
-                           vi->d_hout, vi->epoch);
+        launch_reduce(vi, vi->d_hout);
         MGDP_HIP(hipGetLastError());
     }
     return 0;
@@ -350,8 +361,7 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
     MGDP_HIP(hipGetLastError());
     vi->fresh = 0;
     if (vi->d.B > vi->inkernel_max) {
-        hipLaunchKernelGGL(vi_reduce_kernel, dim3(1), dim3(1024), 0, vi->stream, vi->d_kenv, vi->d_dvenv, vi->d.B,
-                           pub, vi->epoch);
+        launch_reduce(vi, pub);
         MGDP_HIP(hipGetLastError());
     }
     return 0;
@@ -866,6 +876,7 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     if (const char *ev = std::getenv("MGDP_SWEEP_BLOCK")) vi->sweep_block = std::min(256, std::max(64, std::atoi(ev) / 64 * 64));
     if (const char *ev = std::getenv("MGDP_PERSISTENT")) vi->persistent = std::atoi(ev) != 0;
     if (const char *ev = std::getenv("MGDP_CHAIN")) vi->chain = std::atoi(ev) != 0;
+    if (const char *ev = std::getenv("MGDP_REDUCE_MULTI")) vi->reduce_multi = std::atoi(ev) != 0;
     if (const char *ev = std::getenv("MGDP_INKERNEL_MAX")) vi->inkernel_max = std::max(0, std::atoi(ev));
     // DoorKey (64-128 B of V per thread) measured slower on the register pipeline (5.38 -> 3.3 TB/s
     // compulsory: the prefetch registers collide with the 16-state backup's), so it keeps the

@@ -444,6 +444,83 @@ vi_reduce_kernel(const int32_t *__restrict__ kenv, const double *__restrict__ dv
     }
 }
 
+// The same reduction over kRedShards workgroups (one shard each, so no two workgroups share an
+// atomic address), the last arrival folding the shards and publishing -- fused_reduce's protocol,
+// whose shards and ticket are idle when the fused launch does not reduce (B > inkernel_max).
+__global__ void __launch_bounds__(256)
+vi_reduce_multi_kernel(const int32_t *__restrict__ kenv, const double *__restrict__ dvenv, int B,
+                       unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
+                       unsigned long long *__restrict__ host_out, unsigned int epoch) {
+    __shared__ unsigned long long sk[4], sd[4], sn[4];
+    __shared__ unsigned int last;
+    unsigned long long km = 0, dm = 0, kn = 0x7fffffffull;
+    auto fold = [&](int k, double d) {
+        km = max(km, (unsigned long long)k);
+        kn = min(kn, (unsigned long long)k);
+        dm = max(dm, (unsigned long long)__double_as_longlong(d));
+    };
+    constexpr int U = 4;
+    const int B4 = B / 4;
+    const int4 *k4 = reinterpret_cast<const int4 *>(kenv);
+    const double2 *d2 = reinterpret_cast<const double2 *>(dvenv);
+    const int step = (int)(blockDim.x * gridDim.x);
+    for (int base = (int)(blockIdx.x * blockDim.x + threadIdx.x); base < B4; base += U * step) {
+        int4 kk[U];
+        double2 da[U], db[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = min(base + u * step, B4 - 1);  // clamped re-reads are harmless for max/min
+            kk[u] = k4[i];
+            da[u] = d2[2 * i];
+            db[u] = d2[2 * i + 1];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            fold(kk[u].x, da[u].x);
+            fold(kk[u].y, da[u].y);
+            fold(kk[u].z, db[u].x);
+            fold(kk[u].w, db[u].y);
+        }
+    }
+    if (blockIdx.x == 0)
+        for (int i = 4 * B4 + (int)threadIdx.x; i < B; i += (int)blockDim.x) fold(kenv[i], dvenv[i]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        km = max(km, (unsigned long long)__shfl_xor(km, o));
+        dm = max(dm, (unsigned long long)__shfl_xor(dm, o));
+        kn = min(kn, (unsigned long long)__shfl_xor(kn, o));
+    }
+    if ((threadIdx.x & 63) == 0) { sk[threadIdx.x >> 6] = km; sd[threadIdx.x >> 6] = dm; sn[threadIdx.x >> 6] = kn; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < (int)(blockDim.x >> 6); ++i) { km = max(km, sk[i]); dm = max(dm, sd[i]); kn = min(kn, sn[i]); }
+        unsigned long long *r = red + (blockIdx.x & (kRedShards - 1)) * 4;
+        const unsigned long long a = __hip_atomic_fetch_max(r + 0, km, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long b = __hip_atomic_fetch_max(r + 1, dm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long c = __hip_atomic_fetch_min(r + 2, kn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" :: "v"(a), "v"(b), "v"(c) : "memory");
+        const unsigned int t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = t == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && threadIdx.x < 64) {  // every shard's updates returned before its ticket add
+        unsigned long long *r = red + threadIdx.x * 4;
+        unsigned long long x = __hip_atomic_exchange(r + 0, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long y = __hip_atomic_exchange(r + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long z = __hip_atomic_exchange(r + 2, 0x7fffffffull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            x = max(x, (unsigned long long)__shfl_xor(x, o));
+            y = max(y, (unsigned long long)__shfl_xor(y, o));
+            z = min(z, (unsigned long long)__shfl_xor(z, o));
+        }
+        if (threadIdx.x == 0) {
+            __hip_atomic_exchange(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            publish(host_out, x, y, z, epoch);
+        }
+    }
+}
+
 // Early exit of a speculatively enqueued sweep: the previous sweep already met the rule.
 __device__ __forceinline__ bool prev_sweep_converged(const unsigned long long *shards, int k, double tol) {
     if (k <= 1) return false;
