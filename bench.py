@@ -20,7 +20,12 @@ Side paths (measured to the same bar; their own metric, no
                  batched reset(seed) grid generation (csrc/gen.hip), 65536 seeds per GPU, grids/s
 
 Run:  python bench.py [--gpus N --steps K --warmup W --workload NAME --method fused|sweep ...]
-      N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+      N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N, or plain
+      `python bench.py --gpus N`, which starts the N ranks itself (torch.distributed.run as a child
+      process, before any GPU call) and exits with its status.
+The line of the default workload also carries a "sharded" block per BASELINE multi-GPU config
+(lava65536, doorkey65536): the global batch sharded over the N ranks (at N = 1 the direct solve),
+updates/s over the whole job, ms per solve, sweeps, and at N > 1 the collectives per solve.
 """
 from __future__ import annotations
 
@@ -161,9 +166,12 @@ def cpu_baseline(cells, model, gamma, tol, dtype, budget_s=8.0, nthreads=1, lone
                       f"oracle/mgdp_oracle.c, {el:.1f} s"}
 
 
-def load_traffic(key, solves_per_launch):
+def load_traffic(key, solves_per_launch, grids=None):
     """HBM bytes per launch from the committed PMC passes (tools/pmc_traffic.sh).  A persistent
-    server launch serves many solves: its entry is per solve, scaled to this launch's solves."""
+    server launch serves many solves: its entry is per solve, scaled to this launch's solves.  A
+    batched entry was measured on `grids_per_launch` grids: a rank launching `grids` of them (a
+    shard of the global batch) moves grids / grids_per_launch of those bytes (None when the entry
+    does not say how many grids it measured)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
@@ -174,10 +182,125 @@ def load_traffic(key, solves_per_launch):
         return None
     if "bytes_per_solve" in v:
         return v["bytes_per_solve"] * solves_per_launch
-    return v.get("bytes_per_launch")
+    b = v.get("bytes_per_launch")
+    measured = v.get("grids_per_launch")
+    if grids is not None and b is not None:
+        if not measured:
+            return None
+        b = b * grids / measured
+    return b
+
+
+def self_launch(argv) -> int:
+    """`--gpus N > 1` without a torch.distributed environment: start the N ranks as a child
+    `torch.distributed.run` (one process per GPU, rendezvous on 127.0.0.1) -- before this process
+    touches the GPU, and never as an exec -- and return its exit status (non-zero if any rank
+    failed).  Rank 0's JSON line reaches stdout through the inherited file descriptor."""
+    import socket
+    import subprocess
+
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    n = ap.parse_known_args(argv)[0].gpus
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    log(f"bench: --gpus {n} without WORLD_SIZE: launching {n} ranks: {' '.join(cmd)}")
+    return subprocess.run(cmd).returncode
+
+
+def dry_run(args, rank, world):
+    """MGDP_BENCH_DRYRUN=1 (tests/test_bench_launch.py, CPU only): the rank plumbing of a multi-GPU
+    run without a GPU -- gloo group, barrier, max-over-ranks of a fake region, rank 0's line.
+    MGDP_BENCH_DRYRUN_FAIL_RANK=r makes rank r fail, to check the launcher's exit status."""
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    if int(os.environ.get("MGDP_BENCH_DRYRUN_FAIL_RANK", "-1")) == rank:
+        log(f"[rank {rank}] dry run: failing on purpose")
+        sys.exit(3)
+    t = torch.tensor([0.001 * (rank + 1)], dtype=torch.float64)
+    if world > 1:
+        dist.barrier()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "dry_run": True, "elapsed_max": float(t.item()),
+                          "ranks": [int(os.environ.get("RANK", "0")), world]}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def workload_roofline(args, dtype, m, workload, grids):
+    """The roofline object of a measured workload: SURVEY 8(d) algorithmic bytes per launch / the
+    dominant kernel's average launch time (HIP events), compulsory bytes, and the committed PMC
+    traffic scaled to this rank's `grids`."""
+    vi_info = m["info"]
+    A = vi_info["A"]
+    tsize = 4 if dtype == "f32" else 8
+    bpu = algorithmic_bytes_per_update(tsize, A)
+    launches = m["launches"]
+    avg_launch_s = (m["kern_ms"] / 1000.0) / max(launches, 1)
+    # solves inside the timed launches: the K timed solves plus the priming solves a resident
+    # server's launch also spans
+    solves_in_launches = args.steps + m["primed"]
+    upd_per_solve = float(vi_info["updates_per_sweep"]) * float(np.mean(m["sweeps"]))
+    alg_bytes_launch = upd_per_solve * solves_in_launches * bpu / max(launches, 1)
+    achieved = alg_bytes_launch / avg_launch_s / 1e9 if launches else 0.0
+    comp_launch = compulsory_bytes_per_solve(vi_info, tsize, args.method, m["sweeps"][-1]) * solves_in_launches / max(launches, 1)
+    key = f"{workload}/{args.method}/{args.mapping}/{dtype}"
+    traffic = load_traffic(key, solves_in_launches / max(launches, 1), grids=None if vi_info["persistent"] else grids)
+    roofline = {
+        "bound": "hbm", "kernel": vi_info["kernel"],
+        "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+        "traffic": traffic, "launches": launches, "avg_launch_us": avg_launch_s * 1e6,
+        "alg_bytes_per_launch": alg_bytes_launch, "alg_bytes_per_update": bpu,
+        "solves_per_launch": solves_in_launches / max(launches, 1),
+        "compulsory_bytes_per_launch": comp_launch,
+        "compulsory_frac": comp_launch / max(avg_launch_s, 1e-30) / 1e9 / HBM_PEAK_GBS,
+        "note": ("achieved = SURVEY 8(d) algorithmic bytes (sizeof V + 1 + sizeof V / A per (s,a) update) per launch "
+                 "/ the launch's HIP-event duration; compulsory = the bytes this kernel must move per launch "
+                 "(fused/served: cells in + V and pi out once per solve, spread over the solve's launches; sweep: "
+                 "2*S*sizeof V + W*H per grid-sweep); traffic = PMC HBM bytes per launch (profiles/pmc_traffic.json), "
+                 "scaled to this rank's grids"),
+    }
+    sq = load_sq(f"{key}/{vi_info['kernel']}")
+    if sq and sq.get("valu_insts_per_launch") and launches and not vi_info["persistent"]:
+        # the batched fused kernel keeps V in LDS: its limits are issue / LDS / latency, not HBM
+        scale = grids / sq["grids_per_launch"] if sq.get("grids_per_launch") else 1.0
+        lane_ops = sq["valu_insts_per_launch"] * scale * 64.0 / avg_launch_s
+        roofline["valu"] = {"achieved": lane_ops, "peak": VALU_PEAK_LANE_OPS, "unit": "lane-ops/s",
+                            "frac": lane_ops / VALU_PEAK_LANE_OPS, "lds_array_busy": sq.get("lds_array_busy"),
+                            "wave_split": sq.get("wave_split"), "source": sq.get("source")}
+    if workload == "empty16":
+        roofline["regime"] = ("single 4 KiB V grid on one resident workgroup: latency bound (barrier + LDS round trip "
+                              "per sweep, host hand-off per solve); HBM is not the limit here (SURVEY 8(d) "
+                              "caveats); see roofline_hbm for the kernels at the HBM-sized config R")
+    if vi_info["persistent"]:
+        roofline["launch_note"] = ("lone grid: one resident vi_serve_kernel launch serves the priming solves and every "
+                                   "timed solve (host posts a request word, the workgroup solves and publishes), so "
+                                   "its duration spans the timed region")
+    if roofline["frac"] > 1.0:  # LDS-served gathers: the algorithmic figure is not an HBM rate
+        roofline["alg_equiv_gbs"] = achieved
+        meas = traffic if traffic else comp_launch
+        roofline["achieved"] = meas / avg_launch_s / 1e9
+        roofline["frac"] = roofline["achieved"] / HBM_PEAK_GBS
+        roofline["achieved_basis"] = "pmc traffic" if traffic else "compulsory bytes"
+    return roofline
 
 
 def main():
+    if int(os.environ.get("WORLD_SIZE", "0") or 0) == 0:
+        ap0 = argparse.ArgumentParser(add_help=False)
+        ap0.add_argument("--gpus", type=int, default=1)
+        if ap0.parse_known_args()[0].gpus > 1:
+            sys.exit(self_launch(sys.argv[1:]))
+
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -192,6 +315,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-hbm", action="store_true", help="skip the HBM-roofline side measurement")
     ap.add_argument("--no-f64", action="store_true", help="skip the fp64 (parity-mode) side measurement")
+    ap.add_argument("--no-sharded", action="store_true", help="skip the sharded lava65536 / doorkey65536 blocks")
     args = ap.parse_args()
 
     import torch
@@ -201,6 +325,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    if os.environ.get("MGDP_BENCH_DRYRUN") == "1":
+        return dry_run(args, rank, world)
     # Rehearsal knobs for a 1-GPU box (never set by the driver): MGDP_BENCH_DEVICE pins every rank
     # to one device, MGDP_BENCH_BACKEND=gloo replaces RCCL (which refuses two ranks per GPU).
     local = int(os.environ.get("MGDP_BENCH_DEVICE", local))
@@ -229,75 +355,49 @@ def main():
             dist.destroy_process_group()
         return
 
-    import minigrid_dynamicprogramming_amd as mg
+    reducer_box = []
 
-    spec = WORKLOADS[args.workload]
-    t_gen = time.perf_counter()
-    cells, (lo, hi) = make_cells(spec, rank, world)
-    log(f"[rank {rank}] {args.workload}: grids [{lo},{hi}) generated in {time.perf_counter() - t_gen:.1f}s")
-    sharded = spec["sharded"] and (world > 1 or force_dist)
-    reducer = None
-    if sharded:
-        from minigrid_dynamicprogramming_amd.distributed import Reducer
+    def get_reducer():
+        if not reducer_box:
+            from minigrid_dynamicprogramming_amd.distributed import Reducer
 
-        reducer = Reducer(timing=True)  # built once; its stream carries the shard's launches and collectives
+            reducer_box.append(Reducer(timing=True))  # built once; its stream carries the shards' launches
+        return reducer_box[0]
 
-    m = measure(args, args.dtype, cells, local, dist, red_dev, reducer, sharded)
+    def run_workload(name, dtype=None):
+        spec = WORKLOADS[name]
+        t_gen = time.perf_counter()
+        cells, (lo, hi) = make_cells(spec, rank, world)
+        log(f"[rank {rank}] {name}: grids [{lo},{hi}) generated in {time.perf_counter() - t_gen:.1f}s")
+        sharded = spec["sharded"] and (world > 1 or force_dist)
+        wargs = argparse.Namespace(**{**vars(args), "workload": name})
+        m = measure(wargs, dtype or args.dtype, cells, local, dist, red_dev, get_reducer() if sharded else None, sharded)
+        return spec, cells, (lo, hi), sharded, m
+
+    spec, cells, (lo, hi), sharded, m = run_workload(args.workload)
+    # the sharded BASELINE multi-GPU configs beside the default line (every rank takes part)
+    blocks = {}
+    if args.workload == "empty16" and not args.no_sharded and args.method == "fused" and args.mapping == "cell":
+        for name in ("lava65536", "doorkey65536"):
+            bspec, _, (blo, bhi), bsharded, bm = run_workload(name)
+            if rank == 0:
+                blk = {"value": bm["upd_total"] / bm["elapsed_max"], "unit": "updates/s",
+                       "ms_per_solve": bm["elapsed_max"] * 1000.0 / args.steps, "sweeps": int(bm["sweeps"][-1]),
+                       "env_id": bspec["env_id"], "global_grids": bspec["global_grids"], "grids_rank0": bhi - blo,
+                       "dtype": args.dtype, "scaling": "strong",
+                       "parallelism": (f"shard{world} + RCCL all-reduce" if bsharded and backend == "nccl" else
+                                       f"shard{world} + {backend} all-reduce" if bsharded else "direct (one GPU)"),
+                       "roofline": workload_roofline(args, args.dtype, bm, name, bhi - blo)}
+                if bm.get("collectives"):
+                    blk["collectives"] = bm["collectives"]
+                blocks[name] = blk
     if rank != 0:  # the fp64 side line and the CPU baselines are N = 1 only
         if dist is not None:
             dist.barrier()
             dist.destroy_process_group()
         return
     vi_info = m["info"]
-    A = vi_info["A"]
-    tsize = 4 if args.dtype == "f32" else 8
-    bpu = algorithmic_bytes_per_update(tsize, A)
-    HW = vi_info["W"] * vi_info["H"]
-    launches = m["launches"]
-    avg_launch_s = (m["kern_ms"] / 1000.0) / max(launches, 1)
-    # solves inside the timed launches: the K timed solves plus the priming solve a resident
-    # server's launch also spans
-    solves_in_launches = args.steps + m["primed"]
-    upd_per_solve = float(vi_info["updates_per_sweep"]) * float(np.mean(m["sweeps"]))
-    alg_bytes_launch = upd_per_solve * solves_in_launches * bpu / max(launches, 1)
-    achieved = alg_bytes_launch / avg_launch_s / 1e9 if launches else 0.0
-    comp_launch = compulsory_bytes_per_solve(vi_info, tsize, args.method, m["sweeps"][-1]) * solves_in_launches / max(launches, 1)
-    key = f"{args.workload}/{args.method}/{args.mapping}/{args.dtype}"
-    traffic = load_traffic(key, solves_in_launches / max(launches, 1))
-    roofline = {
-        "bound": "hbm", "kernel": vi_info["kernel"],
-        "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-        "traffic": traffic, "launches": launches, "avg_launch_us": avg_launch_s * 1e6,
-        "alg_bytes_per_launch": alg_bytes_launch, "alg_bytes_per_update": bpu,
-        "solves_per_launch": solves_in_launches / max(launches, 1),
-        "compulsory_bytes_per_launch": comp_launch,
-        "compulsory_frac": comp_launch / max(avg_launch_s, 1e-30) / 1e9 / HBM_PEAK_GBS,
-        "note": ("achieved = SURVEY 8(d) algorithmic bytes (sizeof V + 1 + sizeof V / A per (s,a) update) per launch "
-                 "/ the launch's HIP-event duration; compulsory = the bytes this kernel must move per launch "
-                 "(fused/served: cells in + V and pi out once per solve; sweep: 2*S*sizeof V + W*H per "
-                 "grid-sweep); traffic = PMC HBM bytes per launch (profiles/pmc_traffic.json)"),
-    }
-    sq = load_sq(f"{key}/{vi_info['kernel']}")
-    if sq and sq.get("valu_insts_per_launch") and launches:
-        # the batched fused kernel keeps V in LDS: its limits are issue / LDS / latency, not HBM
-        lane_ops = sq["valu_insts_per_launch"] * 64.0 / avg_launch_s
-        roofline["valu"] = {"achieved": lane_ops, "peak": VALU_PEAK_LANE_OPS, "unit": "lane-ops/s",
-                            "frac": lane_ops / VALU_PEAK_LANE_OPS, "lds_array_busy": sq.get("lds_array_busy"),
-                            "wave_split": sq.get("wave_split"), "source": sq.get("source")}
-    if args.workload == "empty16":
-        roofline["regime"] = ("single 4 KiB V grid on one resident workgroup: latency bound (barrier + LDS round trip "
-                              "per sweep, host hand-off per solve); HBM is not the limit here (SURVEY 8(d) "
-                              "caveats); see roofline_hbm for the kernels at the HBM-sized config R")
-    if vi_info["persistent"]:
-        roofline["launch_note"] = ("lone grid: one resident vi_serve_kernel launch serves the priming solve and every "
-                                   "timed solve (host posts a request word, the workgroup solves and publishes), so "
-                                   "its duration spans the timed region")
-    if roofline["frac"] > 1.0:  # LDS-served gathers: the algorithmic figure is not an HBM rate
-        roofline["alg_equiv_gbs"] = achieved
-        meas = traffic if traffic else comp_launch
-        roofline["achieved"] = meas / avg_launch_s / 1e9
-        roofline["frac"] = roofline["achieved"] / HBM_PEAK_GBS
-        roofline["achieved_basis"] = "pmc traffic" if traffic else "compulsory bytes"
+    roofline = workload_roofline(args, args.dtype, m, args.workload, hi - lo)
     out = {
         "metric": METRIC,
         "value": m["upd_total"] / m["elapsed_max"],
@@ -315,7 +415,7 @@ def main():
         "config": {
             "workload": args.workload, "env_id": spec["env_id"], "grids_per_gpu": hi - lo,
             "global_grids": (hi - lo) * world if not spec["sharded"] else spec["global_grids"],
-            "states_per_grid": vi_info["S"], "actions": A, "gamma": args.gamma, "tol": args.tol,
+            "states_per_grid": vi_info["S"], "actions": vi_info["A"], "gamma": args.gamma, "tol": args.tol,
             "method": args.method, "mapping": args.mapping,
             "parallelism": (f"shard{world} + RCCL dV all-reduce" if sharded else
                             ("replicas only" if spec["replicate"] else f"independent batches x{world}")),
@@ -326,8 +426,10 @@ def main():
     }
     if m.get("collectives"):
         out["collectives"] = m["collectives"]
+    if blocks:
+        out["sharded"] = blocks
     if args.dtype == "f32" and world == 1 and not args.no_f64:
-        m64 = measure(args, "f64", cells, local, dist, red_dev, reducer, sharded)
+        m64 = measure(args, "f64", cells, local, dist, red_dev, get_reducer() if sharded else None, sharded)
         out["f64"] = {"value": m64["upd_total"] / m64["elapsed_max"], "unit": "updates/s",
                       "ms_per_step": m64["elapsed_max"] * 1000.0 / args.steps, "sweeps": int(m64["sweeps"][-1]),
                       "kernel": m64["info"]["kernel"],
@@ -633,7 +735,7 @@ def step_bench(args, rank, world, local, dist, red_dev):
                        "global_envs": B * world, "view": V, "parallelism": f"independent env batches x{world}"},
             "roofline": {"bound": "hbm", "kernel": "envs_step_kernel", "achieved": ach, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                         "traffic": load_traffic(f"{args.workload}/step", 1.0), "launches": args.steps,
+                         "traffic": load_traffic(f"{args.workload}/step", 1.0, grids=B), "launches": args.steps,
                          "avg_launch_us": avg * 1e6, "alg_bytes_per_launch": bpe * B,
                          "alg_bytes_per_env_step": bpe,
                          "timing": "one event pair on the launch stream around the K launches / K"},
@@ -704,7 +806,7 @@ def gen_bench(args, rank, world, local, dist, red_dev):
                        "global_grids": B * world, "parallelism": f"seed ranges x{world}"},
             "roofline": {"bound": "hbm", "kernel": "gen_grids_kernel", "achieved": ach, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                         "traffic": load_traffic(f"{args.workload}/gen", 1.0), "launches": args.steps,
+                         "traffic": load_traffic(f"{args.workload}/gen", 1.0, grids=B), "launches": args.steps,
                          "avg_launch_us": avg * 1e6, "alg_bytes_per_launch": bpg * B, "alg_bytes_per_grid": bpg,
                          "regime": "integer RNG / rejection-loop latency bound (one thread per seed); "
                                    "HBM carries only the output"},
@@ -770,10 +872,10 @@ def hbm_side_measurement(args, n_solves=3):
         info = {"B": vi.B, "S": vi.S, "W": vi.W, "H": vi.H}
         if method == "sweep":  # one timed launch per sweep (the pi pass is not timed)
             comp = compulsory_bytes_per_sweep(vi.S, vi.W * vi.H, tsize) * vi.B
-        else:  # one launch per solve; V lives in LDS between sweeps
-            comp = compulsory_bytes_per_solve(info, tsize, "fused", ks[-1])
+        else:  # V lives in LDS between sweeps: a solve's compulsory bytes, spread over its launches
+            comp = compulsory_bytes_per_solve(info, tsize, "fused", ks[-1]) * n_solves / max(n, 1)
         key = f"empty16x65536/{method}/{args.mapping}/{args.dtype}"
-        traffic = load_traffic(key, n_solves / max(n, 1))
+        traffic = load_traffic(key, n_solves / max(n, 1), grids=vi.B)
         meas = traffic if traffic else comp
         r = {"kernel": vi.kernel_name, "updates_per_s": upd / el, "sweeps": ks[-1], "launches": n,
              "avg_launch_us": avg * 1e6, "bound": "hbm" if method == "sweep" else "valu/lds (not hbm)",

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MGDP_ABI_VERSION 4
+#define MGDP_ABI_VERSION 5
 
 enum {
     MGDP_OK = 0,
@@ -115,9 +115,11 @@ int mgdp_vi_set_stream(mgdp_vi *vi, void *hip_stream);
  * persistent lone-grid server resident (see mgdp_vi_solve) the grid is staged in host-mapped
  * memory and handed to the server with the next request: no stream drain, no relaunch. */
 int mgdp_vi_load_cells(mgdp_vi *vi, const uint8_t *cells);
-/* Same from device memory (already validated by the caller).  The bytes must be complete before
- * the call and unchanged until the next solve returns: a resident lone-grid server reads them
- * itself with the next request; otherwise they are copied on the handle's stream. */
+/* Same from device memory (already validated by the caller).  On the handle's own stream a
+ * resident lone-grid server reads the bytes itself with its next request: they must then be
+ * complete before the call and stay valid and unchanged until the next solve returns (or, if no
+ * solve follows, until the next call that uses the handle's stream).  On a caller-bound stream
+ * (mgdp_vi_set_stream) they are copied on that stream, ordered after the caller's earlier work. */
 int mgdp_vi_load_cells_device(mgdp_vi *vi, const uint8_t *d_cells);
 
 /* Whole solve on one device: V_0 = 0, sweeps until the global rule stops.  Synchronous.
@@ -135,15 +137,21 @@ int mgdp_vi_persistent(const mgdp_vi *vi, int32_t *on);
  * vi_fused_kernel, vi_fused_opts_kernel, vi_sweep_pipe_kernel or vi_sweep_kernel; NULL on error. */
 const char *mgdp_vi_kernel_name(const mgdp_vi *vi);
 
-/* Multi-device protocol (DESIGN.md "convergence across GPUs"): every rank calls
- *   mgdp_vi_reset -> mgdp_vi_run_local(&k_local) -> all-reduce(MAX) k -> mgdp_vi_run_to(k, &dv)
- *   -> all-reduce(MAX) dv; while (dv >= tol && k < max_sweeps) { mgdp_vi_sweep(&dv); all-reduce; }
- *   -> mgdp_vi_finish(k).
+/* Multi-device protocol: every rank calls
+ *   mgdp_vi_reset -> mgdp_vi_run_local(&k_local) -> mgdp_vi_local_result(&k, &dv_own, &k_min)
+ *   -> all-reduce(MAX) {k, dv_own} -> mgdp_vi_run_to(K, &dv)
+ *   -> [only if the all-reduced dv_own != 0] all-reduce(MAX) dv;
+ *   while (dv >= tol && k < max_sweeps) { mgdp_vi_sweep(&dv); all-reduce; } -> mgdp_vi_finish(K).
  * Because each grid's Jacobi trajectory is independent of the others, this yields exactly the
- * V_k of the single global rule; the all-reduces carry one scalar each over RCCL/xGMI. */
+ * V_K of the single global rule.  dv_own = 0 everywhere means every grid ended its own rule at an
+ * exact fixed point (V_k == V_{k-1} bit for bit; a sweep is a function of V alone), so every later
+ * sweep changes nothing and dV at K is 0 on every rank: one all-reduce per solve then suffices. */
 int mgdp_vi_reset(mgdp_vi *vi);
 /* Each grid sweeps until its own max|dV| < tol (or max_sweeps); returns max sweeps over grids. */
 int mgdp_vi_run_local(mgdp_vi *vi, int32_t *k_local_max);
+/* The last launch's reduction: max / min sweeps over the grids and the max|dV| of their last sweeps
+ * (after mgdp_vi_run_local: each grid's own stopping sweep). */
+int mgdp_vi_local_result(const mgdp_vi *vi, int32_t *k_max, double *dv, int32_t *k_min);
 /* Continue every grid to exactly k_target sweeps; dv_out = max over grids of |dV| at sweep k. */
 int mgdp_vi_run_to(mgdp_vi *vi, int32_t k_target, double *dv_out);
 /* One more Jacobi sweep of every grid (all at the same sweep index); dv_out as above. */
@@ -154,14 +162,21 @@ int mgdp_vi_finish(mgdp_vi *vi, int32_t sweeps);
 /* The same protocol with no host round trip between its steps (fused method, no horizon / lava
  * options; distributed.py drives it over RCCL).  d_pub / d_k are caller-owned DEVICE int64 buffers
  * ordered on the handle's stream (mgdp_vi_set_stream):
- *   mgdp_vi_reset -> mgdp_vi_run_local_dev(p) -> all-reduce(MAX) p[0] on the stream
- *   -> mgdp_vi_run_to_dev(p, p + 4) -> all-reduce(MAX) p[5] -> ONE host read of p[0] (K), p[5]
+ *   mgdp_vi_reset -> mgdp_vi_run_local_dev(p) -> all-reduce(MAX) p[0..1] on the stream
+ *   -> mgdp_vi_run_to_dev_sync(p, &K, &dv, &dv_own)   (one wait on host-mapped words)
+ *   -> [only if dv_own != 0: p[5] <- dv, all-reduce(MAX) p[5], host read]
  *   -> mgdp_vi_set_result(K, dv) -> (rare fallback: mgdp_vi_sweep + host all-reduces) -> finish.
  * A launch writes d_pub[0..3] = {max sweeps over the shard's grids, max|dV| as IEEE-754 bits
- * (non-negative doubles order like their bits), min sweeps, launch epoch}; both calls only enqueue. */
+ * (non-negative doubles order like their bits), min sweeps, launch epoch}; run_local_dev only
+ * enqueues. */
 int mgdp_vi_run_local_dev(mgdp_vi *vi, int64_t *d_pub);
-/* Every grid to exactly the sweep *d_k (read on the device when the launch starts). */
+/* Every grid to exactly the sweep *d_k (read on the device when the launch starts); enqueue only. */
 int mgdp_vi_run_to_dev(mgdp_vi *vi, const int64_t *d_k, int64_t *d_pub);
+/* Every grid to exactly K = d_kdv[0] (read on the device); waits for the launch's result on the
+ * host without a stream synchronisation: k_out = K, dv_out = this shard's max|dV| at sweep K,
+ * dv_rule_out = d_kdv[1] read as a double (the all-reduced own-rule dV of run_local_dev). */
+int mgdp_vi_run_to_dev_sync(mgdp_vi *vi, const int64_t *d_kdv, int32_t *k_out, double *dv_out,
+                            double *dv_rule_out);
 /* Hand the all-reduced K and dV back to the handle (every grid is at sweep K). */
 int mgdp_vi_set_result(mgdp_vi *vi, int32_t k, double dv);
 

@@ -11,6 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # MGDP_LIB: an alternative build of the same sources (tools/ experiments with compile-time knobs)
 LIB_PATH = os.environ.get("MGDP_LIB") or os.path.join(HERE, "libmgdp.so")
 
+ABI_VERSION = 5
 MGDP_OK = 0
 MGDP_E_INVALID = -1
 MGDP_E_HIP = -2
@@ -85,6 +86,8 @@ SIGNATURES = {
     "mgdp_vi_run_local_dev": (ctypes.c_int, [_P, _P]),
     "mgdp_vi_run_to_dev": (ctypes.c_int, [_P, _P, _P]),
     "mgdp_vi_set_result": (ctypes.c_int, [_P, _I32, ctypes.c_double]),
+    "mgdp_vi_run_to_dev_sync": (ctypes.c_int, [_P, _P, _I32P, _DP, _DP]),
+    "mgdp_vi_local_result": (ctypes.c_int, [_P, _I32P, _DP, _I32P]),
     "mgdp_vi_get_values": (ctypes.c_int, [_P, _P]),
     "mgdp_vi_get_policy": (ctypes.c_int, [_P, _P]),
     "mgdp_vi_get_dv_trace": (ctypes.c_int, [_P, _P, _I32]),
@@ -148,7 +151,7 @@ def load():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.mgdp_abi_version() != 4:
+    if L.mgdp_abi_version() != ABI_VERSION:
         raise MgdpError("libmgdp ABI version mismatch")
     _lib = L
     return L

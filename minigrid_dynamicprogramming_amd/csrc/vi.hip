@@ -122,7 +122,14 @@ struct mgdp_vi {
     uint8_t *d_stage = nullptr;   // its device alias
     unsigned long long pending_src = 0;
     bool last_req = false;        // the request being posted is the server's last (mgdp_vi_solve_last)
-    bool exiting = false;         // a server told to leave after its last request may still be on the stream
+    bool exiting = false;         // a server told to leave after its last request is the stream's last work
+    unsigned long long serve_tag = 0;  // tag of the latest server launch: its exit word (h_out[11]) carries it
+    // launch-wide global rule (GkCtx, fused_wave2_xyd): one launch per batched solve when every grid
+    // wave of the batch can be resident at once (MGDP_GK=0 turns it off)
+    bool gk = false;
+    int gk_cap = 256;             // extra sweeps a fixed-point grid does while K is not yet published
+    int gk_capacity = 0;          // resident workgroups of the wave2 kernel on this device
+    unsigned long long *d_gk = nullptr;
 };
 
 namespace {
@@ -311,7 +318,8 @@ F pick_dkhalf(int n, F dflt) {
 // polls; the multi-GPU device protocol passes a device buffer it all-reduces); k_dev: the target
 // sweep read from device memory instead of k_target (mgdp_vi_run_to_dev).
 template <typename T, int MODEL, bool SLIP, int MAP>
-int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr, const long long *k_dev = nullptr) {
+int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr, const long long *k_dev = nullptr,
+                   unsigned long long *mirror = nullptr) {
     if (vi->opts) return launch_opts<T>(vi, k_target);
     if (!pub) pub = vi->d_hout;
     const Geo g = make_geo(vi);
@@ -354,10 +362,13 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
     if (smem > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
     TimedPair tp;
     if (int rc = timed_begin(vi, -1, &tp)) return rc;
+    // the launch-wide rule: a fresh own-rule launch of a resident batch (every grid then also does
+    // the sweeps up to the global K, and the run_to launch is skipped when all reached it)
+    unsigned long long *gk = (vi->gk && k_target < 0 && vi->fresh && !k_dev) ? vi->d_gk : nullptr;
     hipExtLaunchKernelGGL(kern, dim3(vi->d.B), dim3(vi->fused_block), smem, vi->stream, tp.a, tp.b, 0, g,
                        make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv,
                        vi->d_dvenv, vi->d_red, vi->d_ticket, pub, k_target, vi->fresh,
-                       vi->d.B <= vi->inkernel_max ? 1 : 0, ++vi->epoch, k_dev);
+                       vi->d.B <= vi->inkernel_max ? 1 : 0, ++vi->epoch, k_dev, mirror, gk, vi->gk_cap);
     MGDP_HIP(hipGetLastError());
     vi->fresh = 0;
     if (vi->d.B > vi->inkernel_max) {
@@ -382,10 +393,11 @@ int launch_serve_t(mgdp_vi *vi, unsigned int served) {
     if (smem > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
     TimedPair tp;
     if (int rc = timed_begin(vi, -1, &tp)) return rc;
+    ++vi->serve_tag;
     hipExtLaunchKernelGGL(kern, dim3(1), dim3(vi->fused_block), smem, vi->stream, tp.a, tp.b, 0, g,
                           make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv, vi->d_dvenv,
                           vi->d_hout, vi->d_hout + 4, (unsigned long long)served, vi->serve_idle_ticks,
-                          vi->serve_life_ticks, vi->serve_pollers);
+                          vi->serve_life_ticks, vi->serve_pollers, vi->serve_tag);
     MGDP_HIP(hipGetLastError());
     return 0;
 }
@@ -460,8 +472,9 @@ int dispatch(mgdp_vi *vi, Args... args) {
 
 template <typename T, int MODEL, bool SLIP, int MAP>
 struct FusedF {
-    static int run(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr, const long long *k_dev = nullptr) {
-        return launch_fused_t<T, MODEL, SLIP, MAP>(vi, k_target, pub, k_dev);
+    static int run(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr, const long long *k_dev = nullptr,
+                   unsigned long long *mirror = nullptr) {
+        return launch_fused_t<T, MODEL, SLIP, MAP>(vi, k_target, pub, k_dev, mirror);
     }
 };
 template <typename T, int MODEL, bool SLIP, int MAP>
@@ -498,7 +511,6 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
                 if (tagged && relaunches < 4) {
                     ++relaunches;
                     DeviceGuard guard(vi->d.device);  // the served fast path of mgdp_vi_solve holds none
-                    __atomic_store_n(vi->h_out + 11, 0ull, __ATOMIC_RELEASE);
                     if (int rc = dispatch<ServeF>(vi, vi->epoch - 1u)) return rc;
                     continue;
                 }
@@ -547,25 +559,33 @@ bool serve_eligible(const mgdp_vi *vi) {
 // drain = false (mgdp_vi_synchronize): wait for the server's exit word -- its V / pi stores are
 // then complete and visible, and nothing else is queued behind it -- instead of the stream's
 // completion signal, which a later device synchronize still observes.
+// Wait for the exit word of the latest server launch (its own tag: a late store of an earlier
+// server cannot satisfy it); a server that never started or faulted is reported by the stream.
+int wait_server_exit(mgdp_vi *vi) {
+    const volatile unsigned long long *h = vi->h_out;
+    for (uint64_t spin = 0; h[11] != vi->serve_tag; ++spin) {
+        if ((spin & 1023) == 1023) {
+            const hipError_t q = hipStreamQuery(vi->stream);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) return hip_fail(q, "persistent server", __FILE__, __LINE__);
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return 0;
+}
 int server_stop(mgdp_vi *vi, bool drain = true) {
     if (vi->serving) {
         __atomic_store_n(vi->h_out + 4, kServeQuit, __ATOMIC_RELEASE);
         vi->serving = false;
         if (drain) {
             MGDP_HIP(hipStreamSynchronize(vi->stream));
-            vi->exiting = false;
-        } else {
-            const volatile unsigned long long *h = vi->h_out;
-            for (uint64_t spin = 0; h[11] == 0; ++spin) {
-                if ((spin & 1023) == 1023) {  // a server that never started or faulted: the stream says
-                    const hipError_t q = hipStreamQuery(vi->stream);
-                    if (q == hipSuccess) break;
-                    if (q != hipErrorNotReady) return hip_fail(q, "persistent server", __FILE__, __LINE__);
-                }
-            }
-            std::atomic_thread_fence(std::memory_order_acquire);
+        } else if (int rc = wait_server_exit(vi)) {
+            return rc;
         }
     }
+    // Whatever the caller enqueues next follows the departed server on the stream, so its exit
+    // word no longer says the stream is idle (mgdp_vi_synchronize's shortcut).
+    vi->exiting = false;
     if (vi->pending_src) {
         MGDP_HIP(hipMemcpyAsync(vi->d_cells, reinterpret_cast<const void *>(vi->pending_src), vi->HW, hipMemcpyDefault,
                                 vi->stream));
@@ -606,7 +626,7 @@ int serve_request(mgdp_vi *vi) {
     }
     post_request(vi);
     if (!vi->serving) {
-        __atomic_store_n(vi->h_out + 11, 0ull, __ATOMIC_RELEASE);  // the exit word of this launch
+        vi->exiting = false;  // a departing earlier server is no longer the stream's last work
         if (int rc = dispatch<ServeF>(vi, vi->epoch - 1u)) return rc;
         vi->serving = true;
     }
@@ -804,6 +824,22 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
             vi->HWs = (int)round_up(vi->HW, 64);
             vi->Ss = vi->S / vi->HW * vi->HWs;
         }
+        if (vi->wave2) {  // the launch-wide rule needs every grid's wave resident at once
+            int gk_on = 1;
+            if (const char *ev = std::getenv("MGDP_GK")) gk_on = std::atoi(ev);
+            if (const char *ev = std::getenv("MGDP_GK_CAP")) vi->gk_cap = std::max(1, std::atoi(ev));
+            const int smem2 = wave2_smem_bytes(vi->HWp, d.W, vi->wave2, vi->tsize);
+            const void *k2 = d.dtype == MGDP_F32
+                ? (const void *)pick_wave2<FusedK, float, MGDP_MODEL_XYD, false, MGDP_MAP_CELL>(
+                      vi->wave2, FusedK<float, MGDP_MODEL_XYD, false, MGDP_MAP_CELL, 0>::fn)
+                : (const void *)pick_wave2<FusedK, double, MGDP_MODEL_XYD, false, MGDP_MAP_CELL>(
+                      vi->wave2, FusedK<double, MGDP_MODEL_XYD, false, MGDP_MAP_CELL, 0>::fn);
+            int per_cu = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k2, 64, smem2) == hipSuccess &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d.device) == hipSuccess)
+                vi->gk_capacity = per_cu * cus;
+            vi->gk = gk_on != 0 && d.B <= vi->gk_capacity;
+        }
         int dk1t = 0;
         if (const char *ev = std::getenv("MGDP_DK_1T")) dk1t = std::atoi(ev) != 0;
         if (dk1t && d.B > 1 && d.model == MGDP_MODEL_DOORKEY && d.dtype == MGDP_F32 && d.method == MGDP_METHOD_FUSED &&
@@ -844,6 +880,10 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     al((void **)&vi->d_shards, sizeof(unsigned long long) * 8 * (size_t)(d.max_sweeps + 1));
     al((void **)&vi->d_red, sizeof(unsigned long long) * (kRedShards * 4 + 2));
     al((void **)&vi->d_pub1, sizeof(unsigned long long) * 4);
+    if (vi->gk) {
+        al((void **)&vi->d_gk, sizeof(unsigned long long) * kGkWords);
+        if (e == hipSuccess) e = hipMemset(vi->d_gk, 0, sizeof(unsigned long long) * kGkWords);
+    }
     if (d.horizon > 0) {
         al(&vi->d_rgoal, (size_t)d.horizon * vi->tsize);
         if (d.flags & MGDP_KEEP_POLICY_T) al((void **)&vi->d_pi_t, (size_t)d.horizon * BS);
@@ -922,6 +962,7 @@ int mgdp_vi_destroy(mgdp_vi *vi) {
     (void)hipFree(vi->d_shards);
     (void)hipFree(vi->d_red);
     (void)hipFree(vi->d_pub1);
+    (void)hipFree(vi->d_gk);
     (void)hipFree(vi->d_rgoal);
     (void)hipFree(vi->d_pi_t);
     if (vi->h_out) (void)hipHostFree(vi->h_out);
@@ -972,7 +1013,11 @@ int mgdp_vi_load_cells(mgdp_vi *vi, const uint8_t *cells) {
 
 int mgdp_vi_load_cells_device(mgdp_vi *vi, const uint8_t *d_cells) {
     MGDP_CHECK(vi && d_cells, MGDP_E_INVALID, "null argument");
-    if (serve_handoff(vi, d_cells)) {  // the resident server reads the bytes with its next request
+    // The resident server reads the bytes itself with its next request, unordered with respect to
+    // any stream: only on the handle's own stream, where no caller kernel can still be producing
+    // them.  On a caller-bound stream (mgdp_vi_set_stream) the copy below is ordered after whatever
+    // the caller enqueued there before this call.
+    if (vi->own_stream && serve_handoff(vi, d_cells)) {
         vi->cells_loaded = true;
         vi->k_done_valid = false;
         return 0;
@@ -1023,7 +1068,11 @@ int mgdp_vi_run_local(mgdp_vi *vi, int32_t *k_local_max) {
         *k_local_max = km;
         return 0;
     }
-    if (int rc = sweep_run(vi, vi->d.max_sweeps, false, nullptr)) return rc;
+    double dv = 0.0;
+    if (int rc = sweep_run(vi, vi->d.max_sweeps, false, &dv)) return rc;
+    vi->k_min = vi->k_max = vi->k_done;  // the sweep method stops the whole batch at once
+    vi->dv_red = dv;
+    vi->k_done_valid = true;
     *k_local_max = vi->k_done;
     return 0;
 }
@@ -1082,6 +1131,41 @@ int mgdp_vi_run_to_dev(mgdp_vi *vi, const int64_t *d_k, int64_t *d_pub) {
     DeviceGuard guard(vi->d.device);
     vi->k_done_valid = false;
     return dispatch<FusedF>(vi, 0, reinterpret_cast<unsigned long long *>(d_pub), reinterpret_cast<const long long *>(d_k));
+}
+
+int mgdp_vi_run_to_dev_sync(mgdp_vi *vi, const int64_t *d_kdv, int32_t *k_out, double *dv_out, double *dv_rule_out) {
+    MGDP_CHECK(vi && d_kdv, MGDP_E_INVALID, "null argument");
+    MGDP_CHECK(vi->d.method == MGDP_METHOD_FUSED && !vi->opts, MGDP_E_UNSUPPORTED,
+               "the device protocol runs the fused method without horizon / lava options");
+    MGDP_CHECK(!vi->fresh, MGDP_E_INVALID, "mgdp_vi_run_to_dev_sync before mgdp_vi_run_local_dev");
+    DeviceGuard guard(vi->d.device);
+    vi->k_done_valid = false;
+    // result -> host-mapped words (reduce_env polls them), d_kdv[1] -> h_out[13] by the launch
+    if (int rc = dispatch<FusedF>(vi, 0, (unsigned long long *)nullptr, reinterpret_cast<const long long *>(d_kdv),
+                                  vi->d_hout + 13))
+        return rc;
+    int32_t km = 0;
+    double dv = 0.0;
+    if (int rc = reduce_env(vi, &km, &dv)) return rc;
+    MGDP_CHECK(vi->k_min == km, MGDP_E_INVALID, "run_to_dev_sync: grids ended at sweeps %d..%d, not at one common K",
+               vi->k_min, km);
+    vi->k_done = km;
+    const unsigned long long rb = vi->h_out[13];
+    double rule;
+    std::memcpy(&rule, &rb, sizeof(double));
+    if (k_out) *k_out = km;
+    if (dv_out) *dv_out = dv;
+    if (dv_rule_out) *dv_rule_out = rule;
+    return 0;
+}
+
+int mgdp_vi_local_result(const mgdp_vi *vi, int32_t *k_max, double *dv, int32_t *k_min) {
+    MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
+    MGDP_CHECK(vi->k_done_valid, MGDP_E_INVALID, "no launch result to report (run mgdp_vi_run_local first)");
+    if (k_max) *k_max = vi->k_max;
+    if (dv) *dv = vi->dv_red;
+    if (k_min) *k_min = vi->k_min;
+    return 0;
 }
 
 int mgdp_vi_set_result(mgdp_vi *vi, int32_t k, double dv) {
@@ -1163,7 +1247,9 @@ int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *con
     if (int rc = mgdp_vi_reset(vi)) return rc;
     int32_t k = 0;
     double dv = 0.0;
-    if (vi->chain && vi->d.method == MGDP_METHOD_FUSED && vi->d.horizon == 0 && !vi->opts && !serve_eligible(vi)) {
+    // With the launch-wide rule (vi->gk) the own-rule launch normally ends with every grid at K:
+    // run_local's result is awaited and run_to is launched only if some grid is still below K.
+    if (vi->chain && !vi->gk && vi->d.method == MGDP_METHOD_FUSED && vi->d.horizon == 0 && !vi->opts && !serve_eligible(vi)) {
         // The single-GPU form of the multi-GPU device protocol: run_local publishes {K, ...} to
         // device memory and run_to(K) reads K there, enqueued back to back -- no host round trip
         // and no launch gap between the two; the host waits once, for run_to's result.
@@ -1172,6 +1258,10 @@ int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *con
         if (int rc = dispatch<FusedF>(vi, -1, vi->d_pub1, (const long long *)nullptr)) return rc;
         if (int rc = dispatch<FusedF>(vi, 0, (unsigned long long *)nullptr, (const long long *)vi->d_pub1)) return rc;
         if (int rc = reduce_env(vi, &k, &dv)) return rc;
+        // run_to read K on the device: every grid must have ended exactly there (the host path's
+        // km == k_target check)
+        MGDP_CHECK(vi->k_min == k && vi->k_max == k, MGDP_E_INVALID,
+                   "chained solve: grids ended at sweeps %d..%d, not at one common K", vi->k_min, vi->k_max);
         vi->k_done = k;
     } else {
         if (int rc = mgdp_vi_run_local(vi, &k)) return rc;
@@ -1266,11 +1356,14 @@ int mgdp_vi_device_buffers(mgdp_vi *vi, void **d_V, void **d_pi) {
 int mgdp_vi_synchronize(mgdp_vi *vi) {
     MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
     DeviceGuard guard(vi->d.device);
-    if (vi->serving && !vi->pending_src) return server_stop(vi, false);  // the server is the stream's last work
-    if (vi->exiting && !vi->pending_src) {  // a server leaving after its last request: its exit word
+    // A resident server, or one leaving after its last request (mgdp_vi_solve_last), is the stream's
+    // last work while nothing else was enqueued since (every other enqueue goes through server_stop
+    // or a relaunch, which clear `exiting`): its tagged exit word then means the stream is done.
+    if (vi->serving && !vi->pending_src) return server_stop(vi, false);
+    if (vi->exiting && !vi->pending_src) {
+        if (int rc = wait_server_exit(vi)) return rc;
         vi->exiting = false;
-        vi->serving = true;  // (server_stop's quit word is harmless: it is leaving anyway)
-        return server_stop(vi, false);
+        return 0;
     }
     if (int rc = server_stop(vi)) return rc;
     MGDP_HIP(hipStreamSynchronize(vi->stream));

@@ -32,7 +32,8 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
                                            T *__restrict__ V, int8_t *__restrict__ pi, int32_t *__restrict__ kenv,
                                            double *__restrict__ dvenv, unsigned long long *__restrict__ host_out,
                                            int k_target, int fresh, bool lone, unsigned int epoch, int e,
-                                           int &k, double &dvl, const typename TopoOf<T, MODEL>::type *pre = nullptr) {
+                                           int &k, double &dvl, const typename TopoOf<T, MODEL>::type *pre = nullptr,
+                                           unsigned long long *gk = nullptr, int gk_cap = 0) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
     T *V0 = reinterpret_cast<T *>(smem);
@@ -59,8 +60,13 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
                 publish(host_out, (unsigned long long)kk, (unsigned long long)__double_as_longlong(dv),
                         (unsigned long long)kk, epoch);
         };
-        if (k_target < 0) fused_wave2_xyd<T, true, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
-        else fused_wave2_xyd<T, false, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
+        if (k_target < 0) {
+            const GkCtx g{gk, epoch, e, geo.B, gk_cap};  // the launch-wide rule when the host passed its buffer
+            fused_wave2_xyd<T, true, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2,
+                                        gk ? &g : nullptr);
+        } else {
+            fused_wave2_xyd<T, false, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
+        }
         if (threadIdx.x == 0) {
             kenv[e] = k;
             dvenv[e] = dvl;
@@ -197,18 +203,29 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
                 unsigned long long *__restrict__ host_out, int k_target, int fresh, int in_kernel_reduce,
-                unsigned int epoch, const long long *__restrict__ k_target_dev) {
+                unsigned int epoch, const long long *__restrict__ k_target_dev,
+                unsigned long long *__restrict__ host_mirror, unsigned long long *__restrict__ gk, int gk_cap) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
     T *slots = reinterpret_cast<T *>(smem + (wp_is_wave2(WP) ? 0 : L.slots_off()));
     // multi-GPU protocol (mgdp_vi_run_to_dev): the target sweep is the all-reduced K in device
     // memory, written by a collective ordered before this launch on the stream
-    if (k_target_dev) k_target = (int)*k_target_dev;
+    if (k_target_dev) {
+        k_target = (int)k_target_dev[0];
+        // mgdp_vi_run_to_dev_sync: the all-reduced word after K (the own-rule dV) goes to the host
+        // with this launch's result.  Stored before the block's reduction ticket (fused_reduce
+        // drains it first) or, past the in-kernel limit, before the reduce kernel runs: it is
+        // visible before the epoch word the host polls.
+        if (host_mirror && blockIdx.x == 0 && threadIdx.x == 0)
+            __hip_atomic_store(host_mirror, (unsigned long long)k_target_dev[1], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     int k;
     double dvl;
     const bool lone = in_kernel_reduce && gridDim.x == 1;
     const bool work = fused_grid<T, MODEL, SLIP, MAP, false, WP>(geo, cf, cells, V, pi, kenv, dvenv, host_out, k_target,
-                                                                 fresh, lone, epoch, blockIdx.x, k, dvl);
+                                                                 fresh, lone, epoch, blockIdx.x, k, dvl, nullptr,
+                                                                 wp_is_wave2(WP) ? gk : nullptr, gk_cap);
     if (in_kernel_reduce) fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16), epoch, work);
 }
 
@@ -237,7 +254,8 @@ __global__ void __launch_bounds__(WP > 0 ? 64 : 1024)
 vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict__ V,
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ host_out, const unsigned long long *__restrict__ host_cmd,
-                unsigned long long served, unsigned long long idle_ticks, unsigned long long life_ticks, int pollers) {
+                unsigned long long served, unsigned long long idle_ticks, unsigned long long life_ticks, int pollers,
+                unsigned long long exit_tag) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ unsigned long long s_cmd, s_src;
     const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
@@ -320,9 +338,11 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
     }
     // Leaving: every wave's V / pi stores complete, then one system-scope release tells the host
     // (server_stop without a drain waits for this word instead of the stream's completion signal).
+    // The word is this launch's own tag, so an earlier server's late exit store can never satisfy
+    // the wait for a later one.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(host_out + 11, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) __hip_atomic_store(host_out + 11, exit_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // The fused solve with the SURVEY 8(f) item-3 options (ND = NoDeath lava, HMODE = finite horizon

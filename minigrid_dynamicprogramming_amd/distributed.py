@@ -2,26 +2,34 @@
 
 Grids are independent units: rank r holds the contiguous block [r*B/G, (r+1)*B/G) of the global
 batch and never exchanges V.  The only collective is the global stopping rule of DESIGN.md "A9"
-(stop after sweep k when max over ALL grids of |V_k - V_{k-1}| < tol), carried as scalar MAX
-all-reduces over RCCL/xGMI (backend "nccl" on ROCm) or gloo on CPU:
+(stop after sweep k when max over ALL grids of |V_k - V_{k-1}| < tol), carried as MAX all-reduces
+of two scalars over RCCL/xGMI (backend "nccl" on ROCm) or gloo on CPU:
 
-    k_r   = run_local()            each grid sweeps until its own |dV| < tol (no communication)
-    K     = allreduce_max(k_r)     the slowest grid anywhere
-    dv    = allreduce_max(run_to(K))   every grid advanced to exactly K sweeps
+    k_r, e_r = run_local()             each grid sweeps until its own |dV| < tol (no communication);
+                                       e_r = max |dV| of the shard's grids at their own last sweeps
+    K, E  = allreduce_max(k_r, e_r)    the slowest grid anywhere, and the largest own-rule dV
+    dv_r  = run_to(K)                  every grid advanced to exactly K sweeps
+    dv    = 0 if E == 0 else allreduce_max(dv_r)
     while dv >= tol and K < max_sweeps:  dv = allreduce_max(sweep()); K += 1   (rare fallback)
 
 Each grid's Jacobi trajectory V_0, V_1, ... does not depend on the other grids, so after this
 protocol every grid holds exactly the V_K / pi_K that one global loop would produce.  The Bellman
 operator is a gamma-contraction in the sup norm, so per-grid |dV| is non-increasing and K is the
-global stopping sweep; the fallback loop covers rounding-level violations (fp32).
+global stopping sweep; the fallback loop covers rounding-level violations (fp32).  E == 0 means
+every grid stopped its own rule at an exact fixed point (V_k equal to V_{k-1} bit for bit; a sweep
+is a function of V alone), so every later sweep reproduces it and dV at K is 0 on every rank: the
+second all-reduce is skipped, and a deterministic batch (the shortest-path values settle exactly)
+needs ONE collective per solve.
 
-Device protocol (RCCL, fused method): K and dV never visit the host between the steps.  The
-shard's two launches publish {k max, dV bits, k min, epoch} into an int64 buffer on the GPU, the
-all-reduces run on the same stream (ProcessGroupNCCL orders its stream after the current one and
-the current one after the collective), run_to reads K on the device, and the host reads K and dV
-ONCE per solve.  Non-negative doubles order like their IEEE-754 bit patterns, so a MAX over the
-int64 bits is the MAX over the values.  Host protocol (gloo, sweep method, DP options): one
-host-synchronous scalar all-reduce per step.
+Device protocol (RCCL, fused method): K and E never visit the host before run_to.  The shard's
+run_local launch publishes {k max, dV bits, k min, epoch} into an int64 buffer on the GPU, the
+all-reduce of its first two words runs on the same stream (ProcessGroupNCCL orders its stream after
+the current one and the current one after the collective), run_to reads K on the device and its
+result comes back through host-mapped memory with E (mgdp_vi_run_to_dev_sync): one host wait per
+solve and no stream synchronisation.  Non-negative doubles order like their IEEE-754 bit patterns,
+so a MAX over the int64 bits is the MAX over the values.  Host protocol (gloo, sweep method, DP
+options): the same steps with host-synchronous all-reduces.  Every rank of a group takes the same
+protocol: a one-time MIN all-reduce of "device-capable" settles it per (shard, reducer).
 """
 from __future__ import annotations
 
@@ -50,7 +58,7 @@ class Reducer:
     """MAX all-reduces of the stopping rule, built ONCE per process and reused by every solve.
 
     device: cuda for the nccl (RCCL) backend, cpu for gloo.  `proto` is the protocol buffer of the
-    device path (int64[8]: [0..3] run_local's result, [4..7] run_to's).  Counters: `calls`
+    device path (int64[8]: [0..3] run_local's result, [5] run_to's dV when it is all-reduced).  Counters: `calls`
     (all-reduces issued), `host_reads` (host round trips of the device path), `wall_s` (host time
     inside the protocol's collectives and its one read), and with `timing` the device time of each
     all-reduce (event pairs on the protocol stream, summed by collect())."""
@@ -65,6 +73,7 @@ class Reducer:
         backend = dist.get_backend(group)
         self.device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
         self.buf = torch.zeros(1, dtype=torch.float64, device=self.device)
+        self.buf2 = torch.zeros(2, dtype=torch.float64, device=self.device)
         self.proto = torch.zeros(8, dtype=torch.int64, device=self.device)
         self.stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
         self.timing = timing and self.device.type == "cuda"
@@ -88,6 +97,24 @@ class Reducer:
         v = float(self.buf.item())
         self.wall_s += time.perf_counter() - t
         return v
+
+    def max2(self, a: float, b: float) -> tuple[float, float]:
+        """Host round trip: all-reduce two scalars (MAX each) and read them back."""
+        t = time.perf_counter()
+        self.buf2[0] = float(a)
+        self.buf2[1] = float(b)
+        self.dist.all_reduce(self.buf2, op=self.dist.ReduceOp.MAX, group=self.group)
+        self.calls += 1
+        self.host_reads += 1
+        x, y = self.buf2.tolist()
+        self.wall_s += time.perf_counter() - t
+        return x, y
+
+    def min_flag(self, flag: bool) -> bool:
+        """All-reduce MIN of a 0/1 flag (protocol agreement; not counted in `calls`)."""
+        f = self.torch.tensor([1 if flag else 0], dtype=self.torch.int64, device=self.device)
+        self.dist.all_reduce(f, op=self.dist.ReduceOp.MIN, group=self.group)
+        return bool(int(f.item()))
 
     def max_(self, t):
         """In-place MAX of a tensor (slice of `proto`), ordered on the current stream, no host read."""
@@ -115,7 +142,7 @@ _Reducer = Reducer
 
 class EmptyShard:
     """A rank that holds no grids (more ranks than grids): it joins every collective with k = 0 and
-    dV = 0, so the other ranks' protocol is unchanged."""
+    dV = 0, so the other ranks' protocol is unchanged; it takes whichever protocol its peers take."""
 
     def __init__(self, tol=1e-6, max_sweeps=10000):
         self.tol, self.max_sweeps = tol, max_sweeps
@@ -127,6 +154,9 @@ class EmptyShard:
     def run_local(self):
         return 0
 
+    def local_result(self):
+        return 0, 0.0
+
     def run_to(self, k):
         return 0.0
 
@@ -136,7 +166,7 @@ class EmptyShard:
     def finish(self, k, dv):
         self.sweeps = k
 
-    protocol_device = None  # follows the reducer (solve_sharded): the same collectives as its peers
+    protocol_device = None  # either protocol: see _agree_protocol
 
     def bind_stream(self, stream_ptr):
         pass
@@ -144,39 +174,77 @@ class EmptyShard:
     def run_local_dev(self, pub):
         pub[0:4] = 0
 
-    def run_to_dev(self, k, pub):
-        pub[0:4] = 0
+    def run_to_dev_sync(self, kdv):
+        h = kdv.tolist()
+        return int(h[0]), 0.0, bits_to_double(h[1])
 
     def set_result(self, k, dv):
         pass
 
 
+def _agree_protocol(vi, red) -> bool:
+    """Whether this solve takes the device protocol: only if EVERY rank's shard can (a MIN
+    all-reduce of a capability flag, once per (shard, reducer) pair and cached on the shard).
+    An EmptyShard can follow either; a shard whose protocol device differs from the reducer's
+    (e.g. GPU handles under gloo, sweep-method or DP-option handles) forces the host protocol."""
+    cached = getattr(vi, "_mgdp_protocol", None)
+    if cached is not None and cached[0] is red:
+        return cached[1]
+    if isinstance(vi, EmptyShard):
+        able = True
+    else:
+        dev = getattr(vi, "protocol_device", None)
+        able = dev is not None and dev.type == red.device.type
+    ok = red.min_flag(able)
+    try:
+        vi._mgdp_protocol = (red, ok)
+    except AttributeError:
+        pass
+    return ok
+
+
 def _device_protocol(vi, red):
     p = red.proto
     vi.reset()
-    vi.run_local_dev(p[0:4])
-    red.max_(p[0:1])                      # K = the slowest grid anywhere
-    vi.run_to_dev(p[0:1], p[4:8])         # every grid to exactly K (K read on the device)
-    red.max_(p[5:6])                      # dV at K over every rank
+    vi.run_local_dev(p[0:4])              # {k max, own-rule dV bits, k min, epoch}
+    red.max_(p[0:2])                      # K = the slowest grid anywhere, E = the largest own-rule dV
     t = time.perf_counter()
-    h = p.tolist()                        # the solve's one host read
+    k, dv, rule = vi.run_to_dev_sync(p[0:2])  # every grid to exactly K; the solve's one host wait
     red.wall_s += time.perf_counter() - t
     red.host_reads += 1
-    k, dv = int(h[0]), bits_to_double(h[5])
+    if rule == 0.0:                       # every grid everywhere at an exact fixed point: dV(K) = 0
+        if dv != 0.0:
+            raise RuntimeError(f"fixed-point invariant violated: dV at sweep {k} is {dv!r} after an exact "
+                               "fixed point on every rank")
+    else:
+        p[5:6].fill_(double_to_bits(dv))
+        red.max_(p[5:6])                  # dV at K over every rank
+        t = time.perf_counter()
+        dv = bits_to_double(int(p[5].item()))
+        red.wall_s += time.perf_counter() - t
+        red.host_reads += 1
     vi.set_result(k, dv)
     return k, dv
 
 
+def _local(vi):
+    """(k_local, own-rule dV) after run_local; a shard without local_result reports dV as unknown."""
+    k = vi.run_local()
+    lr = getattr(vi, "local_result", None)
+    return (k, float("inf")) if lr is None else (k, float(lr()[1]))
+
+
 def solve_sharded(vi, group=None, reducer=None) -> dict:
     """Run the protocol above on this rank's shard `vi` (a dp.ValueIteration, an EmptyShard, or any
-    object with reset/run_local/run_to/sweep/finish and tol/max_sweeps; with protocol_device and
-    run_local_dev/run_to_dev/set_result it takes the device path when that device matches the
-    reducer's).  Returns sweeps, dv, converged and the all-reduces / host reads of this solve.
-    Must be called by every rank of the group; build the Reducer once and pass it in."""
+    object with reset/run_local/run_to/sweep/finish and tol/max_sweeps, optionally local_result;
+    with protocol_device and run_local_dev/run_to_dev_sync/set_result it can take the device path).
+    Returns sweeps, dv, converged and the all-reduces / host reads of this solve (the one-time
+    protocol agreement not counted).  Must be called by every rank of the group; build the Reducer
+    once and pass it in."""
     red = reducer or Reducer(group)
+    device = _agree_protocol(vi, red)
     calls0, reads0 = red.calls, red.host_reads
-    dev = red.device if isinstance(vi, EmptyShard) else getattr(vi, "protocol_device", None)
-    if dev is not None and dev.type == red.device.type:
+    if device:
         if red.stream is not None:
             vi.bind_stream(red.stream.cuda_stream)
             with red.torch.cuda.stream(red.stream):
@@ -185,8 +253,15 @@ def solve_sharded(vi, group=None, reducer=None) -> dict:
             k, dv = _device_protocol(vi, red)
     else:
         vi.reset()
-        k = int(red.max(vi.run_local()))
-        dv = red.max(vi.run_to(k))
+        k_loc, e_loc = _local(vi)
+        K, E = red.max2(k_loc, e_loc)
+        k = int(K)
+        dv = vi.run_to(k)
+        if E == 0.0:
+            if dv != 0.0:
+                raise RuntimeError(f"fixed-point invariant violated: dV at sweep {k} is {dv!r}")
+        else:
+            dv = red.max(dv)
     while not (dv < vi.tol) and k < vi.max_sweeps:
         dv = red.max(vi.sweep())
         k += 1

@@ -267,6 +267,15 @@ class ValueIteration:
         _lib.check(self.L.mgdp_vi_run_local(self.h, ctypes.byref(k)), "mgdp_vi_run_local")
         return k.value
 
+    def local_result(self) -> tuple[int, float]:
+        """(max sweeps, max |dV| of each grid's last sweep) of the last launch (mgdp_vi_local_result):
+        after run_local, dV of every grid at its own stopping sweep."""
+        k = ctypes.c_int32(0)
+        dv = ctypes.c_double(0)
+        _lib.check(self.L.mgdp_vi_local_result(self.h, ctypes.byref(k), ctypes.byref(dv), None),
+                   "mgdp_vi_local_result")
+        return k.value, dv.value
+
     def run_to(self, k: int) -> float:
         dv = ctypes.c_double(0)
         _lib.check(self.L.mgdp_vi_run_to(self.h, int(k), ctypes.byref(dv)), "mgdp_vi_run_to")
@@ -301,6 +310,19 @@ class ValueIteration:
     def run_to_dev(self, k, pub):
         """Every grid to exactly the sweep held by the int64 device word k; results into pub."""
         _lib.check(self.L.mgdp_vi_run_to_dev(self.h, _lib.ptr(k), _lib.ptr(pub)), "mgdp_vi_run_to_dev")
+
+    def run_to_dev_sync(self, kdv) -> tuple[int, float, float]:
+        """Every grid to exactly K = kdv[0] (int64 device words, read on the device), then wait on
+        the host-mapped result: (K, this shard's dV at K, kdv[1] as a double)."""
+        if getattr(self, "_sync_fn", None) is None:
+            self._sync_fn = _lib.raw_fn("mgdp_vi_run_to_dev_sync")
+            self._sync_out = (ctypes.c_int32(0), ctypes.c_double(0), ctypes.c_double(0))
+        k, dv, rule = self._sync_out
+        rc = self._sync_fn(self.h, ctypes.c_void_p(kdv.data_ptr()), ctypes.byref(k), ctypes.byref(dv),
+                           ctypes.byref(rule))
+        if rc:
+            _lib.check(rc, "mgdp_vi_run_to_dev_sync")
+        return k.value, dv.value, rule.value
 
     def set_result(self, k: int, dv: float):
         _lib.check(self.L.mgdp_vi_set_result(self.h, int(k), float(dv)), "mgdp_vi_set_result")

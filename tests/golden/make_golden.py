@@ -74,8 +74,13 @@ def gen_grids():
             agents.append(agent_xyd(env))
         np.savez_compressed(os.path.join(HERE, f"grids_{name}.npz"),
                             enc=np.stack(encs), agent=np.array(agents, dtype=np.int32))
+
+
+def gen_digests():
+    # the BASELINE batch sizes: FourRooms x 4096 (configs[2]), LavaS11N5 x 65536 (configs[3]),
+    # DoorKey-16 x 65536 (configs[4], SURVEY 8(d) cfg 5)
     digests = {}
-    for name, n in (("fourrooms", 4096), ("lava11n5", 65536), ("doorkey16", 8192)):
+    for name, n in (("fourrooms", 4096), ("lava11n5", 65536), ("doorkey16", 65536)):
         env = ENVS[name]()
         h = hashlib.sha256()
         for seed in range(n):
@@ -342,10 +347,12 @@ def gen_tables():
 
 
 if __name__ == "__main__":
-    what = sys.argv[1:] or ["grids", "traj", "tables"]
+    what = sys.argv[1:] or ["grids", "traj", "tables"]  # or "digests" alone
     if "tables" in what:
         gen_tables()
     if "traj" in what:
         gen_trajectories()
     if "grids" in what:
         gen_grids()
+    if "grids" in what or "digests" in what:
+        gen_digests()

@@ -30,9 +30,13 @@ class OracleShard:
         self.k = 0
 
     def run_local(self):
-        ks = [oracle.value_iteration(self.model, c, tol=self.tol, max_sweeps=self.max_sweeps, slip_p=self.slip,
-                                     dtype=self.dtype)["sweeps"] for c in self.cells]
-        return max(ks)
+        rs = [oracle.value_iteration(self.model, c, tol=self.tol, max_sweeps=self.max_sweeps, slip_p=self.slip,
+                                     dtype=self.dtype) for c in self.cells]
+        self._local = (max(r["sweeps"] for r in rs), max(r["dv"] for r in rs))
+        return self._local[0]
+
+    def local_result(self):
+        return self._local
 
     def run_to(self, k):
         self.k = k
@@ -59,16 +63,13 @@ class DevOracleShard(OracleShard):
 
     def run_local_dev(self, pub):
         pub[0] = self.run_local()
-        pub[1] = 0
+        pub[1] = double_to_bits(self._local[1])
         pub[2] = 0
         pub[3] = 1
 
-    def run_to_dev(self, k, pub):
-        kk = int(k[0])
-        pub[0] = kk
-        pub[1] = double_to_bits(self.run_to(kk))
-        pub[2] = kk
-        pub[3] = 2
+    def run_to_dev_sync(self, kdv):
+        kk = int(kdv[0])
+        return kk, self.run_to(kk), bits_to_double(int(kdv[1]))
 
     def set_result(self, k, dv):
         self.k = k
@@ -93,12 +94,15 @@ def _worker(rank, world, port, cells, slip, out, device_proto=False, solves=1):
     if hi == lo:
         shard = EmptyShard()
     else:
-        shard = (DevOracleShard if device_proto else OracleShard)(cells[lo:hi], slip=slip)
+        # device_proto "mixed": odd ranks' shards can only take the host protocol
+        dev = device_proto is True or (device_proto == "mixed" and rank % 2 == 0)
+        shard = (DevOracleShard if dev else OracleShard)(cells[lo:hi], slip=slip)
     for _ in range(solves):
         res = solve_sharded(shard, reducer=red)
     V = getattr(shard, "V", None)
     pi = getattr(shard, "pi", None)
-    out[rank] = (res["sweeps"], res["allreduces"], V, pi, lo, hi, res["host_reads"], red.calls)
+    out[rank] = (res["sweeps"], res["allreduces"], V, pi, lo, hi, res["host_reads"], red.calls,
+                 getattr(shard, "_mgdp_protocol", (None, None))[1])
     dist.barrier()
     dist.destroy_process_group()
 
@@ -126,10 +130,13 @@ def test_two_rank_gloo_matches_global_loop(slip):
     cells = np.stack([cells_from_enc(e) for e in g["enc"][:12]])
     ref = oracle.value_iteration(0, cells, slip_p=slip)
     out = run_world(cells, 2, slip)
-    for rank, (k, nred, V, pi, lo, hi, reads, _) in out.items():
+    for rank, (k, nred, V, pi, lo, hi, reads, _, proto) in out.items():
         assert k == ref["sweeps"]
-        assert nred == 2  # one all-reduce for K, one for dV: the contraction holds in fp64
-        assert reads == 2  # host protocol: each all-reduce is read back
+        assert proto is False  # gloo + host-only shards: the host protocol on every rank
+        # deterministic: every grid ends its own rule at an exact fixed point, so one all-reduce of
+        # {K, own-rule dV} settles the solve; slip: a second one for dV at K (the contraction holds in fp64)
+        assert nred == (1 if slip is None else 2)
+        assert reads == nred  # host protocol: each all-reduce is read back
         np.testing.assert_array_equal(V, ref["V"][lo:hi])
         np.testing.assert_array_equal(pi, ref["pi"][lo:hi])
 
@@ -144,10 +151,44 @@ def test_device_protocol_uneven_shards_one_host_read(world, n):
     ref = oracle.value_iteration(0, cells)
     out = run_world(cells, world, device_proto=True, solves=2)
     assert len(out) == world
-    for rank, (k, nred, V, pi, lo, hi, reads, total_calls) in out.items():
+    for rank, (k, nred, V, pi, lo, hi, reads, total_calls, proto) in out.items():
         assert k == ref["sweeps"], (rank, k)
-        assert nred == 2 and reads == 1
-        assert total_calls == 4  # two solves on one reducer
+        assert proto is True
+        assert nred == 1 and reads == 1  # deterministic grids: one all-reduce, one host wait
+        assert total_calls == 2  # two solves on one reducer (the one-time agreement not counted)
+        if hi > lo:
+            np.testing.assert_array_equal(V, ref["V"][lo:hi])
+            np.testing.assert_array_equal(pi, ref["pi"][lo:hi])
+
+
+@pytest.mark.parametrize("world,n,slip", [(4, 3, None), (8, 5, 0.9), (4, 9, None)])
+def test_protocol_agreement_with_host_only_peers(world, n, slip):
+    """More ranks than grids (EmptyShards) next to shards that can only run the host protocol, and
+    device-capable shards next to host-only ones ("mixed"): every rank must take the SAME protocol
+    (one MIN all-reduce of a capability flag), else the ranks would issue different collectives."""
+    g = load("grids_fourrooms.npz")
+    cells = np.stack([cells_from_enc(e) for e in g["enc"][:n]])
+    ref = oracle.value_iteration(0, cells, slip_p=slip)
+    out = run_world(cells, world, slip=slip, device_proto="mixed")
+    for rank, (k, nred, V, pi, lo, hi, reads, _, proto) in out.items():
+        assert k == ref["sweeps"], (rank, k)
+        assert proto is False, rank
+        if hi > lo:
+            np.testing.assert_array_equal(V, ref["V"][lo:hi])
+            np.testing.assert_array_equal(pi, ref["pi"][lo:hi])
+
+
+@pytest.mark.parametrize("world,n", [(4, 6), (8, 5)])
+def test_device_protocol_slip_second_allreduce(world, n):
+    """Slip grids end their own rule above an exact fixed point (dV > 0): the device protocol then
+    all-reduces dV at K as well -- two all-reduces, two host reads -- and still equals the global loop."""
+    g = load("grids_lava11n5.npz")
+    cells = np.stack([cells_from_enc(e) for e in g["enc"][:n]])
+    ref = oracle.value_iteration(0, cells, slip_p=0.9)
+    out = run_world(cells, world, slip=0.9, device_proto=True)
+    for rank, (k, nred, V, pi, lo, hi, reads, _, proto) in out.items():
+        assert k == ref["sweeps"], (rank, k)
+        assert proto is True and nred >= 2 and reads >= 2
         if hi > lo:
             np.testing.assert_array_equal(V, ref["V"][lo:hi])
             np.testing.assert_array_equal(pi, ref["pi"][lo:hi])
@@ -159,7 +200,7 @@ def test_host_protocol_uneven_shards(world):
     cells = np.stack([cells_from_enc(e) for e in g["enc"][:11]])
     ref = oracle.value_iteration(0, cells, slip_p=0.9)
     out = run_world(cells, world, slip=0.9)
-    for rank, (k, nred, V, pi, lo, hi, reads, _) in out.items():
+    for rank, (k, nred, V, pi, lo, hi, reads, _, _) in out.items():
         assert k == ref["sweeps"]
         np.testing.assert_array_equal(V, ref["V"][lo:hi])
         np.testing.assert_array_equal(pi, ref["pi"][lo:hi])
@@ -183,6 +224,13 @@ class _FakeReducer:
     def max(self, x):
         self.calls += 1
         return x
+
+    def max2(self, a, b):
+        self.calls += 1
+        return a, b
+
+    def min_flag(self, flag):
+        return flag
 
 
 class _NonMonotoneShard:
@@ -232,15 +280,20 @@ class _FakeDeviceReducer(_FakeReducer):
     def max_(self, t):
         self.calls += 1
 
+    def min_flag(self, flag):
+        return flag
+
 
 class _NonMonotoneDevShard(_NonMonotoneShard):
     protocol_device = property(lambda self: __import__("torch").device("cpu"))
 
     def run_local_dev(self, pub):
         pub[0] = self.run_local()
+        pub[1] = double_to_bits(5e-7)  # own-rule dV below tol but not an exact fixed point
 
-    def run_to_dev(self, k, pub):
-        pub[1] = double_to_bits(self.run_to(int(k[0])))
+    def run_to_dev_sync(self, kdv):
+        k = int(kdv[0])
+        return k, self.run_to(k), bits_to_double(int(kdv[1]))
 
     def set_result(self, k, dv):
         self.k = k
@@ -251,4 +304,18 @@ def test_device_protocol_fallback_loop():
     red = _FakeDeviceReducer()
     res = solve_sharded(s, reducer=red)
     assert res["sweeps"] == 5 and res["converged"] and s.final[0] == 5
-    assert res["allreduces"] == 4 and res["host_reads"] == 3  # 1 device read + 2 fallback sweeps
+    # {K, E} and dV(K) all-reduced on the device, then 2 fallback sweeps on the host
+    assert res["allreduces"] == 4 and res["host_reads"] == 4
+
+
+class _BrokenFixedPointShard(_NonMonotoneDevShard):
+    """Claims an exact fixed point at its own stop, yet dV at K is not 0: the protocol must refuse."""
+
+    def run_local_dev(self, pub):
+        pub[0] = self.run_local()
+        pub[1] = 0
+
+
+def test_device_protocol_refuses_broken_fixed_point():
+    with pytest.raises(RuntimeError, match="fixed-point invariant"):
+        solve_sharded(_BrokenFixedPointShard(), reducer=_FakeDeviceReducer())

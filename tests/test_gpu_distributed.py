@@ -52,7 +52,9 @@ def test_two_ranks_match_single_device(env_id, slip, method):
     mp.spawn(_worker, args=(2, _port(), encs, kw, out), nprocs=2, join=True)
     for rank, (k, nred, V, pi, lo, hi) in dict(out).items():
         assert k == ref.sweeps
-        assert nred >= 2
+        # gloo with GPU handles: the host protocol.  Deterministic grids end their own rule at an
+        # exact fixed point: one all-reduce of {K, own-rule dV}; slip grids also all-reduce dV at K
+        assert nred == 1 if slip is None else nred >= 2
         np.testing.assert_array_equal(V, ref.V[lo:hi])
         np.testing.assert_array_equal(pi, ref.pi[lo:hi])
 
@@ -68,12 +70,13 @@ from minigrid_dynamicprogramming_amd.distributed import Reducer, bits_to_double,
 
 mode = sys.argv[2]
 env_id, B, dtype = sys.argv[3], int(sys.argv[4]), sys.argv[5]
+slip = float(sys.argv[6]) if len(sys.argv) > 6 else None
 cells = gen.generate(env_id, 0, B, enc=False, cells=True, agent=False)["cells"]
-ref = mg.ValueIteration(cells, dtype=dtype)
+ref = mg.ValueIteration(cells, dtype=dtype, slip_p=slip)
 k_ref = ref.solve()
 V_ref, pi_ref = ref.values(), ref.policy()
 ref.close()
-vi = mg.ValueIteration(cells, dtype=dtype)
+vi = mg.ValueIteration(cells, dtype=dtype, slip_p=slip)
 if mode == "steps":
     # the C entry points alone, on a torch stream: K and dV stay in device memory between launches
     s = torch.cuda.Stream()
@@ -90,13 +93,35 @@ if mode == "steps":
             vi.set_result(k, dv)
             vi.finish(k, dv)
             assert np.array_equal(vi.values(), V_ref) and np.array_equal(vi.policy(), pi_ref)
+elif mode == "sync":
+    # run_local_dev, then run_to_dev_sync: K read on the device, the result and p[1] (the own-rule
+    # dV; all-reduced in a real run) come back through host-mapped words, no stream synchronisation
+    s = torch.cuda.Stream()
+    vi.bind_stream(s.cuda_stream)
+    p = torch.zeros(8, dtype=torch.int64, device="cuda")
+    with torch.cuda.stream(s):
+        for rep in range(3):
+            vi.reset()
+            vi.run_local_dev(p[0:4])
+            k, dv, rule = vi.run_to_dev_sync(p[0:2])
+            # deterministic grids end their own rule at an exact fixed point: own-rule dV and dV(K) are 0
+            assert k == k_ref and dv == 0.0 and rule == 0.0, (k, dv, rule, k_ref)
+            assert vi.local_result()[0] == k
+            vi.set_result(k, dv)
+            vi.finish(k, dv)
+            assert np.array_equal(vi.values(), V_ref) and np.array_equal(vi.policy(), pi_ref)
 else:
     import torch.distributed as dist
     dist.init_process_group("nccl", device_id=torch.device("cuda", 0))  # RCCL, one rank
     red = Reducer(timing=True)
     for rep in range(3):
         res = solve_sharded(vi, reducer=red)
-        assert res["sweeps"] == k_ref and res["allreduces"] == 2 and res["host_reads"] == 1, res
+        # deterministic grids: one all-reduce of {K, own-rule dV} and one host wait per solve; slip
+        # grids also all-reduce dV at K
+        if slip is None:
+            assert res["sweeps"] == k_ref and res["allreduces"] == 1 and res["host_reads"] == 1, res
+        else:
+            assert res["sweeps"] == k_ref and res["allreduces"] >= 2 and res["host_reads"] >= 2, res
         assert np.array_equal(vi.values(), V_ref) and np.array_equal(vi.policy(), pi_ref)
     torch.cuda.synchronize()
     print("allreduce device ms", red.collect(), "calls", red.calls)
@@ -106,14 +131,15 @@ print("device protocol ok")
 """
 
 
-@pytest.mark.parametrize("mode", ["steps", "rccl1"])
+@pytest.mark.parametrize("mode", ["steps", "sync", "rccl1"])
 @pytest.mark.parametrize("env_id,B,dtype", [("MiniGrid-LavaCrossingS11N5-v0", 2048, "f32"),
                                             ("MiniGrid-FourRooms-v0", 300, "f64"),
                                             ("MiniGrid-DoorKey-16x16-v0", 700, "f32"),
                                             ("MiniGrid-Empty-16x16-v0", 1, "f32")])
 def test_device_protocol(mode, env_id, B, dtype):
     """mgdp_vi_run_local_dev / run_to_dev / set_result: K and dV in a device buffer, read once.
-    "steps": the entry points on a torch stream; "rccl1": distributed.solve_sharded over a one-rank
+    "steps": the entry points on a torch stream; "sync": run_local_dev + run_to_dev_sync (result via
+    host-mapped words); "rccl1": distributed.solve_sharded over a one-rank
     RCCL group (the all-reduces are real RCCL collectives ordered on the protocol stream).  Batches
     on both sides of the in-kernel-reduce limit (512) and a lone grid; equal to a one-device solve."""
     import subprocess
@@ -124,4 +150,19 @@ def test_device_protocol(mode, env_id, B, dtype):
                LOCAL_RANK="0")
     r = subprocess.run([sys.executable, "-c", _DEVICE_PROTO, root, mode, env_id, str(B), dtype], capture_output=True,
                        text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "device protocol ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("B", [300, 2048])
+def test_device_protocol_rccl1_slip(B):
+    """Slip grids over a one-rank RCCL group: the own-rule dV is not an exact fixed point, so the
+    protocol all-reduces dV at K too (two collectives) and still equals a one-device solve."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "-c", _DEVICE_PROTO, root, "rccl1", "MiniGrid-LavaCrossingS11N5-v0", str(B),
+                        "f32", "0.9"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "device protocol ok" in r.stdout, r.stdout + r.stderr

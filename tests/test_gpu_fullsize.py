@@ -26,9 +26,13 @@ CONFIGS = {
     "fourrooms4096": ("MiniGrid-FourRooms-v0", 4096, "xyd"),
     "lava65536": ("MiniGrid-LavaCrossingS11N5-v0", 65536, "xyd"),
     "doorkey16x65536": ("MiniGrid-DoorKey-16x16-v0", 65536, "doorkey"),
+    # fp64 DoorKey batches above the in-kernel-reduce limit (512) run the has_key-split loop
+    # (fused_dk_half), vi_reduce_multi_kernel and the chained launches: bench.py's f64 side line of
+    # doorkey65536 is exactly this path (seeds 0..16383 of the same generator)
+    "doorkey16x16384": ("MiniGrid-DoorKey-16x16-v0", 16384, "doorkey"),
 }
 CASES = [("fourrooms4096", "f32"), ("fourrooms4096", "f64"), ("lava65536", "f32"), ("lava65536", "f64"),
-         ("doorkey16x65536", "f32")]
+         ("doorkey16x65536", "f32"), ("doorkey16x16384", "f64")]
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 

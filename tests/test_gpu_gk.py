@@ -1,0 +1,75 @@
+"""The launch-wide global rule (GkCtx in csrc/vi_loops.h): a batch whose grid waves are all resident
+runs the global stopping rule inside ONE launch -- each grid at its own stopping sweep arrives at a
+launch-wide counter, grids at an exact fixed point keep sweeping until they have done the global K
+sweeps -- and the separate run_to launch is skipped.  Against the oracle's global loop (sweeps, V and
+pi bit-exact), with the rule on, off (MGDP_GK=0), and forced onto its fallback (MGDP_GK_CAP=1: a
+waiting grid gives up after one extra sweep and the run_to launch finishes the job)."""
+import os
+
+import numpy as np
+import pytest
+
+import minigrid_dynamicprogramming_amd as mg
+from minigrid_dynamicprogramming_amd import gen
+from oracle import oracle
+from tests.test_gpu_wave2 import random_grids
+
+pytestmark = pytest.mark.gpu
+
+
+def _solve_timed(cells, dtype, env, solves=2):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        vi = mg.ValueIteration(cells, dtype=dtype)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    try:
+        vi.enable_timing(True)
+        for _ in range(solves):
+            k = vi.solve()
+        _, launches = vi.kernel_time()
+        return k, vi.values(), vi.policy(), launches / solves
+    finally:
+        vi.close()
+
+
+@pytest.mark.parametrize("env,launches", [({}, 1), ({"MGDP_GK": "0"}, 2), ({"MGDP_GK_CAP": "1"}, 2)])
+@pytest.mark.parametrize("B,W,H,dtype", [(37, 16, 16, "f32"), (600, 11, 11, "f32"), (300, 19, 19, "f64"),
+                                         (2000, 9, 7, "f32")])
+def test_launch_wide_rule_matches_oracle(B, W, H, dtype, env, launches):
+    cells = random_grids(B, W, H, seed=B + W, goals=2)
+    o = oracle.value_iteration(0, cells, dtype=dtype, nthreads=8)
+    k, V, pi, per_solve = _solve_timed(cells, dtype, env)
+    assert k == o["sweeps"]
+    np.testing.assert_array_equal(pi, o["pi"])
+    np.testing.assert_array_equal(V, o["V"])
+    # deterministic grids: the own-rule launch leaves every grid at K (one launch per solve); off or
+    # capped: run_to runs too (MGDP_GK_CAP=1 can only leave some grid below K when K > k_e + 1)
+    if env.get("MGDP_GK_CAP") == "1":
+        assert per_solve in (1, 2)
+    else:
+        assert per_solve == launches, per_solve
+
+
+def test_fourrooms4096_one_launch_per_solve():
+    cells = gen.generate("MiniGrid-FourRooms-v0", 0, 4096, enc=False, cells=True, agent=False)["cells"]
+    o = oracle.value_iteration(0, cells, dtype="f32", nthreads=16)
+    k, V, pi, per_solve = _solve_timed(cells, "f32", {}, solves=3)
+    assert k == o["sweeps"] and per_solve == 1
+    assert np.array_equal(V, o["V"]) and np.array_equal(pi, o["pi"])
+
+
+def test_slip_grids_are_not_fixed_points_and_fall_back():
+    # slip batches do not take the one-wave path at all; a deterministic batch capped by max_sweeps
+    # stops every grid on the cap (no fixed point claimed): run_to / the cap path stay exact
+    cells = random_grids(64, 16, 16, seed=3)
+    r = mg.value_iteration(cells, dtype="f64", max_sweeps=12, tol=1e-300)
+    o = oracle.value_iteration(0, cells, dtype="f64", max_sweeps=12, tol=1e-300)
+    assert r.sweeps == o["sweeps"]
+    np.testing.assert_array_equal(r.V, o["V"])
+    np.testing.assert_array_equal(r.pi, o["pi"])

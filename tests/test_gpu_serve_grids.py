@@ -150,3 +150,81 @@ def test_solve_last_dismisses_the_server_and_the_next_solve_relaunches():
         np.testing.assert_array_equal(vi.result().V, o["V"])
     finally:
         vi.close()
+
+
+def _hip_runtime():
+    """The HIP runtime this process already loaded (PyTorch's and libmgdp's are the same one)."""
+    import ctypes
+
+    for line in open("/proc/self/maps"):
+        if "libamdhip64" in line:
+            return ctypes.CDLL(line.split()[-1])
+    raise RuntimeError("libamdhip64 not loaded")
+
+
+def _raw_read(hip, dptr, nbytes, dtype):
+    """hipMemcpy on the null stream: NOT ordered after the handle's non-blocking stream, so it sees
+    whatever is in HBM now -- a read that is only correct if synchronize() really drained."""
+    import ctypes
+
+    out = np.empty(nbytes // np.dtype(dtype).itemsize, dtype)
+    assert hip.hipMemcpy(out.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(dptr), ctypes.c_size_t(nbytes), 2) == 0
+    return out
+
+
+@pytest.mark.parametrize("then", ["sweep", "load_device"])
+def test_synchronize_after_solve_last_then_other_work(then):
+    """solve(last=True) leaves the departing server as the stream's last work; a later non-served
+    enqueue (a fused sweep, a device-to-device grid copy) must end the synchronize() shortcut on the
+    server's exit word: after synchronize() the raw HBM contents are final (round-2 advisor finding)."""
+    import ctypes
+
+    cells = family_cells("MiniGrid-LavaCrossingS11N5-v0", [3, 4])
+    vi = mg.ValueIteration(cells[:1], dtype="f32", slip_p=0.9)
+    hip = _hip_runtime()
+    try:
+        assert vi.persistent
+        vi.solve()
+        dV, dpi = ctypes.c_void_p(), ctypes.c_void_p()
+        mg._lib.check(vi.L.mgdp_vi_device_buffers(vi.h, ctypes.byref(dV), ctypes.byref(dpi)), "device_buffers")
+        for rep in range(4):
+            k = vi.solve(last=True)
+            if then == "sweep":
+                vi.sweep()  # one more Jacobi sweep on the non-served fused path: V_{k+1}
+                o = oracle.value_iteration(0, cells[:1], dtype="f32", slip_p=0.9, tol=-1.0, max_sweeps=k + 1)
+            else:
+                dev = torch.from_numpy(cells[1:2]).cuda()
+                torch.cuda.synchronize()
+                vi.load_device(dev.data_ptr())  # the server has left: a stream-ordered copy
+                o = None
+            vi.synchronize()
+            if o is not None:
+                V = _raw_read(hip, dV.value, vi.S * 4, np.float32)
+                pi = _raw_read(hip, dpi.value, vi.S, np.int8)
+                np.testing.assert_array_equal(V, o["V"][0])
+                np.testing.assert_array_equal(pi, o["pi"][0])
+            else:
+                assert vi.solve() == oracle.value_iteration(0, cells[1:2], dtype="f32", slip_p=0.9)["sweeps"]
+                vi.load(cells[:1])
+    finally:
+        vi.close()
+
+
+def test_load_device_on_a_bound_stream_is_ordered_after_the_producer():
+    """A handle bound to a caller stream takes device grids by a copy on that stream, so a grid
+    written by a kernel enqueued there just before is the one solved (round-2 advisor finding)."""
+    cells = family_cells("MiniGrid-FourRooms-v0", [8, 9])
+    s = torch.cuda.Stream()
+    vi = mg.ValueIteration(cells[:1], dtype="f32", stream=s.cuda_stream)
+    try:
+        check(vi, cells[:1], 0, "f32")
+        vi.solve()  # server resident on the caller's stream
+        src = torch.from_numpy(cells[1:2]).cuda()
+        buf = torch.zeros_like(src)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s):
+            buf.copy_(src)  # the producer, enqueued on the bound stream
+            vi.load_device(buf.data_ptr())
+        check(vi, cells[1:2], 0, "f32")
+    finally:
+        vi.close()
