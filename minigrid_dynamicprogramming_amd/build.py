@@ -15,8 +15,12 @@ ARCH = os.environ.get("MGDP_ARCH", "gfx950")
 # -ffp-contract=off: no FMA contraction, so fp32/fp64 arithmetic matches the CPU oracle bit for bit.
 # Device code: -fno-honor-nans (V, Q and rewards are finite by construction), which lets max/min
 # select v_max_f32 directly instead of canonicalising both operands first under IEEE mode.
+# Device code: -fno-slp-vectorize -- the SLP vectorizer packed the batched loops' independent f32
+# multiplies and differences into v_pk_mul_f32 / v_pk_add_f32, which measured 5-23 % slower on
+# MI355X than the scalar form (FourRooms x 4096 1.33 -> 1.64e13 updates/s unpacked;
+# profiles/r03_slp_gk/).
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Xarch_device", "-fno-honor-nans",
-         f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result"]
+         "-Xarch_device", "-fno-slp-vectorize", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result"]
 
 
 def needs_build() -> bool:
@@ -37,7 +41,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return OUT
     objdir = os.path.join(os.path.dirname(OUT) if os.environ.get("MGDP_BUILD_OUT") else HERE, "build")
     os.makedirs(objdir, exist_ok=True)
-    cflags = [f for f in FLAGS if f != "-shared"]
+    # MGDP_EXTRA_FLAGS: compile-time knobs of an A/B build (e.g. -DMGDP_LAZY_STOP=0), with MGDP_BUILD_OUT
+    cflags = [f for f in FLAGS if f != "-shared"] + os.environ.get("MGDP_EXTRA_FLAGS", "").split()
     jobs = []
     for src in SOURCES:
         obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")

@@ -881,8 +881,8 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     al((void **)&vi->d_red, sizeof(unsigned long long) * (kRedShards * 4 + 2));
     al((void **)&vi->d_pub1, sizeof(unsigned long long) * 4);
     if (vi->gk) {
-        al((void **)&vi->d_gk, sizeof(unsigned long long) * kGkWords);
-        if (e == hipSuccess) e = hipMemset(vi->d_gk, 0, sizeof(unsigned long long) * kGkWords);
+        al((void **)&vi->d_gk, sizeof(unsigned long long) * gk_words(d.B));
+        if (e == hipSuccess) e = hipMemset(vi->d_gk, 0, sizeof(unsigned long long) * gk_words(d.B));
     }
     if (d.horizon > 0) {
         al(&vi->d_rgoal, (size_t)d.horizon * vi->tsize);

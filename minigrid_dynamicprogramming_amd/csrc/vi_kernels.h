@@ -61,9 +61,9 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
                         (unsigned long long)kk, epoch);
         };
         if (k_target < 0) {
-            const GkCtx g{gk, epoch, e, geo.B, gk_cap};  // the launch-wide rule when the host passed its buffer
+            // the launch-wide rule when the host passed its buffer (buf == nullptr: off)
             fused_wave2_xyd<T, true, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2,
-                                        gk ? &g : nullptr);
+                                        GkCtx{gk, epoch, e, geo.B, gk_cap});
         } else {
             fused_wave2_xyd<T, false, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
         }

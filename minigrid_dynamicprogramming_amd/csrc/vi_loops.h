@@ -594,56 +594,84 @@ __host__ __device__ inline int wave2_smem_bytes(int HWp, int W, int P, int tsize
 }
 // One launch for the whole global rule (mgdp_vi_solve / run_local on a batch whose waves are all
 // resident at once; the host enables it only then): each grid wave, at its own stopping sweep k_e,
-// arrives at a launch-wide counter (64 shards by blockIdx & 63 folded into a top word, every access
-// an agent-scope atomic); the last arrival publishes K = max k_e, tagged with the launch epoch, to
-// 64 replicas on separate 128-B lines.  A grid that ended its own rule at an EXACT fixed point
-// (|dV| = 0: V_k == V_{k-1} bit for bit, so every later sweep reproduces it) keeps sweeping, polling
-// its replica once per sweep, until it has done at least K sweeps: every grid performs the K sweeps
-// of the global rule inside this launch, and the separate run_to launch of the batch is not needed.
+// arrives: it stores k_e to its slot, then draws a ticket of its shard's counter (256 shards by
+// e % 256, each counter on its own 128-B line, so at most B / 256 arrivals contend per line); a
+// shard's last arrival reduces its grids' slots into a shard slot and draws a ticket of the top
+// counter, whose last arrival reduces the shard slots to K = max k_e and publishes K, tagged with
+// the launch epoch, to 512 replicas on separate 128-B lines (a waiting wave polls replica e % 512).  Slots are stored and loaded agent-scope
+// (sc1) and every store is drained before the ticket that announces it (MI355X_MICROARCH.md:
+// inter-workgroup hand-off).  A grid that ended its own rule at an EXACT fixed point (|dV| = 0:
+// V_k == V_{k-1} bit for bit, so every later sweep reproduces it) keeps sweeping, polling its
+// replica once per sweep, until it has done at least K sweeps: every grid performs the K sweeps of
+// the global rule inside this launch, and the separate run_to launch of the batch is not needed.
 // A grid that is not at a fixed point (fp rounding, max_sweeps) stops at k_e as before, and so does
 // a waiting grid after `cap` extra sweeps without K (residency not as planned): the host's run_to
 // launch then takes every grid below K to exactly K.  Reported sweeps (kenv): K if the grid reached
 // it (its V / pi are V_K / pi_K: identical past the fixed point), else its own k_e.
 struct GkCtx {
-    unsigned long long *buf;  // kGkWords: shards [64][16] (count, kmax), top [16], replicas [64][16]
+    unsigned long long *buf;  // gk_words(B) u64: counters, top, replicas, shard slots, grid slots
     unsigned int epoch;
     int e;                    // grid (workgroup) index
     int B;                    // grids in the launch
     int cap;                  // extra sweeps a waiting fixed-point grid may do without seeing K
 };
-constexpr int kGkShards = 64;
-constexpr int kGkLine = 16;  // u64 words per 128-B line
-constexpr int kGkWords = (2 * kGkShards + 1) * kGkLine;
+constexpr int kGkShards = 256;
+constexpr int kGkReplicas = 512;  // a replica line per 8 polling waves of a 4096-grid launch
+constexpr int kGkLine = 16;                                    // u64 words per 128-B line
+constexpr int kGkTop = kGkShards * kGkLine;                    // top counter line
+constexpr int kGkRep = kGkTop + kGkLine;                       // replica lines
+constexpr int kGkSslot = kGkRep + kGkReplicas * kGkLine;       // int32 [kGkShards] shard maxima
+constexpr int kGkKslot = kGkSslot + kGkShards / 2;             // int32 [B] grid stopping sweeps
+__host__ __device__ inline int gk_words(int B) { return kGkKslot + (B + 1) / 2; }
 
-// Lane 0: count this grid's arrival with its own stopping sweep; the launch's last arrival
-// publishes K to the replicas.
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+}
+
+// The whole wave (uniform call): count this grid's arrival with its own stopping sweep; the
+// launch's last arrival publishes K to the replicas.
 __device__ __forceinline__ void gk_arrive(const GkCtx &g, int k_e) {
-    unsigned long long *sh = g.buf + (g.e & (kGkShards - 1)) * kGkLine;
-    unsigned long long *top = g.buf + kGkShards * kGkLine;
+    const int lane = (int)threadIdx.x & 63;
+    int *kslot = reinterpret_cast<int *>(g.buf + kGkKslot);
+    int *sslot = reinterpret_cast<int *>(g.buf + kGkSslot);
     const int nsh = g.B < kGkShards ? g.B : kGkShards;
-    const int s = g.e & (kGkShards - 1);
-    const unsigned int size = (unsigned int)(g.B / kGkShards + (s < g.B % kGkShards ? 1 : 0));
-    const unsigned long long a = __hip_atomic_fetch_max(sh + 1, (unsigned long long)k_e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" :: "v"(a) : "memory");
-    const unsigned long long t = __hip_atomic_fetch_add(sh, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t != size - 1) return;
-    // the shard's last arrival: fold it into the top word (and re-arm the shard for the next launch)
-    const unsigned long long km = __hip_atomic_exchange(sh + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_exchange(sh, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long b = __hip_atomic_fetch_max(top + 1, km, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" :: "v"(b) : "memory");
-    const unsigned long long t2 = __hip_atomic_fetch_add(top, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t2 != (unsigned long long)(nsh - 1)) return;
-    const unsigned long long K = __hip_atomic_exchange(top + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_exchange(top, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long w = ((unsigned long long)g.epoch << 32) | (K & 0xffffffffull);
-    unsigned long long *rep = g.buf + (kGkShards + 1) * kGkLine;
-    for (int r = 0; r < kGkShards; ++r) __hip_atomic_store(rep + r * kGkLine, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int s = g.e % nsh;
+    const int size = g.B / nsh + (s < g.B % nsh ? 1 : 0);
+    unsigned long long t = 0;
+    if (lane == 0) {
+        __hip_atomic_store(kslot + g.e, k_e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        t = __hip_atomic_fetch_add(g.buf + s * kGkLine, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (__builtin_amdgcn_readfirstlane((unsigned int)t) != (unsigned int)(size - 1)) return;
+    // the shard's last arrival: every slot of the shard was drained before its ticket
+    int m = 0;
+    for (int i = lane; i < size; i += 64)
+        m = max(m, __hip_atomic_load(kslot + s + i * nsh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    m = wave_max_i(m);
+    unsigned long long t2 = 0;
+    if (lane == 0) {
+        __hip_atomic_exchange(g.buf + s * kGkLine, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+        __hip_atomic_store(sslot + s, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        t2 = __hip_atomic_fetch_add(g.buf + kGkTop, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (__builtin_amdgcn_readfirstlane((unsigned int)t2) != (unsigned int)(nsh - 1)) return;
+    int K = 0;
+    for (int i = lane; i < nsh; i += 64)
+        K = max(K, __hip_atomic_load(sslot + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    K = wave_max_i(K);
+    if (lane == 0) __hip_atomic_exchange(g.buf + kGkTop, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long w = ((unsigned long long)g.epoch << 32) | (unsigned int)K;
+    for (int r = lane; r < kGkReplicas; r += 64)
+        __hip_atomic_store(g.buf + kGkRep + r * kGkLine, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // K of this launch if published yet (wave-uniform), else -1.
 __device__ __forceinline__ int gk_poll(const GkCtx &g) {
-    const unsigned long long *rep = g.buf + (kGkShards + 1 + (g.e & (kGkShards - 1))) * kGkLine;
+    const unsigned long long *rep = g.buf + kGkRep + (g.e & (kGkReplicas - 1)) * kGkLine;
     unsigned long long w = 0;
     if ((threadIdx.x & 63) == 0) w = __hip_atomic_load(rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned int hi = __builtin_amdgcn_readfirstlane((unsigned int)(w >> 32));
@@ -654,7 +682,7 @@ __device__ __forceinline__ int gk_poll(const GkCtx &g) {
 template <typename T, bool LOCAL, int P, typename Done>
 __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *tile,
                                                 const T *Vg, T *Vg_out, int8_t *pig, int &k, int k_target,
-                                                double &dvl, const Done &done, const GkCtx *gk = nullptr) {
+                                                double &dvl, const Done &done, const GkCtx gk = GkCtx{}) {
     static_assert(P >= 1 && P <= 8, "goal bits: 4 per cell, 32 per lane");
     const int lane = (int)threadIdx.x;
     const int W = geo.W, padw = wave2_padw(W);
@@ -700,12 +728,12 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
         if (k_e < 0) {
             k_e = k;
             fixed = wave_max(diff) == (T)0;
-            if (lane == 0) gk_arrive(*gk, k_e);
+            gk_arrive(gk, k_e);
         }
         if (!fixed || at_cap) return false;
-        if (K_seen < 0) K_seen = gk_poll(*gk);
+        if (K_seen < 0) K_seen = gk_poll(gk);
         if (K_seen >= 0) return k < K_seen;
-        return k - k_e < gk->cap;
+        return k - k_e < gk.cap;
     };
     auto sweep = [&](const T (&in)[P][4], T (&out)[P][4]) -> bool {  // `out` written only on commit
         T FS[P], FN[P];
@@ -717,7 +745,7 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
         if (LOCAL) {
             const bool at_cap = k >= geo.max_sweeps;
             if (at_cap || (k > k_start && !more)) {
-                if (gk == nullptr || !gk_go(at_cap)) return false;
+                if (gk.buf == nullptr || !gk_go(at_cap)) return false;
             }
         } else if (k >= k_target) {
             return false;
@@ -786,10 +814,10 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
         }
     }
     dvl = (double)wave_max(diff);
-    if (LOCAL && gk != nullptr) {
+    if (LOCAL && gk.buf != nullptr) {
         if (k_e < 0) {  // (a launch that stopped before any rule fired cannot happen: k_start = 0)
             k_e = k;
-            if (lane == 0) gk_arrive(*gk, k_e);
+            gk_arrive(gk, k_e);
         }
         // sweeps to report: K when reached (V_k = V_K past an exact fixed point), else the own stop
         k = (K_seen >= 0 && k >= K_seen) ? K_seen : k_e;
