@@ -63,7 +63,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
         if (k_target < 0) {
             // the launch-wide rule when the host passed its buffer (buf == nullptr: off)
             fused_wave2_xyd<T, true, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2,
-                                        GkCtx{gk, epoch, e, geo.B, gk_cap});
+                                        GkCtx{gk, epoch, e, geo.B, gk_cap, host_out});
         } else {
             fused_wave2_xyd<T, false, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
         }
@@ -226,7 +226,10 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
     const bool work = fused_grid<T, MODEL, SLIP, MAP, false, WP>(geo, cf, cells, V, pi, kenv, dvenv, host_out, k_target,
                                                                  fresh, lone, epoch, blockIdx.x, k, dvl, nullptr,
                                                                  wp_is_wave2(WP) ? gk : nullptr, gk_cap);
-    if (in_kernel_reduce) fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16), epoch, work);
+    // a launch-wide-rule launch (wave2 with gk) reduces and publishes through its own counter tree
+    const bool gk_pub = wp_is_wave2(WP) && gk != nullptr && k_target < 0 && !k_target_dev;
+    if (in_kernel_reduce && !gk_pub)
+        fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16), epoch, work);
 }
 
 // Persistent solver for a lone grid: one workgroup stays resident and serves solve requests posted

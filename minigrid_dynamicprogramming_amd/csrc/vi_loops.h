@@ -587,6 +587,10 @@ __device__ __forceinline__ void fused_pair_xyd(const Geo &geo, const Coef<T> &cf
 // fused_pair_xyd (invalid states hold +0); the stop rule is the wave's ballot.  Same backups,
 // rule and pi pass as fused_fast_xyd_soa: bit-identical V, pi and sweep counts.
 // LDS: [slots 256 B][cells HWp][tile: pad | plane 3 (64P) | plane 1 (64P) | pad] (wave2_* below).
+// -DMGDP_WAVE2_FRONT=0: the per-state |dV| stop test in fused_wave2_xyd (A/B of the frontier test)
+#ifndef MGDP_WAVE2_FRONT
+#define MGDP_WAVE2_FRONT 1
+#endif
 __host__ __device__ inline int wave2_padw(int W) { return (W + 15) / 16 * 16; }
 __host__ __device__ inline int wave2_tile_off(int HWp) { return 256 + (HWp + 15) / 16 * 16; }
 __host__ __device__ inline int wave2_smem_bytes(int HWp, int W, int P, int tsize) {
@@ -609,24 +613,45 @@ __host__ __device__ inline int wave2_smem_bytes(int HWp, int W, int P, int tsize
 // launch then takes every grid below K to exactly K.  Reported sweeps (kenv): K if the grid reached
 // it (its V / pi are V_K / pi_K: identical past the fixed point), else its own k_e.
 struct GkCtx {
-    unsigned long long *buf;  // gk_words(B) u64: counters, top, replicas, shard slots, grid slots
+    unsigned long long *buf;  // gk_words(B) u64: counters, replicas, shard slots, grid slots (layout below)
     unsigned int epoch;
     int e;                    // grid (workgroup) index
     int B;                    // grids in the launch
     int cap;                  // extra sweeps a waiting fixed-point grid may do without seeing K
+    unsigned long long *pub;  // where the launch's {kmax, dV bits, kmin, epoch} go (host-mapped or device)
 };
 constexpr int kGkShards = 256;
 constexpr int kGkReplicas = 512;  // a replica line per 8 polling waves of a 4096-grid launch
 constexpr int kGkLine = 16;                                    // u64 words per 128-B line
-constexpr int kGkTop = kGkShards * kGkLine;                    // top counter line
+constexpr int kGkTop = kGkShards * kGkLine;                    // arrival: [256 shard lines][top line]
 constexpr int kGkRep = kGkTop + kGkLine;                       // replica lines
-constexpr int kGkSslot = kGkRep + kGkReplicas * kGkLine;       // int32 [kGkShards] shard maxima
-constexpr int kGkKslot = kGkSslot + kGkShards / 2;             // int32 [B] grid stopping sweeps
-__host__ __device__ inline int gk_words(int B) { return kGkKslot + (B + 1) / 2; }
+constexpr int kGkCnt2 = kGkRep + kGkReplicas * kGkLine;        // exit: [256 shard lines][top line]
+constexpr int kGkTop2 = kGkCnt2 + kGkShards * kGkLine;
+constexpr int kGkSslot = kGkTop2 + kGkLine;                    // int32 [256] shard max k_e
+constexpr int kGkSxMin = kGkSslot + kGkShards / 2;             // int32 [256] shard min reported sweeps
+constexpr int kGkSxMax = kGkSxMin + kGkShards / 2;             // int32 [256] shard max reported sweeps
+constexpr int kGkSxDv = kGkSxMax + kGkShards / 2;              // u64 [256] shard max dV bits
+constexpr int kGkKslot = kGkSxDv + kGkShards;                  // int32 [B] own stopping sweeps, then
+__host__ __device__ inline int gk_kr_off(int B) { return kGkKslot + (B + 1) / 2; }  // int32 [B] reported sweeps,
+__host__ __device__ inline int gk_dv_off(int B) { return gk_kr_off(B) + (B + 1) / 2; }  // u64 [B] dV bits
+__host__ __device__ inline int gk_words(int B) { return gk_dv_off(B) + B; }
 
 __device__ __forceinline__ int wave_max_i(int v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long w = __shfl_xor(v, o);
+        v = w > v ? w : v;
+    }
     return v;
 }
 
@@ -667,6 +692,68 @@ __device__ __forceinline__ void gk_arrive(const GkCtx &g, int k_e) {
     const unsigned long long w = ((unsigned long long)g.epoch << 32) | (unsigned int)K;
     for (int r = lane; r < kGkReplicas; r += 64)
         __hip_atomic_store(g.buf + kGkRep + r * kGkLine, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The whole wave, once it has its final answer: the launch's {kmax, dV, kmin} reduced over the same
+// counter tree (a second bank), the last exit publishing it -- the reduce kernel a batch launch
+// otherwise needs, folded into the launch.
+__device__ __forceinline__ void gk_exit(const GkCtx &g, int k_rep, double dv) {
+    const int lane = (int)threadIdx.x & 63;
+    int *kr = reinterpret_cast<int *>(g.buf + gk_kr_off(g.B));
+    unsigned long long *dvr = g.buf + gk_dv_off(g.B);
+    int *smin = reinterpret_cast<int *>(g.buf + kGkSxMin);
+    int *smax = reinterpret_cast<int *>(g.buf + kGkSxMax);
+    unsigned long long *sdv = g.buf + kGkSxDv;
+    const int nsh = g.B < kGkShards ? g.B : kGkShards;
+    const int s = g.e % nsh;
+    const int size = g.B / nsh + (s < g.B % nsh ? 1 : 0);
+    unsigned long long t = 0;
+    if (lane == 0) {
+        __hip_atomic_store(kr + g.e, k_rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(dvr + g.e, (unsigned long long)__double_as_longlong(dv), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        t = __hip_atomic_fetch_add(g.buf + kGkCnt2 + s * kGkLine, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (__builtin_amdgcn_readfirstlane((unsigned int)t) != (unsigned int)(size - 1)) return;
+    int mn = 0x7fffffff, mx = 0;
+    unsigned long long dm = 0;
+    for (int i = lane; i < size; i += 64) {
+        const int x = __hip_atomic_load(kr + s + i * nsh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long y = __hip_atomic_load(dvr + s + i * nsh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mn = min(mn, x);
+        mx = max(mx, x);
+        dm = y > dm ? y : dm;
+    }
+    mn = wave_min_i(mn);
+    mx = wave_max_i(mx);
+    dm = wave_max_u64(dm);
+    unsigned long long t2 = 0;
+    if (lane == 0) {
+        __hip_atomic_exchange(g.buf + kGkCnt2 + s * kGkLine, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(smin + s, mn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(smax + s, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(sdv + s, dm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        t2 = __hip_atomic_fetch_add(g.buf + kGkTop2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (__builtin_amdgcn_readfirstlane((unsigned int)t2) != (unsigned int)(nsh - 1)) return;
+    mn = 0x7fffffff;
+    mx = 0;
+    dm = 0;
+    for (int i = lane; i < nsh; i += 64) {
+        mn = min(mn, __hip_atomic_load(smin + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        mx = max(mx, __hip_atomic_load(smax + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        const unsigned long long y = __hip_atomic_load(sdv + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        dm = y > dm ? y : dm;
+    }
+    mn = wave_min_i(mn);
+    mx = wave_max_i(mx);
+    dm = wave_max_u64(dm);
+    if (lane == 0) {
+        __hip_atomic_exchange(g.buf + kGkTop2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        publish(g.pub, (unsigned long long)mx, dm, (unsigned long long)mn, g.epoch);
+    }
 }
 
 // K of this launch if published yet (wave-uniform), else -1.
@@ -720,15 +807,37 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
     const int k_start = k;
     bool more = true;
     T diff = (T)0;
+#if MGDP_WAVE2_FRONT
+    // The frontier stop test.  Deterministic XYD values are shortest-path powers: a state at
+    // distance d (actions to the goal, the last one entering it) holds P_{d-1} from sweep d on and 0
+    // before (induction: fl(g * x) is monotone and P strictly decreasing, so the max over successors
+    // is the nearest one), and every value that changes at sweep n changes from 0 to P_{n-1}.  So
+    // max |dV| of sweep n is exactly P_{n-1} if any value changed, else 0: the per-state |dV| max
+    // becomes one compare per state (o != in), and P_{n-1} is the scalar recurrence below (table for
+    // the starting sweep).  Bit-identical V, pi, sweep counts and dV to the |dV| form.
+    T pk = cf.ptab[k];     // P_k: the value that sweep k + 1 sets
+    T p_last = (T)0;       // P of the last sweep run
+    bool ch_last = false;  // whether it changed a value
+    (void)diff;
+#endif
     // launch-wide rule (gk): this grid's own stopping sweep (-1: not yet), fixed point, K seen
     int k_e = -1, K_seen = -1;
     bool fixed = false;
     // false: stop before this sweep.  Called when the own rule or max_sweeps says stop.
+    // VALU issue on a SIMD goes by priority, then age (MI355X_MICROARCH.md, "two waves per SIMD"):
+    // grids still converging run at priority 1 and a grid sweeping on past its own fixed point drops
+    // to 0, so its no-op sweeps take only the issue slots the converging grids leave
+    if (LOCAL && gk.buf != nullptr) __builtin_amdgcn_s_setprio(1);
     auto gk_go = [&](bool at_cap) -> bool {
         if (k_e < 0) {
             k_e = k;
+#if MGDP_WAVE2_FRONT
+            fixed = !ch_last;
+#else
             fixed = wave_max(diff) == (T)0;
+#endif
             gk_arrive(gk, k_e);
+            __builtin_amdgcn_s_setprio(0);
         }
         if (!fixed || at_cap) return false;
         if (K_seen < 0) K_seen = gk_poll(gk);
@@ -777,19 +886,33 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
         }
 #pragma unroll
         for (int j = 0; j < P; ++j) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) dm = vmax(dm, vabs(o[j][q] - in[j][q]));
-#pragma unroll
-            for (int q = 0; q < 4; ++q) out[j][q] = o[j][q];
-        }
-#pragma unroll
-        for (int j = 0; j < P; ++j) {
             S1[j * 64 + lane] = o[j][1];
             N3[j * 64 + lane] = o[j][3];
         }
         asm volatile("" ::: "memory");
+#if MGDP_WAVE2_FRONT
+        bool ch = false;
+#pragma unroll
+        for (int j = 0; j < P; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ch |= o[j][q] != in[j][q];
+        ch_last = __ballot(ch) != 0ull;
+        p_last = pk;
+        pk = cf.g * pk;
+        if (LOCAL) more = ch_last && p_last >= cf.tol;
+        (void)dm;
+#else
+#pragma unroll
+        for (int j = 0; j < P; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dm = vmax(dm, vabs(o[j][q] - in[j][q]));
         diff = dm;
         if (LOCAL) more = __ballot(dm >= cf.tol) != 0ull;
+#endif
+#pragma unroll
+        for (int j = 0; j < P; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) out[j][q] = o[j][q];
         ++k;
         return true;
     };
@@ -813,7 +936,11 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
             break;
         }
     }
+#if MGDP_WAVE2_FRONT
+    dvl = ch_last ? (double)p_last : 0.0;
+#else
     dvl = (double)wave_max(diff);
+#endif
     if (LOCAL && gk.buf != nullptr) {
         if (k_e < 0) {  // (a launch that stopped before any rule fired cannot happen: k_start = 0)
             k_e = k;
@@ -821,6 +948,7 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
         }
         // sweeps to report: K when reached (V_k = V_K past an exact fixed point), else the own stop
         k = (K_seen >= 0 && k >= K_seen) ? K_seen : k_e;
+        gk_exit(gk, k, dvl);  // this launch's reduction and its publication (no reduce kernel)
     }
     done(k, dvl);
     // pi of the last sweep = argmax on V_{k-1} (`prev`), per action with the usual topology
