@@ -130,7 +130,6 @@ struct mgdp_vi {
     int gk_cap = 256;             // extra sweeps a fixed-point grid does while K is not yet published
     int gk_capacity = 0;          // resident workgroups of the wave2 kernel on this device
     unsigned long long *d_gk = nullptr;
-    void *d_ptab = nullptr;       // T[max_sweeps + 2]: P_n = fl(g * P_{n-1}), P_0 = 1 (Coef::ptab, wave2 handles)
 };
 
 namespace {
@@ -168,7 +167,6 @@ Coef<T> make_coef(const mgdp_vi *vi) {
     if ((double)t < vi->d.tol) t = std::nextafter(t, std::numeric_limits<T>::infinity());
     c.tol = t;
     c.dc = (T)vi->d.death_cost;
-    c.ptab = reinterpret_cast<const T *>(vi->d_ptab);
     return c;
 }
 
@@ -882,22 +880,6 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     al((void **)&vi->d_shards, sizeof(unsigned long long) * 8 * (size_t)(d.max_sweeps + 1));
     al((void **)&vi->d_red, sizeof(unsigned long long) * (kRedShards * 4 + 2));
     al((void **)&vi->d_pub1, sizeof(unsigned long long) * 4);
-    if (vi->wave2) {  // the frontier values of the deterministic model, in the working type
-        al(&vi->d_ptab, (size_t)(d.max_sweeps + 2) * vi->tsize);
-        if (e == hipSuccess) {
-            std::vector<unsigned char> pt((size_t)(d.max_sweeps + 2) * vi->tsize);
-            if (vi->tsize == 4) {
-                float *q = reinterpret_cast<float *>(pt.data()), g = (float)d.gamma;
-                q[0] = 1.0f;
-                for (int n = 1; n < d.max_sweeps + 2; ++n) q[n] = g * q[n - 1];
-            } else {
-                double *q = reinterpret_cast<double *>(pt.data()), g = d.gamma;
-                q[0] = 1.0;
-                for (int n = 1; n < d.max_sweeps + 2; ++n) q[n] = g * q[n - 1];
-            }
-            e = hipMemcpy(vi->d_ptab, pt.data(), pt.size(), hipMemcpyHostToDevice);
-        }
-    }
     if (vi->gk) {
         al((void **)&vi->d_gk, sizeof(unsigned long long) * gk_words(d.B));
         if (e == hipSuccess) e = hipMemset(vi->d_gk, 0, sizeof(unsigned long long) * gk_words(d.B));
@@ -981,7 +963,6 @@ int mgdp_vi_destroy(mgdp_vi *vi) {
     (void)hipFree(vi->d_red);
     (void)hipFree(vi->d_pub1);
     (void)hipFree(vi->d_gk);
-    (void)hipFree(vi->d_ptab);
     (void)hipFree(vi->d_rgoal);
     (void)hipFree(vi->d_pi_t);
     if (vi->h_out) (void)hipHostFree(vi->h_out);

@@ -587,10 +587,6 @@ __device__ __forceinline__ void fused_pair_xyd(const Geo &geo, const Coef<T> &cf
 // fused_pair_xyd (invalid states hold +0); the stop rule is the wave's ballot.  Same backups,
 // rule and pi pass as fused_fast_xyd_soa: bit-identical V, pi and sweep counts.
 // LDS: [slots 256 B][cells HWp][tile: pad | plane 3 (64P) | plane 1 (64P) | pad] (wave2_* below).
-// -DMGDP_WAVE2_FRONT=0: the per-state |dV| stop test in fused_wave2_xyd (A/B of the frontier test)
-#ifndef MGDP_WAVE2_FRONT
-#define MGDP_WAVE2_FRONT 1
-#endif
 __host__ __device__ inline int wave2_padw(int W) { return (W + 15) / 16 * 16; }
 __host__ __device__ inline int wave2_tile_off(int HWp) { return 256 + (HWp + 15) / 16 * 16; }
 __host__ __device__ inline int wave2_smem_bytes(int HWp, int W, int P, int tsize) {
@@ -807,19 +803,6 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
     const int k_start = k;
     bool more = true;
     T diff = (T)0;
-#if MGDP_WAVE2_FRONT
-    // The frontier stop test.  Deterministic XYD values are shortest-path powers: a state at
-    // distance d (actions to the goal, the last one entering it) holds P_{d-1} from sweep d on and 0
-    // before (induction: fl(g * x) is monotone and P strictly decreasing, so the max over successors
-    // is the nearest one), and every value that changes at sweep n changes from 0 to P_{n-1}.  So
-    // max |dV| of sweep n is exactly P_{n-1} if any value changed, else 0: the per-state |dV| max
-    // becomes one compare per state (o != in), and P_{n-1} is the scalar recurrence below (table for
-    // the starting sweep).  Bit-identical V, pi, sweep counts and dV to the |dV| form.
-    T pk = cf.ptab[k];     // P_k: the value that sweep k + 1 sets
-    T p_last = (T)0;       // P of the last sweep run
-    bool ch_last = false;  // whether it changed a value
-    (void)diff;
-#endif
     // launch-wide rule (gk): this grid's own stopping sweep (-1: not yet), fixed point, K seen
     int k_e = -1, K_seen = -1;
     bool fixed = false;
@@ -831,11 +814,7 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
     auto gk_go = [&](bool at_cap) -> bool {
         if (k_e < 0) {
             k_e = k;
-#if MGDP_WAVE2_FRONT
-            fixed = !ch_last;
-#else
             fixed = wave_max(diff) == (T)0;
-#endif
             gk_arrive(gk, k_e);
             __builtin_amdgcn_s_setprio(0);
         }
@@ -890,25 +869,12 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
             N3[j * 64 + lane] = o[j][3];
         }
         asm volatile("" ::: "memory");
-#if MGDP_WAVE2_FRONT
-        bool ch = false;
-#pragma unroll
-        for (int j = 0; j < P; ++j)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) ch |= o[j][q] != in[j][q];
-        ch_last = __ballot(ch) != 0ull;
-        p_last = pk;
-        pk = cf.g * pk;
-        if (LOCAL) more = ch_last && p_last >= cf.tol;
-        (void)dm;
-#else
 #pragma unroll
         for (int j = 0; j < P; ++j)
 #pragma unroll
             for (int q = 0; q < 4; ++q) dm = vmax(dm, vabs(o[j][q] - in[j][q]));
         diff = dm;
         if (LOCAL) more = __ballot(dm >= cf.tol) != 0ull;
-#endif
 #pragma unroll
         for (int j = 0; j < P; ++j)
 #pragma unroll
@@ -936,11 +902,7 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
             break;
         }
     }
-#if MGDP_WAVE2_FRONT
-    dvl = ch_last ? (double)p_last : 0.0;
-#else
     dvl = (double)wave_max(diff);
-#endif
     if (LOCAL && gk.buf != nullptr) {
         if (k_e < 0) {  // (a launch that stopped before any rule fired cannot happen: k_start = 0)
             k_e = k;

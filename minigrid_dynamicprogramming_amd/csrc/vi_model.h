@@ -22,9 +22,6 @@ struct Coef {
     T g, p, c;  // gamma, slip keep-prob, (1-p)/6   (all rounded to T once on the host)
     T tol;      // smallest T >= tol: for x of type T, x >= tol (T)  <=>  (double)x >= tol
     T dc;       // NoDeath: reward for entering lava (the wrapper's death_cost)
-    // ptab[n] = P_n = fl(g * P_{n-1}), P_0 = 1, n <= max_sweeps: in the deterministic XYD model every
-    // value that changes at sweep n changes from 0 to P_{n-1} (fused_wave2_xyd); nullptr if unused
-    const T *ptab;
 };
 
 template <typename T>
