@@ -7,12 +7,14 @@ immediately) are excluded, matching bench.py's event accounting."""
 import csv
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
 SRC = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 OUT = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_traffic.json"
-# run -> (bench key, kernel, solves per launch for a persistent server launch or None)
+# run -> (bench key, kernel, solves per launch for a persistent server launch or None); the grids one
+# launch solves (bench.py scales traffic to a shard by it) is the number after the last "x" of the key
 RUNS = {
     # --steps 20 --warmup 0: the timed launch serves the 16 priming solves and the 20 timed ones
     "empty16": ("empty16/fused/cell/f32", "vi_serve_kernel", 36),
@@ -31,6 +33,16 @@ RUNS = {
     "gen_fourrooms65536": ("gen_fourrooms65536/gen", "gen_grids_kernel", None),
     "gen_doorkey16x65536": ("gen_doorkey16x65536/gen", "gen_grids_kernel", None),
 }
+
+
+def grids_of(key):
+    """Grids (envs) one launch of the workload handles: the trailing count of its name ("lava65536",
+    "empty16x65536", "step_doorkey16x1m"); a bare family name ("empty16") is the lone grid."""
+    head = key.split("/")[0]
+    m = re.search(r"x(\d+)(m?)$", head) or re.search(r"[a-z](\d{3,})(m?)$", head)
+    if not m:
+        return 1
+    return int(m.group(1)) * ((1 << 20) if m.group(2) else 1)
 
 
 def per_dispatch(path, kernel):
@@ -67,6 +79,7 @@ for run, (key, kernel, solves) in RUNS.items():
     if run.startswith(("step_", "gen_")):
         res[key]["note"] += "; dword/byte-wide accesses: the x2 is calibrated for 16-B streaming reads only"
         res[key]["src"] = SRC
+    res[key]["grids_per_launch"] = grids_of(key)
     if solves:  # one resident launch served `solves` requests (bench.py scales per solve)
         res[key]["solves_per_launch"] = solves
         res[key]["bytes_per_solve"] = res[key]["bytes_per_launch"] / solves

@@ -4,6 +4,7 @@ bench.py's roofline blocks read: per-launch VALU / LDS wave-instructions, VALU i
 LDS-array busy fraction, wave-cycle split.  Usage: python tools/sq_counters_json.py KEY=SUMMARY..."""
 import json
 import os
+import re
 import sys
 
 OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "sq_counters.json")
@@ -20,6 +21,8 @@ for arg in sys.argv[1:]:
         "lds_array_busy": s.get("lds_array_busy"),
         "wave_split": s.get("wave_split"),
         "avg_dispatch_us_under_pmc": s["avg_dispatch_us"],
+        # the grids one launch solved (bench.py scales per-launch counts to a shard by it)
+        "grids_per_launch": int(re.search(r"(\d+)/", key).group(1)),
         "source": os.path.relpath(path, os.path.dirname(os.path.dirname(OUT))),
     }
 json.dump(res, open(OUT, "w"), indent=1)
