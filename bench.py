@@ -332,6 +332,13 @@ def main():
     local = int(os.environ.get("MGDP_BENCH_DEVICE", local))
     backend = os.environ.get("MGDP_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
+    # The solving (main) thread on the CPUs of its GPU's NUMA node, before any handle exists (its
+    # host-mapped words are allocated by this thread): a served lone-grid solve measured 9.1 us from
+    # the GPU's node and 10.8 us from the other socket (tools/probe_numa.cpp).
+    # MGDP_BENCH_PIN=0 leaves the thread where the scheduler put it.
+    from minigrid_dynamicprogramming_amd import _lib as mglib
+
+    pinned = mglib.pin_host_thread(local) if os.environ.get("MGDP_BENCH_PIN", "1") == "1" else 0
     # MGDP_BENCH_FORCE_DIST=1 (rehearsal, never set by the driver): the process group and the sharded
     # protocol at any world size, so one GPU runs the RCCL all-reduces of the multi-GPU path
     force_dist = os.environ.get("MGDP_BENCH_FORCE_DIST") == "1"
@@ -419,6 +426,7 @@ def main():
             "method": args.method, "mapping": args.mapping,
             "parallelism": (f"shard{world} + RCCL dV all-reduce" if sharded else
                             ("replicas only" if spec["replicate"] else f"independent batches x{world}")),
+            "host_thread": (f"pinned to the GPU's NUMA node ({pinned} CPUs)" if pinned else "unpinned"),
         },
         "sweeps": int(m["sweeps"][-1]),
         "roofline": roofline,

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MGDP_ABI_VERSION 5
+#define MGDP_ABI_VERSION 6
 
 enum {
     MGDP_OK = 0,
@@ -49,6 +49,12 @@ const char *mgdp_last_error(void);
 int mgdp_abi_version(void);
 /* Number of visible HIP devices (0 when none). */
 int mgdp_device_count(int32_t *n);
+/* Restrict the CALLING thread to the CPUs of `device`'s NUMA node (sysfs local_cpulist, within the
+ * thread's current affinity); *ncpus_out = the CPUs kept, 0 if the node is unknown or none of its
+ * CPUs is allowed (the affinity is then left unchanged).  Call it before mgdp_vi_create on the
+ * thread that will solve: a served lone-grid solve polls host memory, and its latency depends on
+ * which socket the polling thread and the handle's host-mapped words live on (ABI 6). */
+int mgdp_pin_host_thread(int32_t device, int32_t *ncpus_out);
 
 /* ---------------------------------------------------------------------------------------------- */
 /* Value iteration over batches of grids (build-defined DP; transition = MiniGridEnv.step,          */

@@ -69,7 +69,10 @@ struct mgdp_vi {
     int inkernel_max = kInKernelReduceMaxB; // batches up to this fold {k, dV} in the fused launch itself (MGDP_INKERNEL_MAX)
     unsigned int *d_ticket = nullptr;       // arrival ticket of the fused reduction
     bool reduce_multi = true;               // B > inkernel_max: vi_reduce_multi_kernel (MGDP_REDUCE_MULTI)
-    unsigned long long *h_out = nullptr;    // host-mapped {kmax, dV bits, kmin, epoch, request}
+    // host-mapped words (kHoutWords): [0..3] {kmax, dV bits, kmin, epoch} of a launch, [5..7] the
+    // server's tagged result, [8..9] trace stamps, [11] server exit word, [13] run_to mirror,
+    // [16] request word and [17] its source word (their own 128-B line: the server polls the pair)
+    unsigned long long *h_out = nullptr;
     unsigned long long *d_hout = nullptr;   // device alias of h_out
     int cur = 0;        // V buffer holding the current V (sweep method)
     int k_min = 0;      // min / max sweeps over grids after the last reduce (fused method)
@@ -94,6 +97,7 @@ struct mgdp_vi {
     int pair = 0;                 // fused XYD: two-sweep step
     int wave_p = 0;               // lone XYD grid on one wave: cells per lane (fused_wave_xyd)
     int cpt = 1;                  // batched XYD fused path: cells per thread (MGDP_CPT; 2 = fused_fast_xyd_soa_x2)
+    int serve_ew = 0;             // served lone deterministic XYD grid on fused_serve_xyd (MGDP_SERVE_EW=0: off)
     int dk1t = 0;                 // batched fp32 DoorKey on one LDS tile (MGDP_DK_1T; fused_fast_dk_1t)
     int dkhalf = 0;               // batched DoorKey, states split by has_key over two threads (MGDP_DK_HALF; fused_dk_half)
     int pair2 = 1;                // batched plain XYD with cpt 2: adjacent-cell pairs (MGDP_PAIR2=0: fused_fast_xyd_soa_xn)
@@ -114,6 +118,7 @@ struct mgdp_vi {
     unsigned long long serve_idle_ticks = 10000;     // 100 us at 100 MHz
     unsigned long long serve_life_ticks = 200000000; // 2 s
     int serve_pollers = 1;  // waves polling the request word (MGDP_SERVE_POLLERS; 1 measured 0.2-0.4 us faster than 4)
+    int serve_poll_dma = 1; // the server's polls land in an LDS mailbox, several in flight (MGDP_SERVE_POLL_DMA=0: one at a time)
     std::chrono::steady_clock::time_point serve_last{};  // host time of the last served result
     // A new lone grid for a resident server: the bytes wait at pending_src (host-mapped staging
     // h_stage, or the caller's device memory) and the next request carries kServeNewCells; a server
@@ -386,6 +391,9 @@ int launch_serve_t(mgdp_vi *vi, unsigned int served) {
     int smem = L.total();
     if constexpr (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL) {
         if (vi->cpt == 2) kern = ServeK<T, MODEL, SLIP, MAP, -2>::fn;
+        if constexpr (!SLIP) {
+            if (vi->serve_ew) kern = ServeK<T, MODEL, SLIP, MAP, kWpServeEw>::fn;
+        }
     }
     if constexpr (MODEL == MGDP_MODEL_DOORKEY && MAP == MGDP_MAP_CELL && !SLIP) {
         if (vi->dkhalf) kern = pick_dkhalf<ServeK, T, MODEL, SLIP, MAP>(vi->HWs / 64, kern);
@@ -396,8 +404,8 @@ int launch_serve_t(mgdp_vi *vi, unsigned int served) {
     ++vi->serve_tag;
     hipExtLaunchKernelGGL(kern, dim3(1), dim3(vi->fused_block), smem, vi->stream, tp.a, tp.b, 0, g,
                           make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv, vi->d_dvenv,
-                          vi->d_hout, vi->d_hout + 4, (unsigned long long)served, vi->serve_idle_ticks,
-                          vi->serve_life_ticks, vi->serve_pollers, vi->serve_tag);
+                          vi->d_hout, vi->d_hout + kHoutReq, (unsigned long long)served, vi->serve_idle_ticks,
+                          vi->serve_life_ticks, vi->serve_pollers, vi->serve_tag, vi->serve_poll_dma);
     MGDP_HIP(hipGetLastError());
     return 0;
 }
@@ -503,8 +511,20 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
         return (h[5] >> 32) == ep && (h[6] >> 32) == ep && (h[7] >> 32) == ep;
     };
     int relaunches = 0;
+    // probe knobs (MGDP_QUERY_SPINS, MGDP_QUERY_AFTER_US, MGDP_SPIN_PAUSE): how often the wait
+    // queries the stream, after how long, and whether each spin pauses
+    static const int q_mask = [] { const char *e = std::getenv("MGDP_QUERY_SPINS"); return e ? std::atoi(e) - 1 : 1023; }();
+    static const double q_after = [] { const char *e = std::getenv("MGDP_QUERY_AFTER_US"); return e ? std::atof(e) : 0.0; }();
+    static const bool s_pause = [] { const char *e = std::getenv("MGDP_SPIN_PAUSE"); return e && std::atoi(e) != 0; }();
+    bool query = q_after <= 0.0;
+    const auto t_wait = std::chrono::steady_clock::now();
     for (uint64_t spin = 0; !ready(); ++spin) {
-        if ((spin & 1023) == 1023) {
+        if (s_pause) __builtin_ia32_pause();
+        if ((spin & (uint64_t)q_mask) == (uint64_t)q_mask) {
+            if (!query) {
+                query = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_wait).count() > q_after;
+                if (!query) continue;
+            }
             const hipError_t q = hipStreamQuery(vi->stream);
             if (q == hipSuccess) {
                 if (ready()) break;
@@ -575,7 +595,7 @@ int wait_server_exit(mgdp_vi *vi) {
 }
 int server_stop(mgdp_vi *vi, bool drain = true) {
     if (vi->serving) {
-        __atomic_store_n(vi->h_out + 4, kServeQuit, __ATOMIC_RELEASE);
+        __atomic_store_n(vi->h_out + kHoutReq, kServeQuit, __ATOMIC_RELEASE);
         vi->serving = false;
         if (drain) {
             MGDP_HIP(hipStreamSynchronize(vi->stream));
@@ -601,11 +621,11 @@ void post_request(mgdp_vi *vi) {
     unsigned long long w = (unsigned long long)vi->epoch;
     if (vi->last_req) w |= kServeLast;
     if (vi->pending_src) {
-        __atomic_store_n(vi->h_out + 12, vi->pending_src | ((w & 0xffffull) << 48), __ATOMIC_RELEASE);
+        __atomic_store_n(vi->h_out + kHoutReq + 1, vi->pending_src | ((w & 0xffffull) << 48), __ATOMIC_RELEASE);
         w |= kServeNewCells;
         vi->pending_src = 0;
     }
-    __atomic_store_n(vi->h_out + 4, w, __ATOMIC_RELEASE);
+    __atomic_store_n(vi->h_out + kHoutReq, w, __ATOMIC_RELEASE);
 }
 // Hand a new lone grid to a resident server (no drain): true if it was taken.
 bool serve_handoff(mgdp_vi *vi, const void *src) {
@@ -840,6 +860,14 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
                 vi->gk_capacity = per_cu * cus;
             vi->gk = gk_on != 0 && d.B <= vi->gk_capacity;
         }
+        // The served lone deterministic XYD grid: east / west fronts by DPP, <= 4 waves (one dword
+        // of stop flags); the two-plane padded tiles must fit the usual V buffers.
+        int serve_ew = 1;
+        if (const char *ev = std::getenv("MGDP_SERVE_EW")) serve_ew = std::atoi(ev);
+        const int padw = serve_ew_padw(d.W);
+        vi->serve_ew = serve_ew && d.B == 1 && d.model == MGDP_MODEL_XYD && d.method == MGDP_METHOD_FUSED &&
+                       d.slip_p < 0.0 && !vi->pair && !vi->quad && !vi->opts && !vi->wave_p && vi->cpt == 1 &&
+                       vi->fused_block <= 256 && vi->HWs >= vi->fused_block && 2 * vi->HWs >= 3 * padw;
         int dk1t = 0;
         if (const char *ev = std::getenv("MGDP_DK_1T")) dk1t = std::atoi(ev) != 0;
         if (dk1t && d.B > 1 && d.model == MGDP_MODEL_DOORKEY && d.dtype == MGDP_F32 && d.method == MGDP_METHOD_FUSED &&
@@ -897,7 +925,7 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
             e = hipMemcpy(vi->d_rgoal, rg.data(), rg.size(), hipMemcpyHostToDevice);
         }
     }
-    if (e == hipSuccess) e = hipHostMalloc((void **)&vi->h_out, 16 * sizeof(unsigned long long),
+    if (e == hipSuccess) e = hipHostMalloc((void **)&vi->h_out, kHoutWords * sizeof(unsigned long long),
                                            hipHostMallocMapped | hipHostMallocCoherent);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&vi->d_hout, vi->h_out, 0);
     if (e == hipSuccess && d.B == 1) {
@@ -929,9 +957,10 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     if (const char *ev = std::getenv("MGDP_SERVE_IDLE_US"))  // s_memrealtime ticks at 100 MHz
         vi->serve_idle_ticks = (unsigned long long)std::max(1LL, std::atoll(ev)) * 100ull;
     if (const char *ev = std::getenv("MGDP_SERVE_POLLERS")) vi->serve_pollers = std::max(1, std::atoi(ev));
+    if (const char *ev = std::getenv("MGDP_SERVE_POLL_DMA")) vi->serve_poll_dma = std::atoi(ev) != 0;
     if (const char *ev = std::getenv("MGDP_SERVE_LIFE_US"))
         vi->serve_life_ticks = (unsigned long long)std::max(1LL, std::atoll(ev)) * 100ull;
-    if (vi->h_out) std::memset(vi->h_out, 0, 16 * sizeof(unsigned long long));
+    if (vi->h_out) std::memset(vi->h_out, 0, kHoutWords * sizeof(unsigned long long));
     if (e == hipSuccess) {  // arm the fused reduction (every launch re-arms it for the next)
         std::vector<unsigned long long> init((size_t)kRedShards * 4 + 2, 0ull);
         for (size_t i = 2; i < (size_t)kRedShards * 4; i += 4) init[i] = 0x7fffffffull;

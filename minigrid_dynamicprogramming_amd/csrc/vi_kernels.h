@@ -22,6 +22,9 @@ __host__ __device__ constexpr bool wp_is_wave2(int wp) { return wp <= kWpWave2 -
 // (fused_dk_half; workgroup = 2 * HWs threads)
 // Tags -501 .. -508: plane stride HWs = 64 * (-tag - 500) known at compile time.
 constexpr int kWpDkHalf = -500;
+// vi_serve_kernel variant tag: the served lone deterministic XYD grid on fused_serve_xyd (east / west
+// fronts by DPP; <= 4 waves), fused_fast_xyd_soa for a grid whose wave edges do not allow it
+constexpr int kWpServeEw = -600;
 __host__ __device__ constexpr bool wp_is_dkhalf(int wp) { return wp <= kWpDkHalf - 1 && wp >= kWpDkHalf - 8; }
 template <typename T, int MODEL> struct TopoOf { using type = XydTopo<T>; };
 template <typename T> struct TopoOf<T, MGDP_MODEL_DOORKEY> { using type = DkTopo; };
@@ -33,7 +36,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
                                            double *__restrict__ dvenv, unsigned long long *__restrict__ host_out,
                                            int k_target, int fresh, bool lone, unsigned int epoch, int e,
                                            int &k, double &dvl, const typename TopoOf<T, MODEL>::type *pre = nullptr,
-                                           unsigned long long *gk = nullptr, int gk_cap = 0) {
+                                           unsigned long long *gk = nullptr, int gk_cap = 0, bool ew = false) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
     T *V0 = reinterpret_cast<T *>(smem);
@@ -79,7 +82,8 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     constexpr bool SOA_ONLY = WP < 0;  // every negative tag runs the direction-major path alone
     constexpr bool PAIR2 = wp_is_pair(WP);
     constexpr bool DKHALF = wp_is_dkhalf(WP);
-    constexpr int CPT = PAIR2 ? 2 : (WP < 0 && !DK1T && !DKHALF && WP != kWpSoa ? -WP : 1);
+    constexpr bool SERVE_EW = WP == kWpServeEw;
+    constexpr int CPT = PAIR2 ? 2 : (WP < 0 && !DK1T && !DKHALF && !SERVE_EW && WP != kWpSoa ? -WP : 1);
     const bool fast = MAP == MGDP_MAP_CELL && geo.HW <= CPT * (int)blockDim.x;
     const bool soa = SOA_ONLY || (fast && !geo.pair && !geo.quad);
     if (!SERVED) copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
@@ -132,6 +136,11 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
         } else if constexpr (MODEL == MGDP_MODEL_DOORKEY && DK1T) {
             if (k_target < 0) fused_fast_dk_1t<T, true>(geo, cf, cl, V0, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
             else fused_fast_dk_1t<T, false>(geo, cf, cl, V0, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+        } else if constexpr (SERVE_EW) {
+            static_assert(SERVED && MODEL == MGDP_MODEL_XYD && !SLIP && MAP == MGDP_MAP_CELL, "served plain XYD grid");
+            if (ew) fused_serve_xyd<T>(geo, cf, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, dvl, done, *pre);
+            else fused_fast_xyd_soa<T, false, true>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target,
+                                                     dvl, done, nullptr, nullptr, 0, pre);
         } else if constexpr (MODEL == MGDP_MODEL_XYD && CPT > 1) {
             if (k_target < 0) fused_fast_xyd_soa_xn<T, SLIP, true, CPT>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
             else fused_fast_xyd_soa_xn<T, SLIP, false, CPT>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
@@ -235,7 +244,7 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
 // Persistent solver for a lone grid: one workgroup stays resident and serves solve requests posted
 // in host-mapped memory, removing the launch and dispatch latency from every solve.  The grid is
 // staged in LDS (and its topology resolved) at launch and again whenever a request carries
-// kServeNewCells: the request's source word (host_cmd[8], tagged with the request's low 16 bits, so
+// kServeNewCells: the request's source word (host_cmd[1], tagged with the request's low 16 bits, so
 // a source written before the request can never be paired with an older one) names the new grid's
 // W*H bytes -- host-mapped staging or device memory --, which the workgroup reads with
 // system-scope loads (coherent with the host and with every XCD's L2), copies into LDS and into
@@ -243,14 +252,45 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
 // polling wave reads the request word (relaxed system-scope loads, the waves staggered by s_sleep)
 // and also watches the LDS word another wave may already have set.  By default only wave 0 polls
 // (`pollers` = 1; the others wait at the barrier): with four staggered pollers the barrier also
-// waited for the other waves' in-flight PCIe reads (measured 0.2-0.4 us per solve slower).  Request
+// waited for the other waves' in-flight PCIe reads (measured 0.2-0.4 us per solve slower).
+// poll_dma (default): the poller does not wait for its reads.  Each poll is an LDS-DMA load
+// (global_load_lds_dwordx4 of the request / source pair) into a 16-B LDS mailbox, issued about
+// every 60 ns, so a PCIe round trip's worth of polls is in flight and the mailbox always holds the
+// latest read to return: a request is seen one round trip after it lands instead of one to two
+// (one blocking read at a time put a 1.2-1.5 us sawtooth on the solve latency, by when the host
+// posted relative to the poll -- tools/probe_serve.cpp with MGDP_PROBE_GAP_US).  The loads are
+// asm the compiler does not track: a stray one still in flight when the request is seen writes only
+// the mailbox, and the wave's next vmcnt wait (the compiler's, for its own accesses, or the one
+// before the exit word) also covers it.  Request
 // r (!= the last served) runs a fresh fused solve whose {k, dV} is published tagged with r.  Every
 // wave leaves on the quit word, after `idle_ticks` without a request or after `life_ticks` in total
 // (s_memrealtime, 100 MHz); the host relaunches the server if a request finds it gone.
+constexpr int kHoutWords = 32;  // host-mapped words of a handle (mgdp_vi::h_out)
+constexpr int kHoutReq = 16;    // request word; its source word follows (one 16-B pair)
 constexpr unsigned long long kServeQuit = ~0ull;
 constexpr unsigned long long kServeNewCells = 1ull << 62;
 constexpr unsigned long long kServeLast = 1ull << 61;  // request flag: leave after serving it
 constexpr unsigned long long kServeSrcMask = (1ull << 48) - 1;
+
+// One poll of the {request, source} pair (16 B of host memory, system scope) into the LDS mailbox
+// `box` by LDS DMA, issued by the calling lane without waiting for it (see vi_serve_kernel).  At
+// most 24 stay in flight (about 1.5 us of polls at the loop's pace; the wait is free below that).
+// M0 holds the LDS address for the load and is restored after it.
+__device__ __forceinline__ void poll_issue(const unsigned long long *src, unsigned long long *box) {
+    const unsigned int lds = (unsigned int)(uintptr_t)box;  // low 32 bits of a shared pointer: its LDS offset
+    unsigned int m0_saved;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %1\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, off sc0 sc1\n\t"
+        "s_nop 0\n\t"
+        "s_mov_b32 m0, %0\n\t"
+        "s_waitcnt vmcnt(24)"
+        : "=&s"(m0_saved)
+        : "s"(lds), "v"(src)
+        : "memory");
+}
 
 template <typename T, int MODEL, bool SLIP, int MAP, int WP = 0>
 __global__ void __launch_bounds__(WP > 0 ? 64 : 1024)
@@ -258,41 +298,58 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ host_out, const unsigned long long *__restrict__ host_cmd,
                 unsigned long long served, unsigned long long idle_ticks, unsigned long long life_ticks, int pollers,
-                unsigned long long exit_tag) {
+                unsigned long long exit_tag, int poll_dma) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ unsigned long long s_cmd, s_src;
+    __shared__ __attribute__((aligned(16))) unsigned long long s_box[2];  // poll mailbox: {request, source}
     const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
     uint8_t *cl = reinterpret_cast<uint8_t *>(smem + L.cells_off());
     copy16(cl, cells, geo.HWp);
-    if (threadIdx.x == 0) s_cmd = served;
+    if (threadIdx.x == 0) {
+        s_cmd = served;
+        s_box[0] = served;
+        s_box[1] = 0;
+    }
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     unsigned long long t_last = t_start;
     __syncthreads();
     // the grid stays put between kServeNewCells requests: resolve this thread's cell topology once
     typename TopoOf<T, MODEL>::type topo;
+    bool ew = false;  // kWpServeEw: may this grid run fused_serve_xyd (serve_ew_ok)
+    __shared__ int s_ew;
     auto resolve = [&]() {
-        if constexpr (WP == 0) {
+        if constexpr (WP == 0 || WP == kWpServeEw) {
             const int cc = (int)threadIdx.x < geo.HW ? (int)threadIdx.x : 0;
             if constexpr (MODEL == MGDP_MODEL_XYD) topo = xyd_topo_soa<T>(cl, geo, cc);
             else topo = dk_topo_soa(cl, geo, cc);
         }
+        if constexpr (WP == kWpServeEw) ew = serve_ew_ok(cl, geo, &s_ew);
     };
     resolve();
     while (true) {
         if (lane == 0 && wave < pollers) {  // the other waves wait at the barrier
             for (int i = 0; i < wave; ++i) __builtin_amdgcn_s_sleep(8);  // stagger the pollers
             while (true) {
-                unsigned long long cmd = __hip_atomic_load(host_cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                unsigned long long cmd, src = 0;
+                if (poll_dma) {
+                    poll_issue(host_cmd, s_box);
+                    __builtin_amdgcn_s_sleep(1);
+                    cmd = __hip_atomic_load(&s_box[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    src = __hip_atomic_load(&s_box[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else {
+                    cmd = __hip_atomic_load(host_cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
                 const unsigned long long now = __builtin_amdgcn_s_memrealtime();
                 if (cmd != served) {
                     if (cmd != kServeQuit && (cmd & kServeNewCells)) {
                         // the host wrote the source word before the request word; its tag proves it
                         // belongs to this request (a stale read is simply repeated)
-                        unsigned long long src = __hip_atomic_load(host_cmd + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        if (!poll_dma || (src >> 48) != (cmd & 0xffffull))
+                            src = __hip_atomic_load(host_cmd + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                         while ((src >> 48) != (cmd & 0xffffull)) {
                             if (__builtin_amdgcn_s_memrealtime() - t_start > life_ticks) { cmd = kServeQuit; break; }
-                            src = __hip_atomic_load(host_cmd + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                            src = __hip_atomic_load(host_cmd + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                         }
                         __hip_atomic_store(&s_src, src & kServeSrcMask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
@@ -304,7 +361,7 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
                     __hip_atomic_store(&s_cmd, kServeQuit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     break;
                 }
-                __builtin_amdgcn_s_sleep(2);
+                if (!poll_dma) __builtin_amdgcn_s_sleep(2);
             }
         }
         __syncthreads();
@@ -327,7 +384,8 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
         int k;
         double dvl;
         if (!fused_grid<T, MODEL, SLIP, MAP, true, WP>(geo, cf, cells, V, pi, kenv, dvenv, host_out, -1, 1, true,
-                                                   (unsigned int)cmd, 0, k, dvl, WP == 0 ? &topo : nullptr) &&
+                                                   (unsigned int)cmd, 0, k, dvl,
+                                                   (WP == 0 || WP == kWpServeEw) ? &topo : nullptr, nullptr, 0, ew) &&
             threadIdx.x == 0)
             publish_tagged(host_out, k, dvl, (unsigned int)cmd);
         served = cmd;

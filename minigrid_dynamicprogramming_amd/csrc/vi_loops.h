@@ -334,6 +334,166 @@ __device__ __forceinline__ void fused_fast_xyd_soa(const Geo &geo, const Coef<T>
     }
 }
 
+// The served lone deterministic XYD grid (vi_serve_kernel, WP = kWpServeEw): fused_fast_xyd_soa's
+// sweep with a shorter per-sweep chain for a latency-bound workgroup of <= 4 waves.
+//  * East / west fronts by DPP: cell c +- 1 is lane +- 1 of the same wave (wave_shl / wave_shr,
+//    0 shifted in at the wave's ends), so only planes 1 and 3 (south / north fronts) go through
+//    LDS: two ds_write and two ds_read per sweep instead of four each.  Fronts are geometric, as in
+//    fused_wave2_xyd: a front the agent cannot enter is an invalid state holding +0, and V >= +0,
+//    so max(., +0) is the identity and no per-direction select is needed.  The shifted-in 0 is
+//    exact unless a wave's first or last cell is valid AND its west / east neighbour (another
+//    wave's) is valid too: the caller checks that once per grid (serve_ew_ok) and otherwise runs
+//    fused_fast_xyd_soa.
+//  * The previous sweep's stop flags are one dword (<= 4 waves), no OR chain.
+//  * Three register sets rotate (unrolled by 6 with the two LDS tiles), so the sweep the rule stops
+//    leaves V_{k-1} intact in registers: the pi pass takes its own values there, its east / west
+//    fronts by the same DPP shifts and its north / south fronts from the V_{k-1} tile.
+// Same backups (one-multiply form), same rule and the same per-action pi pass as fused_fast_xyd_soa:
+// bit-identical V, pi, sweep count and dV.  LDS: each tile = [pad][plane 1][pad][plane 3][pad]
+// (serve_ew_tile_elems), carved from the two V buffers of the usual layout.
+__host__ __device__ inline int serve_ew_padw(int W) { return (W + 15) / 16 * 16; }
+__host__ __device__ inline int serve_ew_tile_elems(int HWs, int W) { return 2 * HWs + 3 * serve_ew_padw(W); }
+
+template <typename T>
+__device__ __forceinline__ T dpp_shl1_zero(T v) {  // lane i <- lane i+1; lane 63 <- +0
+    if constexpr (sizeof(T) == 4) {
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xF, 0xF, true));
+    } else {
+        const long long b = __double_as_longlong(v);
+        const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xF, 0xF, true);
+        const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xF, 0xF, true);
+        return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+    }
+}
+template <typename T>
+__device__ __forceinline__ T dpp_shr1_zero(T v) {  // lane i <- lane i-1; lane 0 <- +0
+    if constexpr (sizeof(T) == 4) {
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, true));
+    } else {
+        const long long b = __double_as_longlong(v);
+        const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xF, 0xF, true);
+        const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xF, 0xF, true);
+        return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+    }
+}
+
+// Whole workgroup (uniform result): may the grid run fused_serve_xyd?  Every wave's first / last
+// cell must not have a valid west / east neighbour in another wave (see above).  `word`: an LDS
+// int the call may use.
+__device__ __forceinline__ bool serve_ew_ok(const uint8_t *cl, const Geo &geo, int *word) {
+    const int c = threadIdx.x, lane = c & 63;
+    bool bad = false;
+    if (c < geo.HW && xyd_free(cl[c])) {
+        if (lane == 63 && c + 1 < geo.HW && xyd_free(cl[c + 1])) bad = true;
+        if (lane == 0 && c > 0 && xyd_free(cl[c - 1])) bad = true;
+    }
+    if (threadIdx.x == 0) *word = 0;
+    __syncthreads();
+    if (bad) *word = 1;
+    __syncthreads();
+    const bool ok = *word == 0;
+    __syncthreads();
+    return ok;
+}
+
+template <typename T, typename Done>
+__device__ __forceinline__ void fused_serve_xyd(const Geo &geo, const Coef<T> &cf, T *T0, T *T1, T *slots,
+                                                uint8_t *flags, const T *Vg, T *Vg_out, int8_t *pig, int &k,
+                                                double &dvl, const Done &done, const XydTopo<T> &tp) {
+    const int c = threadIdx.x;
+    const int cc = c < geo.HW ? c : 0;
+    const bool own_cell = c < geo.HW;
+    const int HW = geo.HWs, W = geo.W, padw = serve_ew_padw(W);
+    const int k_start = k;
+    const T ge = tp.valid ? cf.g : (T)0;
+    // plane 1 (V of direction 1) of cell x at tile[padw + x], plane 3 at tile[2 * padw + HW + x]
+    const int o1 = padw + c, o3 = 2 * padw + HW + c;
+    T A[4], B[4], C[4];
+    {
+        V4<T> x = V4<T>{{(T)0, (T)0, (T)0, (T)0}};
+        if (k != 0) x = *reinterpret_cast<const V4<T> *>(Vg + cc * 4);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) A[d] = own_cell ? x.v[d] : (T)0;
+    }
+    const int te = serve_ew_tile_elems(HW, W);
+    for (int i = c; i < te; i += blockDim.x) {  // pads (and planes) of both tiles start at +0
+        T0[i] = (T)0;
+        T1[i] = (T)0;
+    }
+    __syncthreads();
+    T0[o1] = A[1];
+    T0[o3] = A[3];
+    __syncthreads();
+    int parity = 0;
+    T diff = (T)0;
+    auto sweep = [&](const T *Vin, T *Vout, const T (&in)[4], T (&out)[4]) -> bool {
+        if (k >= geo.max_sweeps) return false;
+        const uint32_t fl = *reinterpret_cast<const uint32_t *>(flags + (parity ^ 1) * 16);
+        const T fS = Vin[o1 + W], fN = Vin[o3 - W];
+        const T fE = dpp_shl1_zero(in[0]), fW = dpp_shr1_zero(in[2]);
+        const T m02 = vmax(in[0], in[2]), m13 = vmax(in[1], in[3]);
+        const T m[4] = {vmax(vmax(in[0], m13), fE), vmax(vmax(in[1], m02), fS), vmax(vmax(in[2], m13), fW),
+                        vmax(vmax(in[3], m02), fN)};
+        T dm = (T)0;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            out[d] = vmax(ge * m[d], tp.tq[d]);
+            dm = vmax(dm, vabs(out[d] - in[d]));
+        }
+        asm volatile("" ::"v"(dm));  // keep the arithmetic ahead of the test (no sinking past it)
+        if (k > k_start && fl == 0u) return false;
+        diff = dm;
+        Vout[o1] = out[1];
+        Vout[o3] = out[3];
+        flag_write(diff >= cf.tol, flags, parity);
+        __syncthreads();
+        parity ^= 1;
+        ++k;
+        return true;
+    };
+    // on the stopping sweep: which register set holds V_k (`pos`: the set the stopped sweep read)
+    int pos;
+    while (true) {
+        if (!sweep(T0, T1, A, B)) { pos = 0; break; }
+        if (!sweep(T1, T0, B, C)) { pos = 1; break; }
+        if (!sweep(T0, T1, C, A)) { pos = 2; break; }
+        if (!sweep(T1, T0, A, B)) { pos = 3; break; }
+        if (!sweep(T0, T1, B, C)) { pos = 4; break; }
+        if (!sweep(T1, T0, C, A)) { pos = 5; break; }
+    }
+    dvl = (double)block_max(diff, slots, 0);
+    done(k, dvl);
+    // V_k = the stopped sweep's input set, V_{k-1} = the set before it (element selects: a pointer
+    // to one of the sets would put them in scratch); the V_{k-1} tile = the stopped sweep's output
+    // tile (positions 0, 2, 4 write T1)
+    const int sk = pos % 3, sp = (pos + 2) % 3;
+    T vk[4], vp[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        vk[d] = sk == 0 ? A[d] : (sk == 1 ? B[d] : C[d]);
+        vp[d] = sp == 0 ? A[d] : (sp == 1 ? B[d] : C[d]);
+    }
+    const T *Tp = (pos & 1) ? T0 : T1;
+    const T pE = dpp_shl1_zero(vp[0]), pW = dpp_shr1_zero(vp[2]);
+    if (own_cell) {
+        // forward reads the front state when the agent can enter it, else its own (xyd_step's nbv)
+        const T geo_f[4] = {pE, Tp[o1 + W], pW, Tp[o3 - W]};
+        T nbv[4];
+        V4<T> op;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            op.v[d] = vp[d];
+            const bool enter = tp.nbi[d] != d * HW + c;
+            nbv[d] = enter ? geo_f[d] : vp[d];
+        }
+        V4<T> tmp;
+        uint32_t pk;
+        xyd_step<T, false, true>(tp, cf, op, nbv, tmp, pk);
+        *reinterpret_cast<uint32_t *>(pig + c * 4) = pk;
+        *reinterpret_cast<V4<T> *>(Vg_out + c * 4) = V4<T>{{vk[0], vk[1], vk[2], vk[3]}};
+    }
+}
+
 // Batched XYD grids with N cells per thread (cells t + j*blockDim, j < N; HWs = N * blockDim): the
 // same sweep as fused_fast_xyd_soa on 1/N of the waves, so the per-sweep fixed work of a wave (flag
 // read, address set-up, ballot, barrier) is paid once per N cells.  Plain deterministic / slip

@@ -249,8 +249,10 @@ class ValueIteration:
             self._out = (ctypes.c_int32(0), ctypes.c_double(0), ctypes.c_int32(0))
             self._solve_args = (ctypes.c_void_p(self.h.value if isinstance(self.h, ctypes.c_void_p) else self.h),) + \
                 tuple(ctypes.byref(o) for o in self._out)
-            self._solve_fn = _lib.raw_fn("mgdp_vi_solve")
-            self._solve_last_fn = _lib.raw_fn("mgdp_vi_solve_last")
+            # a resident lone-grid server answers in ~10 us: keep the GIL across that call
+            quick = self.persistent
+            self._solve_fn = _lib.raw_fn("mgdp_vi_solve", keep_gil=quick)
+            self._solve_last_fn = _lib.raw_fn("mgdp_vi_solve_last", keep_gil=quick)
         rc = (self._solve_last_fn if last else self._solve_fn)(*self._solve_args)
         if rc:
             _lib.check(rc, "mgdp_vi_solve")

@@ -29,7 +29,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_version_and_error_string():
     L = _lib.load()
-    assert L.mgdp_abi_version() == _lib.ABI_VERSION == 5
+    assert L.mgdp_abi_version() == _lib.ABI_VERSION == 6
     n = ctypes.c_int32(-1)
     assert L.mgdp_device_count(ctypes.byref(n)) == 0
     assert n.value >= 0
@@ -48,6 +48,14 @@ def test_desc_struct_layout_matches_header():
     assert ctypes.sizeof(_lib.ViDesc) == 10 * 4 + 3 * 8 + 4 * 4 + 8
     assert _lib.ViDesc.gamma.offset == 40
     assert _lib.ViDesc.horizon.offset == 64 and _lib.ViDesc.death_cost.offset == 80
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="GPU present: the no-GPU error path is not reachable")
+def test_pin_host_thread_rejects_missing_device():
+    n = ctypes.c_int32(-1)
+    assert _lib.load().mgdp_pin_host_thread(0, ctypes.byref(n)) == _lib.MGDP_E_INVALID
+    assert n.value == 0
+    assert _lib.load().mgdp_pin_host_thread(0, None) == _lib.MGDP_E_INVALID
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="GPU present: the no-GPU error path is not reachable")

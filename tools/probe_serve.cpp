@@ -9,6 +9,8 @@
 
 #include "mgdp.h"
 
+static double g_gap_us = 0.0;  // busy-wait between solves (not timed): the request then comes later
+
 static void run(int max_sweeps, int n, const char *tag) {
     const int W = 16, H = 16;
     std::vector<uint8_t> cells(W * H, 1);
@@ -28,6 +30,11 @@ static void run(int max_sweeps, int n, const char *tag) {
     std::vector<double> t(n);
     auto T0 = std::chrono::steady_clock::now();
     for (int i = 0; i < n; ++i) {
+        if (g_gap_us > 0) {
+            const auto g0 = std::chrono::steady_clock::now();
+            while (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - g0).count() < g_gap_us) {
+            }
+        }
         auto a = std::chrono::steady_clock::now();
         if (mgdp_vi_solve(vi, &k, &dv, &conv)) { std::printf("%s\n", mgdp_last_error()); std::exit(1); }
         auto b = std::chrono::steady_clock::now();
@@ -35,14 +42,18 @@ static void run(int max_sweeps, int n, const char *tag) {
     }
     double tot = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - T0).count();
     std::sort(t.begin(), t.end());
-    std::printf("{\"tag\": \"%s\", \"max_sweeps\": %d, \"sweeps\": %d, \"n\": %d, \"mean_us\": %.3f, \"min_us\": %.3f, "
+    std::printf("{\"tag\": \"%s\", \"gap_us\": %.2f, \"max_sweeps\": %d, \"sweeps\": %d, \"n\": %d, \"mean_us\": %.3f, \"min_us\": %.3f, "
                 "\"p10_us\": %.3f, \"median_us\": %.3f, \"p90_us\": %.3f, \"p99_us\": %.3f}\n",
-                tag, max_sweeps, k, n, tot / n, t[0], t[n / 10], t[n / 2], t[n * 9 / 10], t[n * 99 / 100]);
+                tag, g_gap_us, max_sweeps, k, n, tot / n, t[0], t[n / 10], t[n / 2], t[n * 9 / 10], t[n * 99 / 100]);
     mgdp_vi_destroy(vi);
 }
 
 int main(int argc, char **argv) {
     const char *tag = argc > 1 ? argv[1] : "default";
+    int32_t pinned = 0;  // the polling thread on the GPU's NUMA node (MGDP_PROBE_PIN=0: unpinned)
+    if (!getenv("MGDP_PROBE_PIN") || atoi(getenv("MGDP_PROBE_PIN")) != 0) mgdp_pin_host_thread(0, &pinned);
+    std::fprintf(stderr, "pinned to %d CPUs\n", (int)pinned);
+    if (getenv("MGDP_PROBE_GAP_US")) g_gap_us = atof(getenv("MGDP_PROBE_GAP_US"));
     run(1, 5000, tag);
     run(2, 5000, tag);
     run(10000, 5000, tag);
