@@ -365,6 +365,11 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
         }
     }
     if (smem > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
+    if (std::getenv("MGDP_DEBUG_OCC")) {  // diagnostics: resident workgroups per CU of this launch
+        int per_cu = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)kern, vi->fused_block, smem);
+        std::fprintf(stderr, "mgdp occupancy: %d workgroups/CU (block %d, LDS %d B)\n", per_cu, vi->fused_block, smem);
+    }
     TimedPair tp;
     if (int rc = timed_begin(vi, -1, &tp)) return rc;
     // the launch-wide rule: a fresh own-rule launch of a resident batch (every grid then also does

@@ -36,7 +36,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
                                            double *__restrict__ dvenv, unsigned long long *__restrict__ host_out,
                                            int k_target, int fresh, bool lone, unsigned int epoch, int e,
                                            int &k, double &dvl, const typename TopoOf<T, MODEL>::type *pre = nullptr,
-                                           unsigned long long *gk = nullptr, int gk_cap = 0, bool ew = false) {
+                                           unsigned long long *gk = nullptr, int gk_cap = 0, int ew = 0) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
     T *V0 = reinterpret_cast<T *>(smem);
@@ -138,7 +138,8 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
             else fused_fast_dk_1t<T, false>(geo, cf, cl, V0, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
         } else if constexpr (SERVE_EW) {
             static_assert(SERVED && MODEL == MGDP_MODEL_XYD && !SLIP && MAP == MGDP_MAP_CELL, "served plain XYD grid");
-            if (ew) fused_serve_xyd<T>(geo, cf, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, dvl, done, *pre);
+            // ew: 0 = this grid falls back, 1 = fused_serve_xyd, 2 = the same, first solve of the grid
+            if (ew) fused_serve_xyd<T>(geo, cf, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, dvl, done, *pre, ew == 2);
             else fused_fast_xyd_soa<T, false, true>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target,
                                                      dvl, done, nullptr, nullptr, 0, pre);
         } else if constexpr (MODEL == MGDP_MODEL_XYD && CPT > 1) {
@@ -316,7 +317,7 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
     __syncthreads();
     // the grid stays put between kServeNewCells requests: resolve this thread's cell topology once
     typename TopoOf<T, MODEL>::type topo;
-    bool ew = false;  // kWpServeEw: may this grid run fused_serve_xyd (serve_ew_ok)
+    int ew = 0;  // kWpServeEw: 0 = the grid falls back, 1 = fused_serve_xyd, 2 = the same, tiles to clear
     __shared__ int s_ew;
     auto resolve = [&]() {
         if constexpr (WP == 0 || WP == kWpServeEw) {
@@ -324,7 +325,7 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
             if constexpr (MODEL == MGDP_MODEL_XYD) topo = xyd_topo_soa<T>(cl, geo, cc);
             else topo = dk_topo_soa(cl, geo, cc);
         }
-        if constexpr (WP == kWpServeEw) ew = serve_ew_ok(cl, geo, &s_ew);
+        if constexpr (WP == kWpServeEw) ew = serve_ew_ok(cl, geo, &s_ew) ? 2 : 0;
     };
     resolve();
     while (true) {
@@ -388,6 +389,7 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
                                                    (WP == 0 || WP == kWpServeEw) ? &topo : nullptr, nullptr, 0, ew) &&
             threadIdx.x == 0)
             publish_tagged(host_out, k, dvl, (unsigned int)cmd);
+        if (ew == 2) ew = 1;  // the tiles' pads stay +0 until the next grid
         served = cmd;
         if (cmd & kServeLast) break;
         t_last = __builtin_amdgcn_s_memrealtime();

@@ -5,6 +5,11 @@
 // vi_kernels.h); see vi.hip for the DP semantics and the data layout.
 #pragma once
 
+// MGDP_RUNTO_DV_ALL=1 (A/B builds): k_target loops compute |dV| on every sweep, not only the last.
+#ifndef MGDP_RUNTO_DV_ALL
+#define MGDP_RUNTO_DV_ALL 0
+#endif
+
 namespace mgdp {
 // ------------------------------------------------------------------------------------------------
 // (state, action) lane mapping: 8 lanes per state, lane a evaluates action a, a wave shuffle
@@ -396,10 +401,13 @@ __device__ __forceinline__ bool serve_ew_ok(const uint8_t *cl, const Geo &geo, i
     return ok;
 }
 
+// zero_tiles: clear both tiles first (the pads must hold +0); the server does it once per grid, as
+// nothing else writes the pads while the grid stays (a solve rewrites tile 0's planes only).
 template <typename T, typename Done>
 __device__ __forceinline__ void fused_serve_xyd(const Geo &geo, const Coef<T> &cf, T *T0, T *T1, T *slots,
                                                 uint8_t *flags, const T *Vg, T *Vg_out, int8_t *pig, int &k,
-                                                double &dvl, const Done &done, const XydTopo<T> &tp) {
+                                                double &dvl, const Done &done, const XydTopo<T> &tp,
+                                                bool zero_tiles) {
     const int c = threadIdx.x;
     const int cc = c < geo.HW ? c : 0;
     const bool own_cell = c < geo.HW;
@@ -415,12 +423,16 @@ __device__ __forceinline__ void fused_serve_xyd(const Geo &geo, const Coef<T> &c
 #pragma unroll
         for (int d = 0; d < 4; ++d) A[d] = own_cell ? x.v[d] : (T)0;
     }
-    const int te = serve_ew_tile_elems(HW, W);
-    for (int i = c; i < te; i += blockDim.x) {  // pads (and planes) of both tiles start at +0
-        T0[i] = (T)0;
-        T1[i] = (T)0;
+    if (zero_tiles) {
+        const int te = serve_ew_tile_elems(HW, W);
+        for (int i = c; i < te; i += blockDim.x) {  // pads (and planes) of both tiles start at +0
+            T0[i] = (T)0;
+            T1[i] = (T)0;
+        }
+        __syncthreads();
     }
-    __syncthreads();
+    B[0] = B[1] = B[2] = B[3] = (T)0;
+    C[0] = C[1] = C[2] = C[3] = (T)0;
     T0[o1] = A[1];
     T0[o3] = A[3];
     __syncthreads();
@@ -1029,10 +1041,13 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
             N3[j * 64 + lane] = o[j][3];
         }
         asm volatile("" ::: "memory");
+        // a k_target loop reports |dV| of its last sweep only (a uniform branch)
+        if (LOCAL || MGDP_RUNTO_DV_ALL || k + 1 == k_target) {
 #pragma unroll
-        for (int j = 0; j < P; ++j)
+            for (int j = 0; j < P; ++j)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) dm = vmax(dm, vabs(o[j][q] - in[j][q]));
+                for (int q = 0; q < 4; ++q) dm = vmax(dm, vabs(o[j][q] - in[j][q]));
+        }
         diff = dm;
         if (LOCAL) more = __ballot(dm >= cf.tol) != 0ull;
 #pragma unroll
@@ -1240,9 +1255,16 @@ __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> 
         if (HMODE != 2) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) nbs[q] = *reinterpret_cast<const V4<T> *>(Vin + tpf.nb[q]);
-            if (wcls == 0u) d = dk_step_fast<T, HMODE != 0, false, false>(tpf, cf, in, nbs, outv, rg);
-            else if (wcls == 1u) d = dk_step_fast<T, HMODE != 0, true, false>(tpf, cf, in, nbs, outv, rg);
-            else d = dk_step_fast<T, HMODE != 0, true, true>(tpf, cf, in, nbs, outv, rg);
+            // a k_target loop reports |dV| of its last sweep only: the others skip the differences
+            if (LOCAL || MGDP_RUNTO_DV_ALL || k + 1 == k_target) {
+                if (wcls == 0u) d = dk_step_fast<T, HMODE != 0, false, false>(tpf, cf, in, nbs, outv, rg);
+                else if (wcls == 1u) d = dk_step_fast<T, HMODE != 0, true, false>(tpf, cf, in, nbs, outv, rg);
+                else d = dk_step_fast<T, HMODE != 0, true, true>(tpf, cf, in, nbs, outv, rg);
+            } else {
+                if (wcls == 0u) d = dk_step_fast<T, HMODE != 0, false, false, false>(tpf, cf, in, nbs, outv, rg);
+                else if (wcls == 1u) d = dk_step_fast<T, HMODE != 0, true, false, false>(tpf, cf, in, nbs, outv, rg);
+                else d = dk_step_fast<T, HMODE != 0, true, true, false>(tpf, cf, in, nbs, outv, rg);
+            }
         } else {
             dk_load_nb(tp, Vin, nbs);
             d = dk_step<T, true, true>(tp, cf, in, nbs, outv, pk, rg);

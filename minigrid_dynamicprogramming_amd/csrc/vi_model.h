@@ -410,7 +410,9 @@ __device__ __forceinline__ uint32_t dk_fast_class(const DkFast &q) {
     return goal | (kd << 1);
 }
 
-template <typename T, bool FH, bool GOAL, bool KD>
+// DV = false: the value sweep only (returns 0) -- for the sweeps of a k_target loop whose |dV| is
+// not reported (only the last one's is).
+template <typename T, bool FH, bool GOAL, bool KD, bool DV = true>
 __device__ __forceinline__ T dk_step_fast(const DkFast &tp, const Coef<T> &cf, const T (&own)[16],
                                           const V4<T> (&nbs)[4], T (&outv)[16], T rg = (T)1) {
     T df[16];
@@ -442,6 +444,7 @@ __device__ __forceinline__ T dk_step_fast(const DkFast &tp, const Coef<T> &cf, c
             }
         }
     }
+    if constexpr (!DV) return (T)0;
     // max is exact and order-free: a three-input tree (v_max3) over the 16 differences
     const T a = vmax(vmax(df[0], df[1]), df[2]), b = vmax(vmax(df[3], df[4]), df[5]);
     const T c = vmax(vmax(df[6], df[7]), df[8]), e = vmax(vmax(df[9], df[10]), df[11]);
