@@ -548,11 +548,15 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
 #ifdef MGDP_SERVE_TRACE
     // trace build (tools/probe_serve_trace.sh): server-side s_memrealtime stamps, 10 ns ticks --
     // [8] request seen by the workgroup, [9] result about to be published
-    if (tagged) {
+    if (tagged) {  // mean of each block of 1000 solves
         static double n = 0, solve = 0;
         n += 1;
         solve += (double)(h[9] - h[8]) * 0.01;
-        if ((long long)n % 1000 == 0) std::fprintf(stderr, "serve trace: %.0f solves, request seen -> publish %.3f us\n", n, solve / n);
+        if ((long long)n % 1000 == 0) {
+            std::fprintf(stderr, "serve trace: solves %.0f-%.0f, request seen -> publish %.3f us (sweeps %llu)\n", n - 999, n,
+                         solve / 1000.0, (unsigned long long)(h[5] & 0xffffffffull));
+            solve = 0;
+        }
     }
 #endif
     unsigned long long km, dvb, kmin;

@@ -28,4 +28,11 @@ timeout -k 10 300 python bench.py --gpus 1 --steps 200 --warmup 5 --no-cpu --no-
 timeout -k 10 300 env MGDP_SERVE_EW=0 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --no-hbm --no-sharded > $OUT/b_ew0.json 2> $OUT/b_ew0.err || exit 1
 grep '"max_sweeps": 10000' $OUT/serve.json
 for f in $OUT/b*.json; do python -c "import json,sys; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$f', '%.4g'%d['value'], '%.3f us'%(d['ms_per_step']*1e3))"; done
+
+# GPU-side request-seen -> publish time per solve (trace build in exp_diag/trace, if present):
+# MGDP_EXTRA_FLAGS=-DMGDP_SERVE_TRACE MGDP_BUILD_OUT=exp_diag/trace/libmgdp.so python -c "from minigrid_dynamicprogramming_amd import build; build.build()"
+if [ -f exp_diag/trace/libmgdp.so ]; then
+  LD_LIBRARY_PATH=exp_diag/trace timeout -k 10 120 ./tools/probe_serve trace > $OUT/trace.json 2> $OUT/trace.err || { echo "trace probe failed"; exit 1; }
+  grep "serve trace" $OUT/trace.err
+fi
 echo "all ok"
