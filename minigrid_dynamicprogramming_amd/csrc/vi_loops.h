@@ -436,11 +436,14 @@ __device__ __forceinline__ void fused_serve_xyd(const Geo &geo, const Coef<T> &c
     T0[o1] = A[1];
     T0[o3] = A[3];
     __syncthreads();
-    int parity = 0;
     T diff = (T)0;
-    auto sweep = [&](const T *Vin, T *Vout, const T (&in)[4], T (&out)[4]) -> bool {
+    // par: this sweep's flag parity, a constant at each unrolled call (the flag addresses fold to
+    // immediate offsets); a sweep at loop position p has parity p & 1
+    uint8_t *const fwave = flags + (threadIdx.x >> 6);
+    const bool lane0 = (threadIdx.x & 63) == 0;
+    auto sweep = [&](const T *Vin, T *Vout, const T (&in)[4], T (&out)[4], const int par) -> bool {
         if (k >= geo.max_sweeps) return false;
-        const uint32_t fl = *reinterpret_cast<const uint32_t *>(flags + (parity ^ 1) * 16);
+        const uint32_t fl = *reinterpret_cast<const uint32_t *>(flags + (par ^ 1) * 16);
         const T fS = Vin[o1 + W], fN = Vin[o3 - W];
         const T fE = dpp_shl1_zero(in[0]), fW = dpp_shr1_zero(in[2]);
         const T m02 = vmax(in[0], in[2]), m13 = vmax(in[1], in[3]);
@@ -457,21 +460,21 @@ __device__ __forceinline__ void fused_serve_xyd(const Geo &geo, const Coef<T> &c
         diff = dm;
         Vout[o1] = out[1];
         Vout[o3] = out[3];
-        flag_write(diff >= cf.tol, flags, parity);
+        const bool any = __ballot(diff >= cf.tol) != 0ull;
+        if (lane0) fwave[par * 16] = any;
         __syncthreads();
-        parity ^= 1;
         ++k;
         return true;
     };
     // on the stopping sweep: which register set holds V_k (`pos`: the set the stopped sweep read)
     int pos;
     while (true) {
-        if (!sweep(T0, T1, A, B)) { pos = 0; break; }
-        if (!sweep(T1, T0, B, C)) { pos = 1; break; }
-        if (!sweep(T0, T1, C, A)) { pos = 2; break; }
-        if (!sweep(T1, T0, A, B)) { pos = 3; break; }
-        if (!sweep(T0, T1, B, C)) { pos = 4; break; }
-        if (!sweep(T1, T0, C, A)) { pos = 5; break; }
+        if (!sweep(T0, T1, A, B, 0)) { pos = 0; break; }
+        if (!sweep(T1, T0, B, C, 1)) { pos = 1; break; }
+        if (!sweep(T0, T1, C, A, 0)) { pos = 2; break; }
+        if (!sweep(T1, T0, A, B, 1)) { pos = 3; break; }
+        if (!sweep(T0, T1, B, C, 0)) { pos = 4; break; }
+        if (!sweep(T1, T0, C, A, 1)) { pos = 5; break; }
     }
     dvl = (double)block_max(diff, slots, 0);
     done(k, dvl);
