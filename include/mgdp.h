@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MGDP_ABI_VERSION 6
+#define MGDP_ABI_VERSION 7
 
 enum {
     MGDP_OK = 0,
@@ -164,6 +164,14 @@ int mgdp_vi_run_to(mgdp_vi *vi, int32_t k_target, double *dv_out);
 int mgdp_vi_sweep(mgdp_vi *vi, double *dv_out);
 /* Extract pi from the last sweep and publish sweeps/converged for mgdp_vi_get_*. */
 int mgdp_vi_finish(mgdp_vi *vi, int32_t sweeps);
+/* Checkpoint / resume (ABI 7; fused method, no horizon): continue a solve that stopped at sweep k
+ * before converging (a max_sweeps cap) from its state {V_k (B*S values of the handle's dtype, as
+ * mgdp_vi_get_values returns them), k, dV_k} -- on this or a new handle of the same grids and
+ * parameters.  Jacobi is memoryless given V_k: the result (global stopping sweep, V, pi, dV) is
+ * bit-identical to the uninterrupted solve.  k in [1, max_sweeps); dV >= tol (a converged
+ * checkpoint is final: its pi is not rebuildable from V_k). */
+int mgdp_vi_resume(mgdp_vi *vi, const void *V, int32_t k, double dv, int32_t *sweeps_out, double *dv_out,
+                   int32_t *converged_out);
 
 /* The same protocol with no host round trip between its steps (fused method, no horizon / lava
  * options; distributed.py drives it over RCCL).  d_pub / d_k are caller-owned DEVICE int64 buffers

@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # MGDP_LIB: an alternative build of the same sources (tools/ experiments with compile-time knobs)
 LIB_PATH = os.environ.get("MGDP_LIB") or os.path.join(HERE, "libmgdp.so")
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 MGDP_OK = 0
 MGDP_E_INVALID = -1
 MGDP_E_HIP = -2
@@ -79,6 +79,7 @@ SIGNATURES = {
     "mgdp_vi_load_cells_device": (ctypes.c_int, [_P, _P]),
     "mgdp_vi_solve": (ctypes.c_int, [_P, _I32P, _DP, _I32P]),
     "mgdp_vi_solve_last": (ctypes.c_int, [_P, _I32P, _DP, _I32P]),
+    "mgdp_vi_resume": (ctypes.c_int, [_P, _P, _I32, ctypes.c_double, _I32P, _DP, _I32P]),
     "mgdp_vi_reset": (ctypes.c_int, [_P]),
     "mgdp_vi_run_local": (ctypes.c_int, [_P, _I32P]),
     "mgdp_vi_run_to": (ctypes.c_int, [_P, _I32, _DP]),

@@ -1317,6 +1317,52 @@ int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *con
     return 0;
 }
 
+// Checkpoint / resume (aux "checkpoint / resume"): Jacobi is memoryless given V_k,
+// so a solve stopped at sweep k (a max_sweeps cap) continues from {V_k, k, dV_k} -- on this handle
+// or on a new one in another process -- to the same global stopping sweep, V and pi, bit for bit,
+// as the uninterrupted solve.  Every grid restarts its own rule at k (kenv / dvenv), then the
+// batch is taken to the global K as in mgdp_vi_solve.  A converged checkpoint (dV < tol) has
+// nothing left to do, and its pi (argmax on V_{k-1}) cannot be rebuilt from V_k: refused.
+int mgdp_vi_resume(mgdp_vi *vi, const void *V, int32_t k, double dv, int32_t *sweeps_out, double *dv_out,
+                   int32_t *converged_out) {
+    MGDP_CHECK(vi && V, MGDP_E_INVALID, "null argument");
+    MGDP_CHECK(vi->cells_loaded, MGDP_E_INVALID, "no cells loaded");
+    MGDP_CHECK(vi->d.method == MGDP_METHOD_FUSED && vi->d.horizon == 0, MGDP_E_INVALID,
+               "resume: the fused method with an infinite horizon");
+    MGDP_CHECK(k >= 1 && k < vi->d.max_sweeps, MGDP_E_INVALID, "resume: sweep %d outside [1, max_sweeps)", k);
+    MGDP_CHECK(!(dv < vi->d.tol), MGDP_E_INVALID,
+               "resume: the checkpoint has converged (dV %g < tol %g); its V and pi are final", dv, vi->d.tol);
+    DeviceGuard guard(vi->d.device);
+    if (int rc = server_stop(vi)) return rc;
+    const size_t BS = (size_t)vi->d.B * vi->S;
+    MGDP_HIP(hipMemcpy(vi->d_V[0], V, BS * vi->tsize, hipMemcpyHostToDevice));
+    std::vector<int32_t> kk((size_t)vi->d.B, k);
+    std::vector<double> dd((size_t)vi->d.B, dv);
+    MGDP_HIP(hipMemcpy(vi->d_kenv, kk.data(), kk.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    MGDP_HIP(hipMemcpy(vi->d_dvenv, dd.data(), dd.size() * sizeof(double), hipMemcpyHostToDevice));
+    vi->fresh = 0;  // the next fused launch continues each grid from kenv / dvenv and V in HBM
+    vi->cur = 0;
+    vi->k_done = k;
+    vi->k_min = k;
+    vi->k_done_valid = false;
+    vi->sweeps = k;
+    vi->converged = 0;
+    int32_t K = k;
+    double dv2 = dv;
+    if (int rc = mgdp_vi_run_local(vi, &K)) return rc;
+    if (int rc = mgdp_vi_run_to(vi, K, &dv2)) return rc;
+    while (!(dv2 < vi->d.tol) && K < vi->d.max_sweeps) {  // contraction broken by rounding: global rule
+        if (int rc = mgdp_vi_sweep(vi, &dv2)) return rc;
+        ++K;
+    }
+    if (int rc = mgdp_vi_finish(vi, K)) return rc;
+    vi->converged = dv2 < vi->d.tol;
+    if (sweeps_out) *sweeps_out = K;
+    if (dv_out) *dv_out = dv2;
+    if (converged_out) *converged_out = vi->converged;
+    return 0;
+}
+
 int mgdp_vi_solve_last(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *converged_out) {
     MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
     vi->last_req = true;

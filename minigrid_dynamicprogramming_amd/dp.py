@@ -351,6 +351,39 @@ class ValueIteration:
         _lib.check(self.L.mgdp_vi_get_policy(self.h, _lib.ptr(pi)), "mgdp_vi_get_policy")
         return pi
 
+    # -- checkpoint / resume: Jacobi is memoryless given V_k
+    def checkpoint(self) -> dict:
+        """The state of the last solve: {"V" (B, S), "pi" (B, S), "sweeps", "dv", "converged"}.  A
+        solve stopped by max_sweeps before converging continues from it with resume() -- on this
+        handle or on a new one of the same grids and parameters -- bit-identical to the
+        uninterrupted solve."""
+        return {"V": self.values(), "pi": self.policy(), "sweeps": int(self.sweeps), "dv": float(self.dv),
+                "converged": bool(self.converged)}
+
+    def resume(self, ckpt: dict) -> int:
+        """Continue from checkpoint() output (mgdp_vi_resume); returns the sweeps of the whole solve.
+        A converged checkpoint is final and is refused."""
+        V = np.ascontiguousarray(ckpt["V"], dtype=self.np_dtype)
+        if V.shape != (self.B, self.S):
+            raise ValueError(f"checkpoint V of shape {V.shape} does not match the handle's {(self.B, self.S)}")
+        k, dv, conv = ctypes.c_int32(0), ctypes.c_double(0), ctypes.c_int32(0)
+        _lib.check(self.L.mgdp_vi_resume(self.h, _lib.ptr(V), int(ckpt["sweeps"]), float(ckpt["dv"]), ctypes.byref(k),
+                                         ctypes.byref(dv), ctypes.byref(conv)), "mgdp_vi_resume")
+        self.sweeps, self.dv, self.converged = k.value, dv.value, bool(conv.value)
+        return self.sweeps
+
+    @staticmethod
+    def save_checkpoint(path, ckpt: dict) -> None:
+        """Write a checkpoint as .npz (plain arrays: np.load needs no pickle)."""
+        np.savez(path, V=ckpt["V"], pi=ckpt["pi"], sweeps=np.int64(ckpt["sweeps"]), dv=np.float64(ckpt["dv"]),
+                 converged=np.bool_(ckpt["converged"]))
+
+    @staticmethod
+    def load_checkpoint(path) -> dict:
+        z = np.load(path)  # allow_pickle=False
+        return {"V": z["V"], "pi": z["pi"], "sweeps": int(z["sweeps"]), "dv": float(z["dv"]),
+                "converged": bool(z["converged"])}
+
     def dv_trace(self) -> np.ndarray:
         t = np.zeros(self.sweeps, np.float64)
         _lib.check(self.L.mgdp_vi_get_dv_trace(self.h, _lib.ptr(t), self.sweeps), "mgdp_vi_get_dv_trace")
