@@ -36,6 +36,7 @@
 #include <cstdlib>
 #include <climits>
 #include <limits>
+#include <type_traits>
 #include <cstring>
 #include <vector>
 

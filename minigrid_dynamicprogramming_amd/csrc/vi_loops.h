@@ -412,7 +412,6 @@ __device__ __forceinline__ void fused_serve_xyd(const Geo &geo, const Coef<T> &c
     const int cc = c < geo.HW ? c : 0;
     const bool own_cell = c < geo.HW;
     const int HW = geo.HWs, W = geo.W, padw = serve_ew_padw(W);
-    const int k_start = k;
     const T ge = tp.valid ? cf.g : (T)0;
     // plane 1 (V of direction 1) of cell x at tile[padw + x], plane 3 at tile[2 * padw + HW + x]
     const int o1 = padw + c, o3 = 2 * padw + HW + c;
@@ -441,8 +440,13 @@ __device__ __forceinline__ void fused_serve_xyd(const Geo &geo, const Coef<T> &c
     // immediate offsets); a sweep at loop position p has parity p & 1
     uint8_t *const fwave = flags + (threadIdx.x >> 6);
     const bool lane0 = (threadIdx.x & 63) == 0;
-    auto sweep = [&](const T *Vin, T *Vout, const T (&in)[4], T (&out)[4], const int par) -> bool {
-        if (k >= geo.max_sweeps) return false;
+    // test: whether this sweep consults the previous sweep's flags (all but the first: the first is
+    // peeled off the loop, so no sweep of the loop tests k > k_start)
+    // cap: whether this sweep checks max_sweeps (every sweep does: a second, unchecked copy of the
+    // six unrolled sweeps for blocks with six to spare measured 8.2 vs 5.6 us per solve -- the
+    // server's code then overflows the instruction cache)
+    auto sweep = [&](const T *Vin, T *Vout, const T (&in)[4], T (&out)[4], const int par, auto test, auto cap) -> bool {
+        if (decltype(cap)::value && k >= geo.max_sweeps) return false;
         const uint32_t fl = *reinterpret_cast<const uint32_t *>(flags + (par ^ 1) * 16);
         const T fS = Vin[o1 + W], fN = Vin[o3 - W];
         const T fE = dpp_shl1_zero(in[0]), fW = dpp_shr1_zero(in[2]);
@@ -456,11 +460,11 @@ __device__ __forceinline__ void fused_serve_xyd(const Geo &geo, const Coef<T> &c
             dm = vmax(dm, vabs(out[d] - in[d]));
         }
         asm volatile("" ::"v"(dm));  // keep the arithmetic ahead of the test (no sinking past it)
-        if (k > k_start && fl == 0u) return false;
+        if (decltype(test)::value && fl == 0u) return false;
         diff = dm;
         Vout[o1] = out[1];
         Vout[o3] = out[3];
-        const bool any = __ballot(diff >= cf.tol) != 0ull;
+        const bool any = __ballot(dm >= cf.tol) != 0ull;
         if (lane0) fwave[par * 16] = any;
         __syncthreads();
         ++k;
@@ -468,13 +472,20 @@ __device__ __forceinline__ void fused_serve_xyd(const Geo &geo, const Coef<T> &c
     };
     // on the stopping sweep: which register set holds V_k (`pos`: the set the stopped sweep read)
     int pos;
-    while (true) {
-        if (!sweep(T0, T1, A, B, 0)) { pos = 0; break; }
-        if (!sweep(T1, T0, B, C, 1)) { pos = 1; break; }
-        if (!sweep(T0, T1, C, A, 0)) { pos = 2; break; }
-        if (!sweep(T1, T0, A, B, 1)) { pos = 3; break; }
-        if (!sweep(T0, T1, B, C, 0)) { pos = 4; break; }
-        if (!sweep(T1, T0, C, A, 1)) { pos = 5; break; }
+    using Yes = std::integral_constant<bool, true>;
+    using No = std::integral_constant<bool, false>;
+    // k_start's sweep has no previous sweep to test (a resumed solve's first one included)
+    if (!sweep(T0, T1, A, B, 0, No{}, Yes{})) {
+        pos = 0;
+    } else {
+        while (true) {
+            if (!sweep(T1, T0, B, C, 1, Yes{}, Yes{})) { pos = 1; break; }
+            if (!sweep(T0, T1, C, A, 0, Yes{}, Yes{})) { pos = 2; break; }
+            if (!sweep(T1, T0, A, B, 1, Yes{}, Yes{})) { pos = 3; break; }
+            if (!sweep(T0, T1, B, C, 0, Yes{}, Yes{})) { pos = 4; break; }
+            if (!sweep(T1, T0, C, A, 1, Yes{}, Yes{})) { pos = 5; break; }
+            if (!sweep(T0, T1, A, B, 0, Yes{}, Yes{})) { pos = 0; break; }
+        }
     }
     dvl = (double)block_max(diff, slots, 0);
     done(k, dvl);
