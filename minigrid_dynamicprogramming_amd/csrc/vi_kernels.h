@@ -25,6 +25,10 @@ constexpr int kWpDkHalf = -500;
 // vi_serve_kernel variant tag: the served lone deterministic XYD grid on fused_serve_xyd (east / west
 // fronts by DPP; <= 4 waves), fused_fast_xyd_soa for a grid whose wave edges do not allow it
 constexpr int kWpServeEw = -600;
+// MGDP_DK_PERM=0 (A/B builds): batched DoorKey grids keep thread t on cell t (no dk_class_perm)
+#ifndef MGDP_DK_PERM
+#define MGDP_DK_PERM 1
+#endif
 __host__ __device__ constexpr bool wp_is_dkhalf(int wp) { return wp <= kWpDkHalf - 1 && wp >= kWpDkHalf - 8; }
 template <typename T, int MODEL> struct TopoOf { using type = XydTopo<T>; };
 template <typename T> struct TopoOf<T, MGDP_MODEL_DOORKEY> { using type = DkTopo; };
@@ -151,10 +155,14 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
                                                   done, nullptr, nullptr, 0, pre);
             else fused_fast_xyd_soa<T, SLIP, false>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
         } else {
+            // batched grids: the special-first thread -> cell map (dk_class_perm) in the unused pi region
+            uint8_t *perm = (MGDP_DK_PERM && !SERVED && 2 * geo.HW + 16 + 128 <= L.pi_bytes)
+                                ? reinterpret_cast<uint8_t *>(pis) : nullptr;
             if (SERVED || k_target < 0)
                 fused_fast_dk_soa<T, true>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done,
-                                           nullptr, nullptr, 0, pre);
-            else fused_fast_dk_soa<T, false>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
+                                           nullptr, nullptr, 0, pre, perm);
+            else fused_fast_dk_soa<T, false>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done,
+                                             nullptr, nullptr, 0, nullptr, perm);
         }
         if (threadIdx.x == 0) {
             kenv[e] = k;

@@ -1229,14 +1229,55 @@ __device__ __forceinline__ DkTopo dk_topo_soa(const uint8_t *cl, const Geo &geo,
     return tp;
 }
 
+// Thread -> cell map of a batched DoorKey grid that puts the "special" cells first (stable): those
+// with a goal, key or door ahead or a key / door under them, whose waves take the longer value
+// sweep (dk_step_fast's GOAL / KD forms, up to 1.7x the VALU work of the plain form).  With the
+// <= ~10 special cells of a DoorKey grid in one wave, the other waves all run the plain form
+// (row-major, 2.7 of a 16x16 grid's 4 waves had some special cell, 2.1 the KD form; 200 seeds).
+// The LDS tiles and HBM rows stay indexed by cell: only which thread owns which cell changes, so V,
+// pi and the sweep count are untouched.  Whole block (two barriers); `perm`: 2*HW bytes of LDS,
+// `cnt`: 32 ints.  Returns this thread's cell (threads past HW keep their index: idle slots).
+__device__ __forceinline__ int dk_class_perm(const uint8_t *cl, const Geo &geo, int16_t *perm, int *cnt) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, nw = (int)(blockDim.x >> 6);
+    bool special = false;
+    if (t < geo.HW) special = dk_fast_class(dk_fast_topo(dk_topo_soa(cl, geo, t), geo.HWs)) != 0u;
+    const unsigned long long bs = __builtin_amdgcn_ballot_w64(special);
+    const unsigned long long bv = __builtin_amdgcn_ballot_w64(t < geo.HW);
+    if (lane == 0) {
+        cnt[w] = __popcll(bs);
+        cnt[16 + w] = __popcll(bv & ~bs);
+    }
+    __syncthreads();
+    int before_s = 0, before_p = 0, total_s = 0;
+    for (int i = 0; i < nw; ++i) {
+        if (i < w) {
+            before_s += cnt[i];
+            before_p += cnt[16 + i];
+        }
+        total_s += cnt[i];
+    }
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    if (t < geo.HW) {
+        const int dest = special ? before_s + __popcll(bs & lt) : total_s + before_p + __popcll(bv & ~bs & lt);
+        perm[dest] = (int16_t)t;
+    }
+    __syncthreads();
+    return t < geo.HW ? (int)perm[t] : t;
+}
+
+// perm_lds: with an LDS scratch (see dk_class_perm; 2*HW + 128 bytes), threads take the cells of
+// the special-first map; nullptr keeps thread t on cell t.
 template <typename T, bool LOCAL, int HMODE = 0, typename Done>  // HMODE: see fused_fast_xyd_soa
 __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> &cf, const uint8_t *cl,
                                                   T *V0, T *V1, T *slots, uint8_t *flags,
                                                   const T *Vg, T *Vg_out, int8_t *pig, int &k,
                                                   int k_target, double &dvl, const Done &done,
                                                   const T *rgoal = nullptr, int8_t *pit = nullptr,
-                                                  long long pit_stride = 0, const DkTopo *pre = nullptr) {
-    const int c = threadIdx.x;
+                                                  long long pit_stride = 0, const DkTopo *pre = nullptr,
+                                                  uint8_t *perm_lds = nullptr) {
+    const int c = perm_lds ? dk_class_perm(cl, geo, reinterpret_cast<int16_t *>(perm_lds),
+                                           reinterpret_cast<int *>(perm_lds + (2 * geo.HW + 15) / 16 * 16))
+                           : (int)threadIdx.x;
     const int cc = c < geo.HW ? c : 0;
     const bool own_cell = c < geo.HW;
     const int HW = geo.HWs;  // LDS stride: every thread (idle ones too) owns a slot, so LDS writes need no mask
