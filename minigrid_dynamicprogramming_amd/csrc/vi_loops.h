@@ -6,6 +6,10 @@
 #pragma once
 
 // MGDP_RUNTO_DV_ALL=1 (A/B builds): k_target loops compute |dV| on every sweep, not only the last.
+// MGDP_DK_DEAD=0 (A/B builds): batched DoorKey waves of absorbing cells only do the full sweep.
+#ifndef MGDP_DK_DEAD
+#define MGDP_DK_DEAD 1
+#endif
 #ifndef MGDP_RUNTO_DV_ALL
 #define MGDP_RUNTO_DV_ALL 0
 #endif
@@ -1235,30 +1239,42 @@ __device__ __forceinline__ DkTopo dk_topo_soa(const uint8_t *cl, const Geo &geo,
 // <= ~10 special cells of a DoorKey grid in one wave, the other waves all run the plain form
 // (row-major, 2.7 of a 16x16 grid's 4 waves had some special cell, 2.1 the KD form; 200 seeds).
 // The LDS tiles and HBM rows stay indexed by cell: only which thread owns which cell changes, so V,
-// pi and the sweep count are untouched.  Whole block (two barriers); `perm`: 2*HW bytes of LDS,
-// `cnt`: 32 ints.  Returns this thread's cell (threads past HW keep their index: idle slots).
+// pi and the sweep count are untouched.  Absorbing cells (walls, the goal: no walkable state) go
+// last, so the 74 of a DoorKey-16 grid fill its fourth wave, which then skips the arithmetic
+// (fused_fast_dk_soa's `wdead`).  Whole block (two barriers); `perm`: 2*HW bytes of LDS, `cnt`:
+// 32 ints.  Returns this thread's cell (threads past HW keep their index: idle slots).
 __device__ __forceinline__ int dk_class_perm(const uint8_t *cl, const Geo &geo, int16_t *perm, int *cnt) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, nw = (int)(blockDim.x >> 6);
-    bool special = false;
-    if (t < geo.HW) special = dk_fast_class(dk_fast_topo(dk_topo_soa(cl, geo, t), geo.HWs)) != 0u;
+    bool special = false, walk = false;
+    if (t < geo.HW) {
+        const DkFast q = dk_fast_topo(dk_topo_soa(cl, geo, t), geo.HWs);
+        special = dk_fast_class(q) != 0u;
+        walk = q.walk != 0u;
+    }
     const unsigned long long bs = __builtin_amdgcn_ballot_w64(special);
+    const unsigned long long bp = __builtin_amdgcn_ballot_w64(walk && !special);
     const unsigned long long bv = __builtin_amdgcn_ballot_w64(t < geo.HW);
     if (lane == 0) {
         cnt[w] = __popcll(bs);
-        cnt[16 + w] = __popcll(bv & ~bs);
+        cnt[16 + w] = __popcll(bp);
     }
     __syncthreads();
-    int before_s = 0, before_p = 0, total_s = 0;
+    int before_s = 0, before_p = 0, total_s = 0, total_p = 0;
     for (int i = 0; i < nw; ++i) {
         if (i < w) {
             before_s += cnt[i];
             before_p += cnt[16 + i];
         }
         total_s += cnt[i];
+        total_p += cnt[16 + i];
     }
     const unsigned long long lt = (1ull << lane) - 1ull;
     if (t < geo.HW) {
-        const int dest = special ? before_s + __popcll(bs & lt) : total_s + before_p + __popcll(bv & ~bs & lt);
+        // the waves before w hold 64*w cells; those not special or plain are absorbing
+        const int before_a = 64 * w - before_s - before_p;
+        const int dest = special ? before_s + __popcll(bs & lt)
+                         : walk  ? total_s + before_p + __popcll(bp & lt)
+                                 : total_s + total_p + before_a + __popcll(bv & ~bs & ~bp & lt);
         perm[dest] = (int16_t)t;
     }
     __syncthreads();
@@ -1288,6 +1304,11 @@ __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> 
     const DkFast tpf = dk_fast_topo(tp, HW);
     const uint32_t cls = dk_fast_class(tpf);
     const uint32_t wcls = (__builtin_amdgcn_ballot_w64(cls & 1u) ? 1u : 0u) | (__builtin_amdgcn_ballot_w64(cls & 2u) ? 2u : 0u);
+    // A wave of absorbing cells only (idle slots read cell 0, a border wall): every value it owns
+    // is +0 in both tiles and stays +0 (dk_step_fast yields exactly +0 there), so its value sweeps
+    // store +0 with no arithmetic and no front reads.  The special-first map packs a DoorKey-16
+    // grid's absorbing cells into its fourth wave.
+    const bool wdead = MGDP_DK_DEAD && __builtin_amdgcn_ballot_w64(tp.walk != 0u) == 0ull;
     T own[16];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1307,7 +1328,11 @@ __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> 
         uint32_t pk[4];
         const T rg = HMODE ? rgoal[k_target - 1 - k] : (T)1;
         T d;
-        if (HMODE != 2) {
+        if (HMODE != 2 && wdead) {
+#pragma unroll
+            for (int l = 0; l < 16; ++l) outv[l] = (T)0;
+            d = (T)0;
+        } else if (HMODE != 2) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) nbs[q] = *reinterpret_cast<const V4<T> *>(Vin + tpf.nb[q]);
             // a k_target loop reports |dV| of its last sweep only: the others skip the differences
