@@ -92,13 +92,21 @@ def compulsory_bytes_per_sweep(S: int, HW: int, tsize: int) -> int:
     return 2 * S * tsize + HW
 
 
+def shard_of(world: int) -> int:
+    """How many ways a sharded workload's global batch is split: the world size, or at world 1 the
+    MGDP_BENCH_SHARD_OF=N rehearsal knob (never set by the driver), which makes the one rank solve
+    rank 0's shard of an N-way split -- the per-rank work of an N-GPU run, measured on one GPU."""
+    n = int(os.environ.get("MGDP_BENCH_SHARD_OF", "0") or 0)
+    return n if world == 1 and n > 1 else world
+
+
 def make_cells(spec, rank, world):
     from minigrid_dynamicprogramming_amd import make
     from minigrid_dynamicprogramming_amd.distributed import shard_range
 
     env = make(spec["env_id"])
     if spec.get("sharded"):
-        lo, hi = shard_range(spec["global_grids"], rank, world)
+        lo, hi = shard_range(spec["global_grids"], rank, shard_of(world))
     elif spec.get("distinct"):
         lo, hi = rank * spec["distinct"], (rank + 1) * spec["distinct"]
     else:
@@ -427,6 +435,7 @@ def main():
             "parallelism": (f"shard{world} + RCCL dV all-reduce" if sharded else
                             ("replicas only" if spec["replicate"] else f"independent batches x{world}")),
             "host_thread": (f"pinned to the GPU's NUMA node ({pinned} CPUs)" if pinned else "unpinned"),
+            **({"emulated_shard_of": shard_of(world)} if spec["sharded"] and shard_of(world) != world else {}),
         },
         "sweeps": int(m["sweeps"][-1]),
         "roofline": roofline,

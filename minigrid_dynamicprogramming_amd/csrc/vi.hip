@@ -1335,6 +1335,9 @@ int mgdp_vi_resume(mgdp_vi *vi, const void *V, int32_t k, double dv, int32_t *sw
                "resume: the checkpoint has converged (dV %g < tol %g); its V and pi are final", dv, vi->d.tol);
     DeviceGuard guard(vi->d.device);
     if (int rc = server_stop(vi)) return rc;
+    // the copies below go through the null stream: drain the handle's own (or a caller-bound,
+    // possibly non-blocking) stream first, so no earlier launch still reads V / kenv / dvenv
+    MGDP_HIP(hipStreamSynchronize(vi->stream));
     const size_t BS = (size_t)vi->d.B * vi->S;
     MGDP_HIP(hipMemcpy(vi->d_V[0], V, BS * vi->tsize, hipMemcpyHostToDevice));
     std::vector<int32_t> kk((size_t)vi->d.B, k);

@@ -18,6 +18,22 @@ __host__ __device__ constexpr bool wp_is_pair(int wp) { return wp <= kWpPair - 1
 // (fused_wave2_xyd, its own compact LDS layout; vi_fused_kernel only).
 constexpr int kWpWave2 = -400;
 __host__ __device__ constexpr bool wp_is_wave2(int wp) { return wp <= kWpWave2 - 1 && wp >= kWpWave2 - 8; }
+// Minimum waves per SIMD the one-wave kernels are compiled for.  Left alone, the fp32 P <= 2
+// variants (LavaS11N5: 121 cells) take 57 VGPRs but 106 SGPRs, and the SGPRs cap them at 7 waves
+// per SIMD (28 workgroups / CU, 7168 grids resident): 8 makes the compiler fit 8 waves' SGPRs too
+// (78 SGPRs, 32 / CU, 8192 resident -- an 8-way shard of LavaS11N5 x 65536 then fits the
+// launch-wide rule in one launch: 89 -> 60 us per solve; the whole 65536 batch +4.5 %).  Same for
+// fp64 P = 1 (57 VGPRs); the other variants are VGPR-bound at <= 6 waves.  Batches at the SGPR-bound
+// residency also hit a dispatcher limit the occupancy API does not see: LavaS11N5 x 7168 at 28 / CU
+// took 199 us (waiting grids ran to the cap) against 57 us at 32 / CU (profiles/r03_w8/).
+// MGDP_WAVE2_W8=0 (A/B builds) keeps the compiler's default.
+#ifndef MGDP_WAVE2_W8
+#define MGDP_WAVE2_W8 1
+#endif
+template <typename T>
+__host__ __device__ constexpr int wave2_min_waves(int wp) {
+    return (MGDP_WAVE2_W8 && wp_is_wave2(wp) && kWpWave2 - wp <= (sizeof(T) == 4 ? 2 : 1)) ? 8 : 1;
+}
 // vi_fused_kernel variant tag: batched DoorKey, a cell's states split over two threads by has_key
 // (fused_dk_half; workgroup = 2 * HWs threads)
 // Tags -501 .. -508: plane stride HWs = 64 * (-tag - 500) known at compile time.
@@ -216,7 +232,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
 // WP > 0: the one-wave lone-grid variant (fused_wave_xyd), 64 threads, so its WP cells per lane
 // may use the whole register file.
 template <typename T, int MODEL, bool SLIP, int MAP, int WP = 0>
-__global__ void __launch_bounds__(WP > 0 || wp_is_wave2(WP) ? 64 : 1024)
+__global__ void __launch_bounds__(WP > 0 || wp_is_wave2(WP) ? 64 : 1024, wave2_min_waves<T>(WP))
 vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
