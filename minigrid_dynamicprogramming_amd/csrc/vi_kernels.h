@@ -30,9 +30,14 @@ __host__ __device__ constexpr bool wp_is_wave2(int wp) { return wp <= kWpWave2 -
 #ifndef MGDP_WAVE2_W8
 #define MGDP_WAVE2_W8 1
 #endif
+#ifndef MGDP_WAVE2_P4_W6  // A/B builds: fp32 P = 4 (Empty-16) at 6 waves instead of its 91-VGPR 5
+#define MGDP_WAVE2_P4_W6 0
+#endif
 template <typename T>
 __host__ __device__ constexpr int wave2_min_waves(int wp) {
-    return (MGDP_WAVE2_W8 && wp_is_wave2(wp) && kWpWave2 - wp <= (sizeof(T) == 4 ? 2 : 1)) ? 8 : 1;
+    return (MGDP_WAVE2_W8 && wp_is_wave2(wp) && kWpWave2 - wp <= (sizeof(T) == 4 ? 2 : 1)) ? 8
+           : (MGDP_WAVE2_P4_W6 && wp_is_wave2(wp) && sizeof(T) == 4 && kWpWave2 - wp == 4) ? 6
+                                                                                            : 1;
 }
 // vi_fused_kernel variant tag: batched DoorKey, a cell's states split over two threads by has_key
 // (fused_dk_half; workgroup = 2 * HWs threads)
