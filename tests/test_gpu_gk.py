@@ -73,3 +73,15 @@ def test_slip_grids_are_not_fixed_points_and_fall_back():
     assert r.sweeps == o["sweeps"]
     np.testing.assert_array_equal(r.V, o["V"])
     np.testing.assert_array_equal(r.pi, o["pi"])
+
+
+
+def test_non_resident_batch_matches_oracle():
+    # more one-wave grids than the GPU holds at once (P = 1: 32 workgroups / CU, 8192 grids): no
+    # launch-wide rule, the chained own-rule + run_to launches -- same sweeps, V and pi as the oracle
+    cells = random_grids(9000, 9, 7, seed=11, goals=2)
+    o = oracle.value_iteration(0, cells, dtype="f32", nthreads=8)
+    k, V, pi, per_solve = _solve_timed(cells, "f32", {})
+    assert k == o["sweeps"] and per_solve == 2, per_solve
+    np.testing.assert_array_equal(pi, o["pi"])
+    np.testing.assert_array_equal(V, o["V"])
