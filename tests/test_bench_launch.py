@@ -40,3 +40,20 @@ def test_single_gpu_does_not_self_launch():
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert out["n_gpus"] == 1 and "launching" not in r.stderr
+
+
+def test_shard_of_rehearsal_knob(monkeypatch):
+    # MGDP_BENCH_SHARD_OF=N (tools/gpu_shard.sh) gives a world-1 run rank 0's shard of an N-way split;
+    # it never changes a real multi-rank run
+    import importlib.util
+
+    from minigrid_dynamicprogramming_amd.distributed import shard_range
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    monkeypatch.delenv("MGDP_BENCH_SHARD_OF", raising=False)
+    assert bench.shard_of(1) == 1 and bench.shard_of(4) == 4
+    monkeypatch.setenv("MGDP_BENCH_SHARD_OF", "8")
+    assert bench.shard_of(1) == 8 and bench.shard_of(2) == 2
+    assert shard_range(65536, 0, bench.shard_of(1)) == (0, 8192)
