@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # MGDP_LIB: an alternative build of the same sources (tools/ experiments with compile-time knobs)
 LIB_PATH = os.environ.get("MGDP_LIB") or os.path.join(HERE, "libmgdp.so")
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 MGDP_OK = 0
 MGDP_E_INVALID = -1
 MGDP_E_HIP = -2
@@ -98,6 +98,7 @@ SIGNATURES = {
     "mgdp_vi_synchronize": (ctypes.c_int, [_P]),
     "mgdp_vi_enable_timing": (ctypes.c_int, [_P, _I32]),
     "mgdp_vi_kernel_time": (ctypes.c_int, [_P, _DP, _I64P]),
+    "mgdp_vi_serve_clock": (ctypes.c_int, [_P, _DP, _DP, _I64P]),
     "mgdp_vi_persistent": (ctypes.c_int, [_P, _I32P]),
     "mgdp_vi_kernel_name": (ctypes.c_char_p, [_P]),
     "mgdp_vi_get_policy_t": (ctypes.c_int, [_P, _P]),

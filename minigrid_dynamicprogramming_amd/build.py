@@ -23,8 +23,25 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Xarch_d
          "-Xarch_device", "-fno-slp-vectorize", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result"]
 
 
+def _extra_flags() -> list:
+    # MGDP_EXTRA_FLAGS: compile-time knobs of an A/B build (e.g. -DMGDP_SERVE_TRACE), with MGDP_BUILD_OUT
+    return os.environ.get("MGDP_EXTRA_FLAGS", "").split()
+
+
+def _stamp_path() -> str:
+    return OUT + ".flags"
+
+
 def needs_build() -> bool:
+    """Stale if any source or the header is newer than the library, or the library was built with
+    other compile flags (recorded beside it in <OUT>.flags)."""
     if not os.path.exists(OUT):
+        return True
+    try:
+        with open(_stamp_path()) as f:
+            if f.read() != " ".join(FLAGS + _extra_flags()):
+                return True
+    except OSError:
         return True
     t = os.path.getmtime(OUT)
     deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [
@@ -39,10 +56,16 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     if not force and not needs_build():
         return OUT
-    objdir = os.path.join(os.path.dirname(OUT) if os.environ.get("MGDP_BUILD_OUT") else HERE, "build")
-    os.makedirs(objdir, exist_ok=True)
-    # MGDP_EXTRA_FLAGS: compile-time knobs of an A/B build (e.g. -DMGDP_LAZY_STOP=0), with MGDP_BUILD_OUT
-    cflags = [f for f in FLAGS if f != "-shared"] + os.environ.get("MGDP_EXTRA_FLAGS", "").split()
+    import hashlib
+    import tempfile
+
+    extra = _extra_flags()
+    # objects of one output and flag set never meet another build's: a private directory per build
+    # (parallel builds of A/B variants in one folder cannot overwrite each other's .o files)
+    tag = hashlib.sha256((OUT + "\0" + " ".join(extra)).encode()).hexdigest()[:12]
+    os.makedirs(os.path.join(HERE, "build"), exist_ok=True)
+    objdir = tempfile.mkdtemp(prefix=f"obj_{tag}_", dir=os.path.join(HERE, "build"))
+    cflags = [f for f in FLAGS if f != "-shared"] + extra
     jobs = []
     for src in SOURCES:
         obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
@@ -55,9 +78,14 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     with ThreadPoolExecutor(max_workers=min(len(jobs), os.cpu_count() or 1)) as ex:
         list(ex.map(run, [c for _, c in jobs]))
-    link = [HIPCC, *FLAGS, "-o", OUT + ".tmp", *[o for o, _ in jobs]]
-    run(link)
-    os.replace(OUT + ".tmp", OUT)
+    tmp = f"{OUT}.tmp{os.getpid()}"
+    run([HIPCC, *FLAGS, "-o", tmp, *[o for o, _ in jobs]])
+    os.replace(tmp, OUT)
+    with open(_stamp_path(), "w") as f:
+        f.write(" ".join(FLAGS + extra))
+    import shutil
+
+    shutil.rmtree(objdir, ignore_errors=True)
     return OUT
 
 

@@ -130,6 +130,11 @@ struct mgdp_vi {
     bool last_req = false;        // the request being posted is the server's last (mgdp_vi_solve_last)
     bool exiting = false;         // a server told to leave after its last request is the stream's last work
     unsigned long long serve_tag = 0;  // tag of the latest server launch: its exit word (h_out[11]) carries it
+    // clock of the departed servers since enable_timing (mgdp_vi_serve_clock): shader-clock cycles and
+    // 100 MHz ticks of their lives, summed as each one's exit word is seen (kHoutClk)
+    unsigned long long clk_tag = 0;  // the last server launch whose clock words were added
+    double clk_cycles = 0.0, clk_ticks = 0.0;
+    long long clk_launches = 0;
     // launch-wide global rule (GkCtx, fused_wave2_xyd): one launch per batched solve when every grid
     // wave of the batch can be resident at once (MGDP_GK=0 turns it off)
     bool gk = false;
@@ -389,6 +394,8 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
     return 0;
 }
 
+void account_server_clock(mgdp_vi *vi);
+
 template <typename T, int MODEL, bool SLIP, int MAP>
 int launch_serve_t(mgdp_vi *vi, unsigned int served) {
     const Geo g = make_geo(vi);
@@ -407,6 +414,7 @@ int launch_serve_t(mgdp_vi *vi, unsigned int served) {
     if (smem > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
     TimedPair tp;
     if (int rc = timed_begin(vi, -1, &tp)) return rc;
+    account_server_clock(vi);  // a server that left on its own (idle / life limit) before this relaunch
     ++vi->serve_tag;
     hipExtLaunchKernelGGL(kern, dim3(1), dim3(vi->fused_block), smem, vi->stream, tp.a, tp.b, 0, g,
                           make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv, vi->d_dvenv,
@@ -549,14 +557,18 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
 #ifdef MGDP_SERVE_TRACE
     // trace build (tools/probe_serve_trace.sh): server-side s_memrealtime stamps, 10 ns ticks --
     // [8] request seen by the workgroup, [9] result about to be published
-    if (tagged) {  // mean of each block of 1000 solves
-        static double n = 0, solve = 0;
+    if (tagged) {  // each block of 1000 solves: mean GPU-side time, the shader clock over it, and when
+        static double n = 0, solve = 0, cyc = 0;
+        static const auto t_first = std::chrono::steady_clock::now();
         n += 1;
         solve += (double)(h[9] - h[8]) * 0.01;
+        cyc += (double)(h[15] - h[14]);
         if ((long long)n % 1000 == 0) {
-            std::fprintf(stderr, "serve trace: solves %.0f-%.0f, request seen -> publish %.3f us (sweeps %llu)\n", n - 999, n,
-                         solve / 1000.0, (unsigned long long)(h[5] & 0xffffffffull));
+            const double t_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_first).count();
+            std::fprintf(stderr, "serve trace: solves %.0f-%.0f, t %.1f ms, request seen -> publish %.3f us, sclk %.0f MHz (sweeps %llu)\n",
+                         n - 999, n, t_ms, solve / 1000.0, cyc / solve, (unsigned long long)(h[5] & 0xffffffffull));
             solve = 0;
+            cyc = 0;
         }
     }
 #endif
@@ -591,6 +603,16 @@ bool serve_eligible(const mgdp_vi *vi) {
 // completion signal, which a later device synchronize still observes.
 // Wait for the exit word of the latest server launch (its own tag: a late store of an earlier
 // server cannot satisfy it); a server that never started or faulted is reported by the stream.
+// Add a departed server's clock words (written before its exit word, which is a release) once.
+void account_server_clock(mgdp_vi *vi) {
+    const volatile unsigned long long *h = vi->h_out;
+    if (vi->serve_tag == 0 || vi->clk_tag == vi->serve_tag || h[11] != vi->serve_tag) return;
+    std::atomic_thread_fence(std::memory_order_acquire);
+    vi->clk_cycles += (double)h[kHoutClk];
+    vi->clk_ticks += (double)h[kHoutClk + 1];
+    ++vi->clk_launches;
+    vi->clk_tag = vi->serve_tag;
+}
 int wait_server_exit(mgdp_vi *vi) {
     const volatile unsigned long long *h = vi->h_out;
     for (uint64_t spin = 0; h[11] != vi->serve_tag; ++spin) {
@@ -601,6 +623,7 @@ int wait_server_exit(mgdp_vi *vi) {
         }
     }
     std::atomic_thread_fence(std::memory_order_acquire);
+    account_server_clock(vi);
     return 0;
 }
 int server_stop(mgdp_vi *vi, bool drain = true) {
@@ -609,6 +632,7 @@ int server_stop(mgdp_vi *vi, bool drain = true) {
         vi->serving = false;
         if (drain) {
             MGDP_HIP(hipStreamSynchronize(vi->stream));
+            account_server_clock(vi);
         } else if (int rc = wait_server_exit(vi)) {
             return rc;
         }
@@ -1467,6 +1491,19 @@ int mgdp_vi_enable_timing(mgdp_vi *vi, int32_t on) {
     vi->timing = on != 0;
     vi->total_ms = 0.0;
     vi->launches = 0;
+    vi->clk_cycles = vi->clk_ticks = 0.0;
+    vi->clk_launches = 0;
+    return 0;
+}
+
+int mgdp_vi_serve_clock(mgdp_vi *vi, double *sclk_mhz, double *server_us, int64_t *launches) {
+    MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
+    DeviceGuard guard(vi->d.device);
+    if (int rc = server_stop(vi)) return rc;
+    account_server_clock(vi);
+    if (sclk_mhz) *sclk_mhz = vi->clk_ticks > 0 ? vi->clk_cycles / (vi->clk_ticks * 0.01) : 0.0;
+    if (server_us) *server_us = vi->clk_ticks * 0.01;
+    if (launches) *launches = vi->clk_launches;
     return 0;
 }
 

@@ -126,6 +126,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
         if (SERVED) {
             if (threadIdx.x == 0) {
 #ifdef MGDP_SERVE_TRACE
+                __hip_atomic_store(host_out + 15, __builtin_amdgcn_s_memtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(host_out + 9, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #endif
                 publish_tagged(host_out, kk, dv, epoch);
@@ -297,6 +298,7 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
 // (s_memrealtime, 100 MHz); the host relaunches the server if a request finds it gone.
 constexpr int kHoutWords = 32;  // host-mapped words of a handle (mgdp_vi::h_out)
 constexpr int kHoutReq = 16;    // request word; its source word follows (one 16-B pair)
+constexpr int kHoutClk = 24;    // a departing server's {shader-clock cycles, 100 MHz ticks} of its life
 constexpr unsigned long long kServeQuit = ~0ull;
 constexpr unsigned long long kServeNewCells = 1ull << 62;
 constexpr unsigned long long kServeLast = 1ull << 61;  // request flag: leave after serving it
@@ -342,6 +344,7 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
     }
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long c_start = __builtin_amdgcn_s_memtime();  // shader-clock cycles
     unsigned long long t_last = t_start;
     __syncthreads();
     // the grid stays put between kServeNewCells requests: resolve this thread's cell topology once
@@ -398,8 +401,10 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
         const unsigned long long cmd = s_cmd;
         if (cmd == kServeQuit) break;
 #ifdef MGDP_SERVE_TRACE
-        if (threadIdx.x == 0)
+        if (threadIdx.x == 0) {  // s_memtime counts shader-clock cycles, s_memrealtime 100 MHz ticks
+            __hip_atomic_store(host_out + 14, __builtin_amdgcn_s_memtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_out + 8, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
 #endif
         if (cmd & kServeNewCells) {  // restage the grid named by the request
             const uint8_t *src = reinterpret_cast<const uint8_t *>(s_src);
@@ -432,9 +437,16 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
     // (server_stop without a drain waits for this word instead of the stream's completion signal).
     // The word is this launch's own tag, so an earlier server's late exit store can never satisfy
     // the wait for a later one.
+    // The launch's shader-clock cycles and 100 MHz ticks go out with it (kHoutClk): the host turns
+    // them into the clock the server ran at (mgdp_vi_serve_clock), at no cost per solve.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(host_out + 11, exit_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(host_out + kHoutClk, __builtin_amdgcn_s_memtime() - c_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host_out + kHoutClk + 1, __builtin_amdgcn_s_memrealtime() - t_start, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host_out + 11, exit_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // The fused solve with the SURVEY 8(f) item-3 options (ND = NoDeath lava, HMODE = finite horizon
