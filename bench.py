@@ -415,6 +415,8 @@ def main():
                     blk.update({"global_grids": (bhi - blo) * world, "scaling": "weak",
                                 "parallelism": f"independent batches x{world}"})
                 blk["roofline"] = workload_roofline(args, args.dtype, bm, name, bhi - blo)
+                if bm.get("executed"):
+                    blk["executed_rank0"] = bm["executed"]
                 if bm.get("collectives"):
                     blk["collectives"] = bm["collectives"]
                 if world == 1 and not args.no_cpu:
@@ -463,6 +465,8 @@ def main():
         out["collectives"] = m["collectives"]
     if m.get("latency"):
         out["latency"] = m["latency"]
+    if m.get("executed"):
+        out["executed_rank0"] = m["executed"]
     if batched:
         out["batched"] = batched
     if blocks:
@@ -603,6 +607,7 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded):
                                       "dev_sync": round(us[-1], 2), "region": round(elapsed * 1e6, 2)}}))
     kern_ms, launches = vi.kernel_time()
     clock = vi.serve_clock() if vi.persistent else None
+    gsw = vi.grid_sweeps() if vi.B > 1 else None  # sweeps each grid executed in the last solve
     vi.enable_timing(False)
     info = {"A": 7 if vi.model == "xyd" else 5, "W": vi.W, "H": vi.H, "S": vi.S, "B": vi.B, "model": vi.model,
             "updates_per_sweep": vi.updates_per_sweep, "kernel": vi.kernel_name, "persistent": vi.persistent}
@@ -640,7 +645,15 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded):
         if clock and clock["launches"]:
             lat["device_clock"] = {**clock, "source": "vi_serve_kernel s_memtime cycles / s_memrealtime over its "
                                                       "launches (priming + timed solves)"}
+    executed = None
+    if gsw is not None and sweeps[-1] > 0:
+        executed = {"mean_grid_sweeps": round(float(gsw.mean()), 3), "global_sweeps": int(sweeps[-1]),
+                    "frac_of_global_rule": round(float(gsw.mean()) / sweeps[-1], 4),
+                    "note": "fixed-point completion: a grid whose own rule stopped at an exact fixed point "
+                            "(|dV| = 0) is complete for the global K (V, pi bit-identical), its remaining "
+                            "K - k_e sweeps are not executed; value counts B*S*A*K as the metric defines"}
     return {"elapsed_max": elapsed_max, "upd_total": upd_total, "sweeps": sweeps, "kern_ms": kern_ms,
+            "executed": executed,
             "launches": launches, "primed": primed, "info": info, "collectives": collectives, "latency": lat}
 
 

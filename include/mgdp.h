@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MGDP_ABI_VERSION 8
+#define MGDP_ABI_VERSION 9
 
 enum {
     MGDP_OK = 0,
@@ -166,10 +166,13 @@ int mgdp_vi_sweep(mgdp_vi *vi, double *dv_out);
 int mgdp_vi_finish(mgdp_vi *vi, int32_t sweeps);
 /* Checkpoint / resume (ABI 7; fused method, no horizon): continue a solve that stopped at sweep k
  * before converging (a max_sweeps cap) from its state {V_k (B*S values of the handle's dtype, as
- * mgdp_vi_get_values returns them), k, dV_k} -- on this or a new handle of the same grids and
- * parameters.  Jacobi is memoryless given V_k: the result (global stopping sweep, V, pi, dV) is
- * bit-identical to the uninterrupted solve.  k in [1, max_sweeps); dV >= tol (a converged
- * checkpoint is final: its pi is not rebuildable from V_k). */
+ * mgdp_vi_get_values returns them), k, dV_k} -- on a handle of the same grids and parameters
+ * whose max_sweeps exceeds k (a solve capped at max_sweeps resumes on a handle with a larger cap,
+ * not on the capped one).  Jacobi is memoryless given V_k: the result (global stopping sweep, V,
+ * pi, dV) is bit-identical to the uninterrupted solve.  k in [1, max_sweeps); dV >= tol (a
+ * converged checkpoint is final: its pi is not rebuildable from V_k).  The C ABI cannot tell
+ * whose V it is given: the Python checkpoint carries the grids' digest and the parameters and
+ * ValueIteration.resume refuses a mismatch. */
 int mgdp_vi_resume(mgdp_vi *vi, const void *V, int32_t k, double dv, int32_t *sweeps_out, double *dv_out,
                    int32_t *converged_out);
 
@@ -201,6 +204,11 @@ int mgdp_vi_get_policy(mgdp_vi *vi, int8_t *pi);
 int mgdp_vi_get_policy_t(mgdp_vi *vi, int8_t *pi_t);
 /* Per-sweep global max|dV| (method SWEEP only; fused runs record only the last): n <= max_sweeps */
 int mgdp_vi_get_dv_trace(mgdp_vi *vi, double *trace, int32_t n);
+/* Sweeps each grid executed (ABI 9), B int32: a grid whose own rule stopped at an exact fixed
+ * point (|dV| = 0) reports that sweep -- its V and pi are those of every later sweep, so the
+ * global rule's remaining sweeps are not executed for it (fixed-point completion) -- any other grid
+ * the sweep it was taken to (the global K).  The sweep method reports K for every grid. */
+int mgdp_vi_get_grid_sweeps(mgdp_vi *vi, int32_t *k);
 /* Device pointers of the handle's V (current) and pi buffers, for zero-copy consumers. */
 int mgdp_vi_device_buffers(mgdp_vi *vi, void **d_V, void **d_pi);
 int mgdp_vi_num_states(const mgdp_vi_desc *desc, int64_t *S);

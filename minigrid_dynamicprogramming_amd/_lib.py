@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # MGDP_LIB: an alternative build of the same sources (tools/ experiments with compile-time knobs)
 LIB_PATH = os.environ.get("MGDP_LIB") or os.path.join(HERE, "libmgdp.so")
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 MGDP_OK = 0
 MGDP_E_INVALID = -1
 MGDP_E_HIP = -2
@@ -93,6 +93,7 @@ SIGNATURES = {
     "mgdp_vi_get_values": (ctypes.c_int, [_P, _P]),
     "mgdp_vi_get_policy": (ctypes.c_int, [_P, _P]),
     "mgdp_vi_get_dv_trace": (ctypes.c_int, [_P, _P, _I32]),
+    "mgdp_vi_get_grid_sweeps": (ctypes.c_int, [_P, _P]),
     "mgdp_vi_device_buffers": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
     "mgdp_vi_num_states": (ctypes.c_int, [ctypes.POINTER(ViDesc), _I64P]),
     "mgdp_vi_synchronize": (ctypes.c_int, [_P]),

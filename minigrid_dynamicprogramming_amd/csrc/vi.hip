@@ -138,7 +138,6 @@ struct mgdp_vi {
     // launch-wide global rule (GkCtx, fused_wave2_xyd): one launch per batched solve when every grid
     // wave of the batch can be resident at once (MGDP_GK=0 turns it off)
     bool gk = false;
-    int gk_cap = 256;             // extra sweeps a fixed-point grid does while K is not yet published
     int gk_capacity = 0;          // resident workgroups of the wave2 kernel on this device
     unsigned long long *d_gk = nullptr;
 };
@@ -384,7 +383,7 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
     hipExtLaunchKernelGGL(kern, dim3(vi->d.B), dim3(vi->fused_block), smem, vi->stream, tp.a, tp.b, 0, g,
                        make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv,
                        vi->d_dvenv, vi->d_red, vi->d_ticket, pub, k_target, vi->fresh,
-                       vi->d.B <= vi->inkernel_max ? 1 : 0, ++vi->epoch, k_dev, mirror, gk, vi->gk_cap);
+                       vi->d.B <= vi->inkernel_max ? 1 : 0, ++vi->epoch, k_dev, mirror, gk);
     MGDP_HIP(hipGetLastError());
     vi->fresh = 0;
     if (vi->d.B > vi->inkernel_max && !gk) {  // a launch-wide-rule launch publishes its own reduction
@@ -878,10 +877,9 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
             vi->HWs = (int)round_up(vi->HW, 64);
             vi->Ss = vi->S / vi->HW * vi->HWs;
         }
-        if (vi->wave2) {  // the launch-wide rule needs every grid's wave resident at once
+        if (vi->wave2) {  // the in-launch reduction (GkCtx) when the batch is resident at once
             int gk_on = 1;
             if (const char *ev = std::getenv("MGDP_GK")) gk_on = std::atoi(ev);
-            if (const char *ev = std::getenv("MGDP_GK_CAP")) vi->gk_cap = std::max(1, std::atoi(ev));
             const int smem2 = wave2_smem_bytes(vi->HWp, d.W, vi->wave2, vi->tsize);
             const void *k2 = d.dtype == MGDP_F32
                 ? (const void *)pick_wave2<FusedK, float, MGDP_MODEL_XYD, false, MGDP_MAP_CELL>(
@@ -1145,8 +1143,12 @@ int mgdp_vi_run_to(mgdp_vi *vi, int32_t k_target, double *dv_out) {
     MGDP_CHECK(k_target >= 0 && k_target <= vi->d.max_sweeps, MGDP_E_INVALID, "k_target %d out of range", k_target);
     DeviceGuard guard(vi->d.device);
     if (vi->d.method == MGDP_METHOD_FUSED) {
-        if (vi->k_min == k_target && vi->k_done_valid) {  // every grid is already there
-            vi->k_done = k_target;
+        // every grid is already there: at k_target, or every grid at an exact fixed point (the
+        // largest |dV| of the last launch is 0) at or below it -- fixed-point completion (fused_grid):
+        // its V and pi are those of every later sweep, so no launch is needed
+        const bool all_fixed = vi->dv_red == 0.0 && vi->k_min > 0 && vi->k_max <= k_target && vi->d.horizon == 0;
+        if (vi->k_done_valid && (vi->k_min == k_target || all_fixed)) {
+            vi->k_done = vi->k_min = vi->k_max = k_target;
             *dv_out = vi->dv_red;
             return 0;
         }
@@ -1203,13 +1205,23 @@ int mgdp_vi_run_to_dev_sync(mgdp_vi *vi, const int64_t *d_kdv, int32_t *k_out, d
     MGDP_CHECK(!vi->fresh, MGDP_E_INVALID, "mgdp_vi_run_to_dev_sync before mgdp_vi_run_local_dev");
     DeviceGuard guard(vi->d.device);
     vi->k_done_valid = false;
-    // result -> host-mapped words (reduce_env polls them), d_kdv[1] -> h_out[13] by the launch
-    if (int rc = dispatch<FusedF>(vi, 0, (unsigned long long *)nullptr, reinterpret_cast<const long long *>(d_kdv),
-                                  vi->d_hout + 13))
-        return rc;
     int32_t km = 0;
     double dv = 0.0;
+    // The gate (one wave): with E = d_kdv[1] == 0 every grid of every rank stopped its own rule at an
+    // exact fixed point, so every grid is at K already (fixed-point completion) and the gate
+    // publishes the result {K, dV 0}; else it publishes "more" and run_to(K) follows.  Either way
+    // E goes to h_out[13] and the host waits on host-mapped words only.
+    hipLaunchKernelGGL(vi_gate_kernel, dim3(1), dim3(64), 0, vi->stream, reinterpret_cast<const long long *>(d_kdv),
+                       vi->d_hout, ++vi->epoch);
+    MGDP_HIP(hipGetLastError());
     if (int rc = reduce_env(vi, &km, &dv)) return rc;
+    if (vi->k_min != km) {
+        // result -> host-mapped words (reduce_env polls them), d_kdv[1] -> h_out[13] by the launch
+        if (int rc = dispatch<FusedF>(vi, 0, (unsigned long long *)nullptr, reinterpret_cast<const long long *>(d_kdv),
+                                      vi->d_hout + 13))
+            return rc;
+        if (int rc = reduce_env(vi, &km, &dv)) return rc;
+    }
     MGDP_CHECK(vi->k_min == km, MGDP_E_INVALID, "run_to_dev_sync: grids ended at sweeps %d..%d, not at one common K",
                vi->k_min, km);
     vi->k_done = km;
@@ -1310,9 +1322,11 @@ int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *con
     if (int rc = mgdp_vi_reset(vi)) return rc;
     int32_t k = 0;
     double dv = 0.0;
-    // With the launch-wide rule (vi->gk) the own-rule launch normally ends with every grid at K:
-    // run_local's result is awaited and run_to is launched only if some grid is still below K.
-    if (vi->chain && !vi->gk && vi->d.method == MGDP_METHOD_FUSED && vi->d.horizon == 0 && !vi->opts && !serve_eligible(vi)) {
+    // Deterministic batches take the plain path: their grids end their own rule at exact fixed
+    // points, so run_local's result completes the solve (run_to launches nothing, see
+    // mgdp_vi_run_to) -- one launch and one wait.  Slip batches keep the chained pair.
+    if (vi->chain && !vi->gk && vi->d.slip_p >= 0.0 && vi->d.method == MGDP_METHOD_FUSED && vi->d.horizon == 0 &&
+        !vi->opts && !serve_eligible(vi)) {
         // The single-GPU form of the multi-GPU device protocol: run_local publishes {K, ...} to
         // device memory and run_to(K) reads K there, enqueued back to back -- no host round trip
         // and no launch gap between the two; the host waits once, for run_to's result.
@@ -1442,6 +1456,19 @@ int mgdp_vi_get_policy(mgdp_vi *vi, int8_t *pi) {
     DeviceGuard guard(vi->d.device);
     if (int rc = server_stop(vi)) return rc;
     MGDP_HIP(hipMemcpyAsync(pi, vi->d_pi, (size_t)vi->d.B * vi->S, hipMemcpyDeviceToHost, vi->stream));
+    MGDP_HIP(hipStreamSynchronize(vi->stream));
+    return 0;
+}
+
+int mgdp_vi_get_grid_sweeps(mgdp_vi *vi, int32_t *k) {
+    MGDP_CHECK(vi && k, MGDP_E_INVALID, "null argument");
+    DeviceGuard guard(vi->d.device);
+    if (int rc = server_stop(vi)) return rc;
+    if (vi->d.method == MGDP_METHOD_SWEEP) {
+        std::fill(k, k + vi->d.B, (int32_t)vi->k_done);
+        return 0;
+    }
+    MGDP_HIP(hipMemcpyAsync(k, vi->d_kenv, sizeof(int32_t) * (size_t)vi->d.B, hipMemcpyDeviceToHost, vi->stream));
     MGDP_HIP(hipStreamSynchronize(vi->stream));
     return 0;
 }

@@ -61,7 +61,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
                                            double *__restrict__ dvenv, unsigned long long *__restrict__ host_out,
                                            int k_target, int fresh, bool lone, unsigned int epoch, int e,
                                            int &k, double &dvl, const typename TopoOf<T, MODEL>::type *pre = nullptr,
-                                           unsigned long long *gk = nullptr, int gk_cap = 0, int ew = 0) {
+                                           unsigned long long *gk = nullptr, int ew = 0) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
     T *V0 = reinterpret_cast<T *>(smem);
@@ -73,6 +73,15 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
 
     k = fresh ? 0 : kenv[e];
     dvl = fresh ? 0.0 : dvenv[e];
+    // Fixed-point completion: a grid whose last sweep changed nothing (|dV| = 0 exactly, so
+    // V_k == V_{k-1} bit for bit) reproduces V_k at every later sweep (a Jacobi sweep is a function
+    // of V alone), and pi_{k'} = argmax on V_{k'-1} = pi_k: it is at sweep k_target already, with
+    // dV 0.  Only its sweep count moves (the reduce kernel reads it).
+    if (k_target > k && k > 0 && dvl == 0.0) {
+        if (threadIdx.x == 0) kenv[e] = k_target;
+        k = k_target;
+        return false;
+    }
     const bool work = k_target < 0 ? (!(k > 0 && dvl < geo.tol) && k < geo.max_sweeps) : (k < k_target);
     if (!work) return false;
     const long long vb = (long long)e * geo.S;
@@ -89,9 +98,9 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
                         (unsigned long long)kk, epoch);
         };
         if (k_target < 0) {
-            // the launch-wide rule when the host passed its buffer (buf == nullptr: off)
+            // the in-launch reduction when the host passed its buffer (buf == nullptr: off)
             fused_wave2_xyd<T, true, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2,
-                                        GkCtx{gk, epoch, e, geo.B, gk_cap, host_out});
+                                        GkCtx{gk, epoch, e, geo.B, host_out});
         } else {
             fused_wave2_xyd<T, false, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
         }
@@ -244,7 +253,7 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
                 unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
                 unsigned long long *__restrict__ host_out, int k_target, int fresh, int in_kernel_reduce,
                 unsigned int epoch, const long long *__restrict__ k_target_dev,
-                unsigned long long *__restrict__ host_mirror, unsigned long long *__restrict__ gk, int gk_cap) {
+                unsigned long long *__restrict__ host_mirror, unsigned long long *__restrict__ gk) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
     T *slots = reinterpret_cast<T *>(smem + (wp_is_wave2(WP) ? 0 : L.slots_off()));
@@ -265,7 +274,7 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
     const bool lone = in_kernel_reduce && gridDim.x == 1;
     const bool work = fused_grid<T, MODEL, SLIP, MAP, false, WP>(geo, cf, cells, V, pi, kenv, dvenv, host_out, k_target,
                                                                  fresh, lone, epoch, blockIdx.x, k, dvl, nullptr,
-                                                                 wp_is_wave2(WP) ? gk : nullptr, gk_cap);
+                                                                 wp_is_wave2(WP) ? gk : nullptr);
     // a launch-wide-rule launch (wave2 with gk) reduces and publishes through its own counter tree
     const bool gk_pub = wp_is_wave2(WP) && gk != nullptr && k_target < 0 && !k_target_dev;
     if (in_kernel_reduce && !gk_pub)
@@ -420,7 +429,7 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
         double dvl;
         if (!fused_grid<T, MODEL, SLIP, MAP, true, WP>(geo, cf, cells, V, pi, kenv, dvenv, host_out, -1, 1, true,
                                                    (unsigned int)cmd, 0, k, dvl,
-                                                   (WP == 0 || WP == kWpServeEw) ? &topo : nullptr, nullptr, 0, ew) &&
+                                                   (WP == 0 || WP == kWpServeEw) ? &topo : nullptr, nullptr, ew) &&
             threadIdx.x == 0)
             publish_tagged(host_out, k, dvl, (unsigned int)cmd);
         if (ew == 2) ew = 1;  // the tiles' pads stay +0 until the next grid
@@ -469,6 +478,11 @@ vi_fused_opts_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *
     const int e = blockIdx.x;
     int k = fresh ? 0 : kenv[e];
     double dvl = fresh ? 0.0 : dvenv[e];
+    // fixed-point completion (fused_grid); not for a finite horizon, whose sweeps depend on the step
+    if (HMODE == 0 && k_target > k && k > 0 && dvl == 0.0) {
+        if (threadIdx.x == 0) kenv[e] = k_target;
+        k = k_target;
+    }
     const bool work = k_target < 0 ? (!(k > 0 && dvl < geo.tol) && k < geo.max_sweeps) : (k < k_target);
     const bool lone = in_kernel_reduce && gridDim.x == 1;
     if (work) {
@@ -514,6 +528,19 @@ vi_fused_opts_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *
         }
     }
     if (in_kernel_reduce) fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16), epoch, work);
+}
+
+// The sharded protocol's gate (mgdp_vi_run_to_dev_sync): kdv = the all-reduced {K, E}, written by
+// the collective ordered before this launch.  E == 0: every grid everywhere is at an exact fixed
+// point, so the result is {K, dV 0, K}; else kmin = kGateMore asks the host for run_to(K).
+constexpr unsigned long long kGateMore = 0xffffffffull;
+__global__ void __launch_bounds__(64) vi_gate_kernel(const long long *__restrict__ kdv,
+                                                     unsigned long long *__restrict__ host_out, unsigned int epoch) {
+    if (threadIdx.x == 0) {
+        const unsigned long long K = (unsigned long long)kdv[0], E = (unsigned long long)kdv[1];
+        __hip_atomic_store(host_out + 13, E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        publish(host_out, K, 0ull, E == 0 ? K : kGateMore, epoch);
+    }
 }
 
 // Large batches: one workgroup reduces the per-grid (kenv, dvenv) into host-mapped memory (a

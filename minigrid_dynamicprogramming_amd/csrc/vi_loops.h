@@ -782,44 +782,32 @@ __host__ __device__ inline int wave2_tile_off(int HWp) { return 256 + (HWp + 15)
 __host__ __device__ inline int wave2_smem_bytes(int HWp, int W, int P, int tsize) {
     return wave2_tile_off(HWp) + (2 * 64 * P + 2 * wave2_padw(W)) * tsize;
 }
-// One launch for the whole global rule (mgdp_vi_solve / run_local on a batch whose waves are all
-// resident at once; the host enables it only then): each grid wave, at its own stopping sweep k_e,
-// arrives: it stores k_e to its slot, then draws a ticket of its shard's counter (256 shards by
-// e % 256, each counter on its own 128-B line, so at most B / 256 arrivals contend per line); a
-// shard's last arrival reduces its grids' slots into a shard slot and draws a ticket of the top
-// counter, whose last arrival reduces the shard slots to K = max k_e and publishes K, tagged with
-// the launch epoch, to 512 replicas on separate 128-B lines (a waiting wave polls replica e % 512).  Slots are stored and loaded agent-scope
-// (sc1) and every store is drained before the ticket that announces it (MI355X_MICROARCH.md:
-// inter-workgroup hand-off).  A grid that ended its own rule at an EXACT fixed point (|dV| = 0:
-// V_k == V_{k-1} bit for bit, so every later sweep reproduces it) keeps sweeping, polling its
-// replica once per sweep, until it has done at least K sweeps: every grid performs the K sweeps of
-// the global rule inside this launch, and the separate run_to launch of the batch is not needed.
-// A grid that is not at a fixed point (fp rounding, max_sweeps) stops at k_e as before, and so does
-// a waiting grid after `cap` extra sweeps without K (residency not as planned): the host's run_to
-// launch then takes every grid below K to exactly K.  Reported sweeps (kenv): K if the grid reached
-// it (its V / pi are V_K / pi_K: identical past the fixed point), else its own k_e.
+// In-launch reduction of an own-rule launch (mgdp_vi_solve / run_local on a one-wave batch that is
+// resident at once; the host picks it then, else the reduce kernel follows the launch).  Each grid
+// wave, at its own stopping sweep k_e, stores {k_e, dV} to its slots and draws a ticket of one of
+// 256 shard counters (by e % 256, each counter on its own 128-B line, so at most B / 256 arrivals
+// contend per line); a shard's last arrival folds its grids' slots into the shard's slots and draws
+// a ticket of the top counter, whose last arrival folds the shards and publishes {kmax, dV bits,
+// kmin, epoch}.  Slots are stored and loaded agent-scope (sc1) and every store is drained before
+// the ticket that announces it (MI355X_MICROARCH.md: inter-workgroup hand-off).  No grid waits for
+// another: a grid whose own rule stopped at an EXACT fixed point (|dV| = 0) is complete for every
+// later sweep index (fixed-point completion, see fused_grid), so the global rule needs no K here.
 struct GkCtx {
-    unsigned long long *buf;  // gk_words(B) u64: counters, replicas, shard slots, grid slots (layout below)
+    unsigned long long *buf;  // gk_words(B) u64: counters, shard slots, grid slots (layout below)
     unsigned int epoch;
     int e;                    // grid (workgroup) index
     int B;                    // grids in the launch
-    int cap;                  // extra sweeps a waiting fixed-point grid may do without seeing K
     unsigned long long *pub;  // where the launch's {kmax, dV bits, kmin, epoch} go (host-mapped or device)
 };
 constexpr int kGkShards = 256;
-constexpr int kGkReplicas = 512;  // a replica line per 8 polling waves of a 4096-grid launch
 constexpr int kGkLine = 16;                                    // u64 words per 128-B line
-constexpr int kGkTop = kGkShards * kGkLine;                    // arrival: [256 shard lines][top line]
-constexpr int kGkRep = kGkTop + kGkLine;                       // replica lines
-constexpr int kGkCnt2 = kGkRep + kGkReplicas * kGkLine;        // exit: [256 shard lines][top line]
+constexpr int kGkCnt2 = 0;                                     // [256 shard counter lines][top line]
 constexpr int kGkTop2 = kGkCnt2 + kGkShards * kGkLine;
-constexpr int kGkSslot = kGkTop2 + kGkLine;                    // int32 [256] shard max k_e
-constexpr int kGkSxMin = kGkSslot + kGkShards / 2;             // int32 [256] shard min reported sweeps
+constexpr int kGkSxMin = kGkTop2 + kGkLine;                    // int32 [256] shard min reported sweeps
 constexpr int kGkSxMax = kGkSxMin + kGkShards / 2;             // int32 [256] shard max reported sweeps
 constexpr int kGkSxDv = kGkSxMax + kGkShards / 2;              // u64 [256] shard max dV bits
-constexpr int kGkKslot = kGkSxDv + kGkShards;                  // int32 [B] own stopping sweeps, then
-__host__ __device__ inline int gk_kr_off(int B) { return kGkKslot + (B + 1) / 2; }  // int32 [B] reported sweeps,
-__host__ __device__ inline int gk_dv_off(int B) { return gk_kr_off(B) + (B + 1) / 2; }  // u64 [B] dV bits
+__host__ __device__ inline int gk_kr_off(int B) { (void)B; return kGkSxDv + kGkShards; }  // int32 [B] sweeps,
+__host__ __device__ inline int gk_dv_off(int B) { return gk_kr_off(B) + (B + 1) / 2; }     // u64 [B] dV bits
 __host__ __device__ inline int gk_words(int B) { return gk_dv_off(B) + B; }
 
 __device__ __forceinline__ int wave_max_i(int v) {
@@ -841,48 +829,9 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
     return v;
 }
 
-// The whole wave (uniform call): count this grid's arrival with its own stopping sweep; the
-// launch's last arrival publishes K to the replicas.
-__device__ __forceinline__ void gk_arrive(const GkCtx &g, int k_e) {
-    const int lane = (int)threadIdx.x & 63;
-    int *kslot = reinterpret_cast<int *>(g.buf + kGkKslot);
-    int *sslot = reinterpret_cast<int *>(g.buf + kGkSslot);
-    const int nsh = g.B < kGkShards ? g.B : kGkShards;
-    const int s = g.e % nsh;
-    const int size = g.B / nsh + (s < g.B % nsh ? 1 : 0);
-    unsigned long long t = 0;
-    if (lane == 0) {
-        __hip_atomic_store(kslot + g.e, k_e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        t = __hip_atomic_fetch_add(g.buf + s * kGkLine, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (__builtin_amdgcn_readfirstlane((unsigned int)t) != (unsigned int)(size - 1)) return;
-    // the shard's last arrival: every slot of the shard was drained before its ticket
-    int m = 0;
-    for (int i = lane; i < size; i += 64)
-        m = max(m, __hip_atomic_load(kslot + s + i * nsh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    m = wave_max_i(m);
-    unsigned long long t2 = 0;
-    if (lane == 0) {
-        __hip_atomic_exchange(g.buf + s * kGkLine, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-        __hip_atomic_store(sslot + s, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        t2 = __hip_atomic_fetch_add(g.buf + kGkTop, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (__builtin_amdgcn_readfirstlane((unsigned int)t2) != (unsigned int)(nsh - 1)) return;
-    int K = 0;
-    for (int i = lane; i < nsh; i += 64)
-        K = max(K, __hip_atomic_load(sslot + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    K = wave_max_i(K);
-    if (lane == 0) __hip_atomic_exchange(g.buf + kGkTop, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long w = ((unsigned long long)g.epoch << 32) | (unsigned int)K;
-    for (int r = lane; r < kGkReplicas; r += 64)
-        __hip_atomic_store(g.buf + kGkRep + r * kGkLine, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// The whole wave, once it has its final answer: the launch's {kmax, dV, kmin} reduced over the same
-// counter tree (a second bank), the last exit publishing it -- the reduce kernel a batch launch
-// otherwise needs, folded into the launch.
+// The whole wave, once it has its final answer: the launch's {kmax, dV, kmin} reduced over the
+// counter tree, the last exit publishing it -- the reduce kernel a batch launch otherwise needs,
+// folded into the launch.
 __device__ __forceinline__ void gk_exit(const GkCtx &g, int k_rep, double dv) {
     const int lane = (int)threadIdx.x & 63;
     int *kr = reinterpret_cast<int *>(g.buf + gk_kr_off(g.B));
@@ -942,16 +891,6 @@ __device__ __forceinline__ void gk_exit(const GkCtx &g, int k_rep, double dv) {
     }
 }
 
-// K of this launch if published yet (wave-uniform), else -1.
-__device__ __forceinline__ int gk_poll(const GkCtx &g) {
-    const unsigned long long *rep = g.buf + kGkRep + (g.e & (kGkReplicas - 1)) * kGkLine;
-    unsigned long long w = 0;
-    if ((threadIdx.x & 63) == 0) w = __hip_atomic_load(rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned int hi = __builtin_amdgcn_readfirstlane((unsigned int)(w >> 32));
-    const unsigned int lo = __builtin_amdgcn_readfirstlane((unsigned int)w);
-    return hi == g.epoch ? (int)lo : -1;
-}
-
 template <typename T, bool LOCAL, int P, typename Done>
 __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *tile,
                                                 const T *Vg, T *Vg_out, int8_t *pig, int &k, int k_target,
@@ -993,26 +932,6 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
     const int k_start = k;
     bool more = true;
     T diff = (T)0;
-    // launch-wide rule (gk): this grid's own stopping sweep (-1: not yet), fixed point, K seen
-    int k_e = -1, K_seen = -1;
-    bool fixed = false;
-    // false: stop before this sweep.  Called when the own rule or max_sweeps says stop.
-    // VALU issue on a SIMD goes by priority, then age (MI355X_MICROARCH.md, "two waves per SIMD"):
-    // grids still converging run at priority 1 and a grid sweeping on past its own fixed point drops
-    // to 0, so its no-op sweeps take only the issue slots the converging grids leave
-    if (LOCAL && gk.buf != nullptr) __builtin_amdgcn_s_setprio(1);
-    auto gk_go = [&](bool at_cap) -> bool {
-        if (k_e < 0) {
-            k_e = k;
-            fixed = wave_max(diff) == (T)0;
-            gk_arrive(gk, k_e);
-            __builtin_amdgcn_s_setprio(0);
-        }
-        if (!fixed || at_cap) return false;
-        if (K_seen < 0) K_seen = gk_poll(gk);
-        if (K_seen >= 0) return k < K_seen;
-        return k - k_e < gk.cap;
-    };
     auto sweep = [&](const T (&in)[P][4], T (&out)[P][4]) -> bool {  // `out` written only on commit
         T FS[P], FN[P];
 #pragma unroll
@@ -1021,10 +940,7 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
             FN[j] = N3[j * 64 + lane - W];
         }
         if (LOCAL) {
-            const bool at_cap = k >= geo.max_sweeps;
-            if (at_cap || (k > k_start && !more)) {
-                if (gk.buf == nullptr || !gk_go(at_cap)) return false;
-            }
+            if (k >= geo.max_sweeps || (k > k_start && !more)) return false;
         } else if (k >= k_target) {
             return false;
         }
@@ -1096,15 +1012,7 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
         }
     }
     dvl = (double)wave_max(diff);
-    if (LOCAL && gk.buf != nullptr) {
-        if (k_e < 0) {  // (a launch that stopped before any rule fired cannot happen: k_start = 0)
-            k_e = k;
-            gk_arrive(gk, k_e);
-        }
-        // sweeps to report: K when reached (V_k = V_K past an exact fixed point), else the own stop
-        k = (K_seen >= 0 && k >= K_seen) ? K_seen : k_e;
-        gk_exit(gk, k, dvl);  // this launch's reduction and its publication (no reduce kernel)
-    }
+    if (LOCAL && gk.buf != nullptr) gk_exit(gk, k, dvl);  // this launch's reduction and its publication
     done(k, dvl);
     // pi of the last sweep = argmax on V_{k-1} (`prev`), per action with the usual topology
 #pragma unroll

@@ -28,8 +28,8 @@ the current one and the current one after the collective), run_to reads K on the
 result comes back through host-mapped memory with E (mgdp_vi_run_to_dev_sync): one host wait per
 solve and no stream synchronisation.  Non-negative doubles order like their IEEE-754 bit patterns,
 so a MAX over the int64 bits is the MAX over the values.  Host protocol (gloo, sweep method, DP
-options): the same steps with host-synchronous all-reduces.  Every rank of a group takes the same
-protocol: a one-time MIN all-reduce of "device-capable" settles it per (shard, reducer).
+options, empty shards): the same collectives on the same int64 words, driven from the host, so each
+rank picks its path from its own shard alone and no agreement collective is needed.
 """
 from __future__ import annotations
 
@@ -98,24 +98,6 @@ class Reducer:
         self.wall_s += time.perf_counter() - t
         return v
 
-    def max2(self, a: float, b: float) -> tuple[float, float]:
-        """Host round trip: all-reduce two scalars (MAX each) and read them back."""
-        t = time.perf_counter()
-        self.buf2[0] = float(a)
-        self.buf2[1] = float(b)
-        self.dist.all_reduce(self.buf2, op=self.dist.ReduceOp.MAX, group=self.group)
-        self.calls += 1
-        self.host_reads += 1
-        x, y = self.buf2.tolist()
-        self.wall_s += time.perf_counter() - t
-        return x, y
-
-    def min_flag(self, flag: bool) -> bool:
-        """All-reduce MIN of a 0/1 flag (protocol agreement; not counted in `calls`)."""
-        f = self.torch.tensor([1 if flag else 0], dtype=self.torch.int64, device=self.device)
-        self.dist.all_reduce(f, op=self.dist.ReduceOp.MIN, group=self.group)
-        return bool(int(f.item()))
-
     def max_(self, t):
         """In-place MAX of a tensor (slice of `proto`), ordered on the current stream, no host read."""
         if self.timing:
@@ -166,7 +148,7 @@ class EmptyShard:
     def finish(self, k, dv):
         self.sweeps = k
 
-    protocol_device = None  # either protocol: see _agree_protocol
+    protocol_device = None  # the host path's collectives (the same as the device path's)
 
     def bind_stream(self, stream_ptr):
         pass
@@ -182,25 +164,15 @@ class EmptyShard:
         pass
 
 
-def _agree_protocol(vi, red) -> bool:
-    """Whether this solve takes the device protocol: only if EVERY rank's shard can (a MIN
-    all-reduce of a capability flag, once per (shard, reducer) pair and cached on the shard).
-    An EmptyShard can follow either; a shard whose protocol device differs from the reducer's
-    (e.g. GPU handles under gloo, sweep-method or DP-option handles) forces the host protocol."""
-    cached = getattr(vi, "_mgdp_protocol", None)
-    if cached is not None and cached[0] is red:
-        return cached[1]
+def _device_capable(vi, red) -> bool:
+    """Whether THIS rank's shard can run the device protocol on this reducer (its protocol device is
+    the reducer's: GPU handles under RCCL).  A per-rank choice with no agreement collective: both
+    protocols issue the same collectives (int64 words of `red.proto`, see solve_sharded), so peers
+    may differ (an EmptyShard, a sweep-method or DP-option handle next to fused handles)."""
     if isinstance(vi, EmptyShard):
-        able = True
-    else:
-        dev = getattr(vi, "protocol_device", None)
-        able = dev is not None and dev.type == red.device.type
-    ok = red.min_flag(able)
-    try:
-        vi._mgdp_protocol = (red, ok)
-    except AttributeError:
-        pass
-    return ok
+        return False
+    dev = getattr(vi, "protocol_device", None)
+    return dev is not None and dev.type == red.device.type
 
 
 def _device_protocol(vi, red):
@@ -227,6 +199,35 @@ def _device_protocol(vi, red):
     return k, dv
 
 
+def _host_protocol(vi, red):
+    """The device protocol's collectives, driven from the host: {k_r, own-rule dV bits} into
+    red.proto[0:2], MAX all-reduce, read back; run_to(K); dV at K through red.proto[5] unless every
+    grid everywhere stopped at an exact fixed point.  Same tensors, dtypes and order as
+    _device_protocol, so ranks on either path meet in the same collectives."""
+    p = red.proto
+    vi.reset()
+    k_loc, e_loc = _local(vi)
+    p[0:2].copy_(red.torch.tensor([int(k_loc), double_to_bits(e_loc)], dtype=red.torch.int64))
+    red.max_(p[0:2])
+    t = time.perf_counter()
+    K, e_bits = p[0:2].tolist()
+    red.wall_s += time.perf_counter() - t
+    red.host_reads += 1
+    k = int(K)
+    dv = vi.run_to(k)
+    if bits_to_double(e_bits) == 0.0:
+        if dv != 0.0:
+            raise RuntimeError(f"fixed-point invariant violated: dV at sweep {k} is {dv!r}")
+    else:
+        p[5:6].fill_(double_to_bits(dv))
+        red.max_(p[5:6])
+        t = time.perf_counter()
+        dv = bits_to_double(int(p[5].item()))
+        red.wall_s += time.perf_counter() - t
+        red.host_reads += 1
+    return k, dv
+
+
 def _local(vi):
     """(k_local, own-rule dV) after run_local; a shard without local_result reports dV as unknown."""
     k = vi.run_local()
@@ -242,7 +243,7 @@ def solve_sharded(vi, group=None, reducer=None) -> dict:
     protocol agreement not counted).  Must be called by every rank of the group; build the Reducer
     once and pass it in."""
     red = reducer or Reducer(group)
-    device = _agree_protocol(vi, red)
+    device = _device_capable(vi, red)
     calls0, reads0 = red.calls, red.host_reads
     if device:
         if red.stream is not None:
@@ -252,22 +253,13 @@ def solve_sharded(vi, group=None, reducer=None) -> dict:
         else:
             k, dv = _device_protocol(vi, red)
     else:
-        vi.reset()
-        k_loc, e_loc = _local(vi)
-        K, E = red.max2(k_loc, e_loc)
-        k = int(K)
-        dv = vi.run_to(k)
-        if E == 0.0:
-            if dv != 0.0:
-                raise RuntimeError(f"fixed-point invariant violated: dV at sweep {k} is {dv!r}")
-        else:
-            dv = red.max(dv)
+        k, dv = _host_protocol(vi, red)
     while not (dv < vi.tol) and k < vi.max_sweeps:
         dv = red.max(vi.sweep())
         k += 1
     vi.finish(k, dv)
     return {"sweeps": k, "dv": dv, "converged": dv < vi.tol, "allreduces": red.calls - calls0,
-            "host_reads": red.host_reads - reads0}
+            "host_reads": red.host_reads - reads0, "protocol": "device" if device else "host"}
 
 
 def gather_results(V: np.ndarray, group=None):

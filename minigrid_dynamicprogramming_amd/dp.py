@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import atexit
 import ctypes
+import hashlib
 import weakref
 from dataclasses import dataclass
 
@@ -211,6 +212,7 @@ class ValueIteration:
             check_doorkey_encoding(enc)
         cells = np.ascontiguousarray(cells, np.uint8)
         _lib.check(self.L.mgdp_vi_load_cells(self.h, _lib.ptr(cells)), "mgdp_vi_load_cells")
+        self._cells_digest = hashlib.sha256(cells.tobytes()).hexdigest()  # checkpoint() / resume()
         self.sweeps = 0
         self.converged = False
         self.dv = float("nan")
@@ -225,6 +227,7 @@ class ValueIteration:
         rc = self._load_dev_fn(self.h, ctypes.c_void_p(int(cells_ptr)))
         if rc:
             _lib.check(rc, "mgdp_vi_load_cells_device")
+        self._cells_digest = None  # not read back: a checkpoint of these grids cannot be verified
         self.sweeps = 0
         self.converged = False
         self.dv = float("nan")
@@ -341,6 +344,13 @@ class ValueIteration:
         _lib.check(self.L.mgdp_vi_get_policy_t(self.h, _lib.ptr(out)), "mgdp_vi_get_policy_t")
         return out
 
+    def grid_sweeps(self) -> np.ndarray:
+        """(B,) int32: the sweeps each grid executed (mgdp_vi_get_grid_sweeps) -- its own stopping
+        sweep if it ended at an exact fixed point (complete for the global K), else K."""
+        k = np.empty(self.B, np.int32)
+        _lib.check(self.L.mgdp_vi_get_grid_sweeps(self.h, _lib.ptr(k)), "mgdp_vi_get_grid_sweeps")
+        return k
+
     def values(self) -> np.ndarray:
         V = np.empty((self.B, self.S), self.np_dtype)
         _lib.check(self.L.mgdp_vi_get_values(self.h, _lib.ptr(V)), "mgdp_vi_get_values")
@@ -352,20 +362,49 @@ class ValueIteration:
         return pi
 
     # -- checkpoint / resume: Jacobi is memoryless given V_k
+    def _ckpt_meta(self) -> dict:
+        """What a checkpoint is only valid for: the grids (sha256 of the cells, None after
+        load_device) and every parameter the Jacobi trajectory depends on."""
+        d = self.desc
+        return {"model": self.model, "dtype": self.dtype, "B": self.B, "W": self.W, "H": self.H,
+                "gamma": float(d.gamma), "tol": float(d.tol), "slip_p": float(d.slip_p),
+                "lava_mode": int(d.lava_mode), "death_cost": float(d.death_cost), "horizon": int(d.horizon),
+                "cells_sha256": self._cells_digest}
+
     def checkpoint(self) -> dict:
-        """The state of the last solve: {"V" (B, S), "pi" (B, S), "sweeps", "dv", "converged"}.  A
-        solve stopped by max_sweeps before converging continues from it with resume() -- on this
-        handle or on a new one of the same grids and parameters -- bit-identical to the
+        """The state of the last solve: {"V" (B, S), "pi" (B, S), "sweeps", "dv", "converged",
+        "meta"}.  A solve stopped by max_sweeps before converging continues from it with resume()
+        on a handle of the same grids and parameters whose max_sweeps is larger than the
+        checkpoint's sweep count (so not on the capped handle itself), bit-identical to the
         uninterrupted solve."""
         return {"V": self.values(), "pi": self.policy(), "sweeps": int(self.sweeps), "dv": float(self.dv),
-                "converged": bool(self.converged)}
+                "converged": bool(self.converged), "meta": self._ckpt_meta()}
 
-    def resume(self, ckpt: dict) -> int:
+    def resume(self, ckpt: dict, verify_cells: bool = True) -> int:
         """Continue from checkpoint() output (mgdp_vi_resume); returns the sweeps of the whole solve.
-        A converged checkpoint is final and is refused."""
-        V = np.ascontiguousarray(ckpt["V"], dtype=self.np_dtype)
+        Refused (ValueError): a converged checkpoint (final), V of another shape or dtype, a
+        checkpoint of other grids or parameters (its "meta"), and with verify_cells a handle or
+        checkpoint whose cells are unknown (loaded with load_device)."""
+        meta = ckpt.get("meta")
+        if meta is None:
+            raise ValueError("checkpoint has no meta (grids and parameters); refusing to resume blind")
+        mine = self._ckpt_meta()
+        for key, val in mine.items():
+            if key == "cells_sha256":
+                continue
+            if meta.get(key) != val:
+                raise ValueError(f"checkpoint {key}={meta.get(key)!r} does not match the handle's {val!r}")
+        if verify_cells:
+            if mine["cells_sha256"] is None or meta.get("cells_sha256") is None:
+                raise ValueError("cells digest unknown (load_device); pass verify_cells=False to resume anyway")
+            if meta["cells_sha256"] != mine["cells_sha256"]:
+                raise ValueError("checkpoint was taken on other grids (cells sha256 differs)")
+        V = np.asarray(ckpt["V"])
+        if V.dtype != self.np_dtype:
+            raise ValueError(f"checkpoint V is {V.dtype}, the handle computes in {np.dtype(self.np_dtype)}")
         if V.shape != (self.B, self.S):
             raise ValueError(f"checkpoint V of shape {V.shape} does not match the handle's {(self.B, self.S)}")
+        V = np.ascontiguousarray(V)
         k, dv, conv = ctypes.c_int32(0), ctypes.c_double(0), ctypes.c_int32(0)
         _lib.check(self.L.mgdp_vi_resume(self.h, _lib.ptr(V), int(ckpt["sweeps"]), float(ckpt["dv"]), ctypes.byref(k),
                                          ctypes.byref(dv), ctypes.byref(conv)), "mgdp_vi_resume")
@@ -374,15 +413,19 @@ class ValueIteration:
 
     @staticmethod
     def save_checkpoint(path, ckpt: dict) -> None:
-        """Write a checkpoint as .npz (plain arrays: np.load needs no pickle)."""
+        """Write a checkpoint as .npz (plain arrays and a JSON string: np.load needs no pickle)."""
+        import json
+
         np.savez(path, V=ckpt["V"], pi=ckpt["pi"], sweeps=np.int64(ckpt["sweeps"]), dv=np.float64(ckpt["dv"]),
-                 converged=np.bool_(ckpt["converged"]))
+                 converged=np.bool_(ckpt["converged"]), meta=np.str_(json.dumps(ckpt.get("meta"))))
 
     @staticmethod
     def load_checkpoint(path) -> dict:
+        import json
+
         z = np.load(path)  # allow_pickle=False
         return {"V": z["V"], "pi": z["pi"], "sweeps": int(z["sweeps"]), "dv": float(z["dv"]),
-                "converged": bool(z["converged"])}
+                "converged": bool(z["converged"]), "meta": json.loads(str(z["meta"])) if "meta" in z else None}
 
     def dv_trace(self) -> np.ndarray:
         t = np.zeros(self.sweeps, np.float64)

@@ -102,7 +102,7 @@ def _worker(rank, world, port, cells, slip, out, device_proto=False, solves=1):
     V = getattr(shard, "V", None)
     pi = getattr(shard, "pi", None)
     out[rank] = (res["sweeps"], res["allreduces"], V, pi, lo, hi, res["host_reads"], red.calls,
-                 getattr(shard, "_mgdp_protocol", (None, None))[1])
+                 res["protocol"] == "device")
     dist.barrier()
     dist.destroy_process_group()
 
@@ -153,26 +153,27 @@ def test_device_protocol_uneven_shards_one_host_read(world, n):
     assert len(out) == world
     for rank, (k, nred, V, pi, lo, hi, reads, total_calls, proto) in out.items():
         assert k == ref["sweeps"], (rank, k)
-        assert proto is True
+        assert proto is (hi > lo)  # an empty rank drives the same collectives from the host
         assert nred == 1 and reads == 1  # deterministic grids: one all-reduce, one host wait
-        assert total_calls == 2  # two solves on one reducer (the one-time agreement not counted)
+        assert total_calls == 2  # two solves on one reducer, no agreement collective
         if hi > lo:
             np.testing.assert_array_equal(V, ref["V"][lo:hi])
             np.testing.assert_array_equal(pi, ref["pi"][lo:hi])
 
 
 @pytest.mark.parametrize("world,n,slip", [(4, 3, None), (8, 5, 0.9), (4, 9, None)])
-def test_protocol_agreement_with_host_only_peers(world, n, slip):
+def test_mixed_protocol_peers(world, n, slip):
     """More ranks than grids (EmptyShards) next to shards that can only run the host protocol, and
-    device-capable shards next to host-only ones ("mixed"): every rank must take the SAME protocol
-    (one MIN all-reduce of a capability flag), else the ranks would issue different collectives."""
+    device-capable shards next to host-only ones ("mixed"): each rank takes its own path, and both
+    paths issue the same collectives on the same int64 words, so the group never mismatches."""
     g = load("grids_fourrooms.npz")
     cells = np.stack([cells_from_enc(e) for e in g["enc"][:n]])
     ref = oracle.value_iteration(0, cells, slip_p=slip)
-    out = run_world(cells, world, slip=slip, device_proto="mixed")
-    for rank, (k, nred, V, pi, lo, hi, reads, _, proto) in out.items():
+    out = run_world(cells, world, slip=slip, device_proto="mixed", solves=2)
+    for rank, (k, nred, V, pi, lo, hi, reads, total_calls, proto) in out.items():
         assert k == ref["sweeps"], (rank, k)
-        assert proto is False, rank
+        assert proto is (hi > lo and rank % 2 == 0), rank
+        assert nred == (1 if slip is None else 2) and total_calls == 2 * nred
         if hi > lo:
             np.testing.assert_array_equal(V, ref["V"][lo:hi])
             np.testing.assert_array_equal(pi, ref["pi"][lo:hi])
@@ -188,7 +189,7 @@ def test_device_protocol_slip_second_allreduce(world, n):
     out = run_world(cells, world, slip=0.9, device_proto=True)
     for rank, (k, nred, V, pi, lo, hi, reads, _, proto) in out.items():
         assert k == ref["sweeps"], (rank, k)
-        assert proto is True and nred >= 2 and reads >= 2
+        assert proto is (hi > lo) and nred >= 2 and reads >= 2
         if hi > lo:
             np.testing.assert_array_equal(V, ref["V"][lo:hi])
             np.testing.assert_array_equal(pi, ref["pi"][lo:hi])
@@ -214,23 +215,26 @@ def test_bits_round_trip_and_order():
 
 
 class _FakeReducer:
+    """One rank's reducer: MAX over one rank is the identity (the proto words stay as written)."""
+
     def __init__(self):
         import torch
 
+        self.torch = torch
         self.calls = 0
         self.host_reads = 0
+        self.wall_s = 0.0
+        self.stream = None
         self.device = torch.device("cpu")
+        self.proto = torch.zeros(8, dtype=torch.int64)
 
     def max(self, x):
         self.calls += 1
+        self.host_reads += 1
         return x
 
-    def max2(self, a, b):
+    def max_(self, t):
         self.calls += 1
-        return a, b
-
-    def min_flag(self, flag):
-        return flag
 
 
 class _NonMonotoneShard:
@@ -259,29 +263,47 @@ def test_fallback_loop_finds_global_stopping_sweep():
     s = _NonMonotoneShard()
     res = solve_sharded(s, reducer=_FakeReducer())
     assert res["sweeps"] == 5 and res["converged"] and s.final[0] == 5
+    # host path: {K, E} (E unknown: no local_result), dV(K), then 2 fallback sweeps
+    assert res["protocol"] == "host" and res["allreduces"] == 4 and res["host_reads"] == 4
 
 
-class _FakeDeviceReducer(_FakeReducer):
-    """One rank's reducer on the device path: MAX over one rank is the identity."""
+def _worker_fresh_empty(rank, world, port, cells, out, solves):
+    """Rank 0 passes a NEW EmptyShard to every solve; rank 1 reuses one device-capable shard."""
+    import torch.distributed as dist
 
-    def __init__(self):
-        import torch
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    red = Reducer()
+    shard = DevOracleShard(cells) if rank == 1 else None
+    res = []
+    for _ in range(solves):
+        r = solve_sharded(shard if rank == 1 else EmptyShard(), reducer=red)
+        res.append((r["sweeps"], r["allreduces"], r["protocol"]))
+    out[rank] = (res, red.calls, getattr(shard, "V", None))
+    dist.barrier()
+    dist.destroy_process_group()
 
-        super().__init__()
-        self.torch = torch
-        self.stream = None
-        self.proto = torch.zeros(8, dtype=torch.int64)
-        self.wall_s = 0.0
 
-    def max(self, x):
-        self.host_reads += 1
-        return super().max(x)
+def test_fresh_empty_shard_every_solve_next_to_reused_shard():
+    """the protocol must not depend on per-rank object state -- a rank building a new
+    shard per solve and a rank reusing its shard issue the same collectives on every solve."""
+    g = load("grids_fourrooms.npz")
+    cells = np.stack([cells_from_enc(e) for e in g["enc"][:4]])
+    ref = oracle.value_iteration(0, cells)
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_fresh_empty, args=(2, port, cells, out, 3), nprocs=2, join=True)
+    res0, calls0, _ = out[0]
+    res1, calls1, V1 = out[1]
+    assert [r[2] for r in res0] == ["host"] * 3 and [r[2] for r in res1] == ["device"] * 3
+    assert [r[0] for r in res0] == [r[0] for r in res1] == [ref["sweeps"]] * 3
+    assert calls0 == calls1 == 3
+    np.testing.assert_array_equal(V1, ref["V"])
 
-    def max_(self, t):
-        self.calls += 1
 
-    def min_flag(self, flag):
-        return flag
+_FakeDeviceReducer = _FakeReducer  # the device path uses the same reducer surface
 
 
 class _NonMonotoneDevShard(_NonMonotoneShard):

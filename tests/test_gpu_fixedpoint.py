@@ -1,0 +1,175 @@
+"""Fixed-point completion (csrc/vi_kernels.h fused_grid, mgdp_vi_run_to): a grid whose own rule
+stopped at an EXACT fixed point (|dV| = 0, V_k == V_{k-1} bit for bit) is at every later sweep
+index already -- a Jacobi sweep is a function of V alone, and pi_{k'} = argmax on V_{k'-1} = pi_k --
+so the global rule's K needs no further sweeps of it: deterministic batches solve in ONE launch
+(own rule + reduction), run_to moves only the sweep count of such grids, and nothing waits on
+another grid's residency.  Every case against the oracle's global Jacobi loop (sweeps, V and pi
+bit-exact), including run_to past K, capped batches mixing fixed and unfinished grids, and batches
+at / around the GPU's resident capacity next to a resident lone-grid server."""
+import os
+import time
+
+import numpy as np
+import pytest
+
+import minigrid_dynamicprogramming_amd as mg
+from minigrid_dynamicprogramming_amd import gen
+from oracle import oracle
+from tests.test_gpu_wave2 import random_grids
+
+pytestmark = pytest.mark.gpu
+
+
+def _handle(cells, dtype, env=None, **kw):
+    old = {k: os.environ.get(k) for k in (env or {})}
+    os.environ.update(env or {})
+    try:
+        return mg.ValueIteration(cells, dtype=dtype, **kw)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _solve_timed(cells, dtype, env=None, solves=2):
+    vi = _handle(cells, dtype, env)
+    try:
+        vi.enable_timing(True)
+        for _ in range(solves):
+            k = vi.solve()
+        _, launches = vi.kernel_time()
+        return k, vi.values(), vi.policy(), launches / solves, vi.grid_sweeps()
+    finally:
+        vi.close()
+
+
+@pytest.mark.parametrize("env", [{}, {"MGDP_GK": "0"}])
+@pytest.mark.parametrize("B,W,H,dtype", [(37, 16, 16, "f32"), (600, 11, 11, "f32"), (300, 19, 19, "f64"),
+                                         (2000, 9, 7, "f32"), (9000, 9, 7, "f32")])
+def test_one_launch_per_deterministic_solve(B, W, H, dtype, env):
+    cells = random_grids(B, W, H, seed=B + W, goals=2)
+    o = oracle.value_iteration(0, cells, dtype=dtype, nthreads=8)
+    k, V, pi, per_solve, ks = _solve_timed(cells, dtype, env)
+    assert k == o["sweeps"]
+    np.testing.assert_array_equal(pi, o["pi"])
+    np.testing.assert_array_equal(V, o["V"])
+    # every grid ends its own rule at an exact fixed point: the own-rule launch is the whole solve,
+    # resident (in-launch reduction) or not (reduce kernel), and each grid did its own sweeps only
+    assert per_solve == 1, per_solve
+    assert ks.max() == k and ks.min() >= 1
+
+
+def test_grid_sweeps_are_each_grids_own_stopping_sweep():
+    cells = random_grids(40, 13, 13, seed=4, goals=1)
+    vi = mg.ValueIteration(cells, dtype="f64")
+    vi.solve()
+    own = np.array([oracle.value_iteration(0, c, dtype="f64")["sweeps"] for c in cells])
+    np.testing.assert_array_equal(vi.grid_sweeps(), own)
+    vi.close()
+
+
+@pytest.mark.parametrize("extra", [1, 5, 40])
+def test_run_to_past_k_reproduces_the_global_loop(extra):
+    """run_local, then run_to(K + extra) through the device-K entry point (always a launch): the
+    fixed-point grids only move their sweep count; V / pi equal the oracle's K + extra sweeps."""
+    import torch
+
+    cells = gen.generate("MiniGrid-LavaCrossingS11N5-v0", 0, 512, enc=False, cells=True, agent=False)["cells"]
+    vi = mg.ValueIteration(cells, dtype="f32")
+    p = torch.zeros(8, dtype=torch.int64, device="cuda")
+    s = torch.cuda.Stream()
+    vi.bind_stream(s.cuda_stream)
+    with torch.cuda.stream(s):
+        vi.reset()
+        vi.run_local_dev(p[0:4])
+        K = int(p[0].item())
+        p[0] = K + extra
+        vi.run_to_dev(p[0:1], p[4:8])
+        h = p.tolist()
+    assert h[4] == h[6] == K + extra and h[5] == 0  # {kmax, dV bits, kmin}: every grid at K + extra, dV 0
+    vi.set_result(K + extra, 0.0)
+    vi.finish(K + extra, 0.0)
+    o = oracle.value_iteration(0, cells, dtype="f32", tol=-1.0, max_sweeps=K + extra)
+    np.testing.assert_array_equal(vi.values(), o["V"])
+    np.testing.assert_array_equal(vi.policy(), o["pi"])
+    assert (vi.grid_sweeps() == K + extra).all()
+    vi.close()
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_capped_batch_mixes_fixed_and_unfinished_grids(dtype):
+    """max_sweeps between the grids' own stopping sweeps: some grids stop at an exact fixed point,
+    the others at the cap (not converged) -- the solve's run_to then launches and the fixed grids
+    skip inside it.  Sweeps, V and pi equal the oracle's capped global loop."""
+    cells = np.concatenate([random_grids(24, 7, 7, seed=1), random_grids(24, 16, 16, seed=2, goals=1)])
+    own = np.array([oracle.value_iteration(0, c, dtype=dtype)["sweeps"] for c in cells])
+    cap = int(np.median(own))
+    assert (own < cap).any() and (own > cap).any()
+    r = mg.value_iteration(cells, dtype=dtype, max_sweeps=cap)
+    o = oracle.value_iteration(0, cells, dtype=dtype, max_sweeps=cap)
+    assert r.sweeps == o["sweeps"] == cap and not r.converged
+    np.testing.assert_array_equal(r.pi, o["pi"])
+    np.testing.assert_array_equal(r.V, o["V"])
+
+
+def test_slip_batch_is_exact():
+    # slip grids rarely reach an exact fixed point: the chained own-rule + run_to pair stays exact
+    cells = random_grids(64, 11, 11, seed=3)
+    r = mg.value_iteration(cells, dtype="f64", slip_p=0.9)
+    o = oracle.value_iteration(0, cells, dtype="f64", slip_p=0.9)
+    assert r.sweeps == o["sweeps"]
+    np.testing.assert_array_equal(r.V, o["V"])
+    np.testing.assert_array_equal(r.pi, o["pi"])
+
+
+def test_fourrooms4096_one_launch_per_solve():
+    cells = gen.generate("MiniGrid-FourRooms-v0", 0, 4096, enc=False, cells=True, agent=False)["cells"]
+    o = oracle.value_iteration(0, cells, dtype="f32", nthreads=16)
+    k, V, pi, per_solve, _ = _solve_timed(cells, "f32", solves=3)
+    assert k == o["sweeps"] and per_solve == 1
+    assert np.array_equal(V, o["V"]) and np.array_equal(pi, o["pi"])
+
+
+def _time_solves(vi, n=5):
+    vi.solve()
+    t = time.perf_counter()
+    for _ in range(n):
+        vi.solve()
+    return (time.perf_counter() - t) / n
+
+
+@pytest.mark.parametrize("delta", [-1, 0, 1])
+def test_capacity_batches_next_to_a_resident_server(delta):
+    """a batch of exactly the one-wave kernel's resident capacity (P = 1 grids: 32
+    workgroups per CU), and one less / one more, solved while a lone-grid server stays resident on
+    another handle (it occupies a CU's slot): bit-exact, and no grid waits on another, so the time
+    stays within 1.3x of the batch with the in-launch reduction off (MGDP_GK=0)."""
+    import torch
+
+    cap = 32 * torch.cuda.get_device_properties(0).multi_processor_count
+    cells = random_grids(cap + delta, 9, 7, seed=7, goals=2)
+    o = oracle.value_iteration(0, cells, dtype="f32", nthreads=16)
+    enc, _ = mg.make("MiniGrid-Empty-16x16-v0").generate(seed=0)
+    # the server stays resident on its own stream (idle limit raised to 0.5 s) while the batches run
+    lone = _handle(np.ascontiguousarray(enc[..., 0].T)[None], "f32", {"MGDP_SERVE_IDLE_US": "500000"})
+    assert lone.persistent
+    lone.solve()
+    on = _handle(cells, "f32")
+    off = _handle(cells, "f32", {"MGDP_GK": "0"})
+    try:
+        t_on, t_off = [], []
+        for _ in range(3):  # interleaved; a request between them keeps the server busy-polling
+            assert lone.solve() == 29
+            t_on.append(_time_solves(on))
+            assert lone.solve() == 29
+            t_off.append(_time_solves(off))
+        assert on.sweeps == o["sweeps"]
+        np.testing.assert_array_equal(on.values(), o["V"])
+        np.testing.assert_array_equal(on.policy(), o["pi"])
+        assert min(t_on) <= 1.3 * min(t_off), (t_on, t_off)
+    finally:
+        on.close()
+        off.close()
+        lone.close()

@@ -82,3 +82,29 @@ def test_resume_sweep_method_refused():
     with pytest.raises((ValueError, MgdpError)):
         vi.resume(vi.checkpoint())
     vi.close()
+
+
+def test_resume_refuses_other_grids_params_and_dtype(tmp_path):
+    """a checkpoint carries the grids' digest, dtype and parameters; resume refuses a
+    mismatch instead of casting or continuing on the wrong grids."""
+    cells = fourrooms(4)
+    part = mg.ValueIteration(cells, dtype="f32", max_sweeps=5)
+    part.solve()
+    path = tmp_path / "c.npz"
+    mg.ValueIteration.save_checkpoint(path, part.checkpoint())
+    part.close()
+    ck = mg.ValueIteration.load_checkpoint(path)
+    assert ck["meta"]["dtype"] == "f32" and ck["meta"]["cells_sha256"]
+    for kw, grids in [(dict(dtype="f64"), cells), (dict(dtype="f32", gamma=0.9), cells),
+                      (dict(dtype="f32", tol=1e-5), cells), (dict(dtype="f32"), fourrooms(5)[1:])]:
+        vi = mg.ValueIteration(grids, **kw)
+        with pytest.raises(ValueError):
+            vi.resume(ck)
+        vi.close()
+    blind = dict(ck)
+    blind.pop("meta")
+    vi = mg.ValueIteration(cells, dtype="f32")
+    with pytest.raises(ValueError):
+        vi.resume(blind)
+    assert vi.resume(ck) == vi.sweeps and vi.converged  # the matching handle resumes
+    vi.close()
