@@ -631,7 +631,7 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded):
     else:
         elapsed_max, upd_total = elapsed, upd_rank
     lat = None
-    if vi.persistent or distinct:
+    if info["persistent"] or distinct:
         pr = np.diff(pstamps) * 1e6
         lat = {"first_solve_us": round(warm_us[0], 2) if warm_us else None,
                "warmup_solves_us": [round(x, 2) for x in warm_us],
