@@ -1,0 +1,121 @@
+"""bench.measure() end to end on the CPU: the ValueIteration handle replaced by a fake backed by the
+oracle (a closed handle refuses every call, like the real one), so the warmup / priming / timed
+region / result bookkeeping runs without a GPU -- the lone-grid priming rule and latency record, the
+batched executed-sweeps record, no handle use after close."""
+import argparse
+import importlib.util
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class FakeVI:
+    """The bits of dp.ValueIteration that bench.measure() uses, solved by the oracle."""
+
+    def __init__(self, cells, gamma=0.99, tol=1e-6, dtype="f32", method="fused", mapping="cell", device=0):
+        self._cells = np.ascontiguousarray(cells)
+        self._open = True
+        self._dtype = dtype
+        self._tol = tol
+        self._timing = False
+        self._solves = 0
+        B, H, W = self._cells.shape
+        self._dims = dict(B=B, H=H, W=W, S=W * H * 4, model="xyd", updates_per_sweep=B * W * H * 4 * 7,
+                          kernel_name="vi_serve_kernel" if B == 1 else "vi_fused_kernel", persistent=B == 1)
+        self._own = None
+
+    def __getattr__(self, name):
+        d = self.__dict__
+        if name in d.get("_dims", {}):
+            if not d["_open"]:
+                raise ValueError("null argument")  # what the C ABI says for a destroyed handle
+            return d["_dims"][name]
+        raise AttributeError(name)
+
+    def _check(self):
+        if not self._open:
+            raise ValueError("null argument")
+
+    def enable_timing(self, on=True):
+        self._check()
+        self._timing = on
+        self._solves = 0
+
+    def solve(self, last=False):
+        self._check()
+        r = oracle.value_iteration(0, self._cells, tol=self._tol, dtype=self._dtype)
+        self._solves += 1
+        if self._own is None:
+            self._own = np.array([oracle.value_iteration(0, c, tol=self._tol, dtype=self._dtype)["sweeps"]
+                                  for c in self._cells], np.int32)
+        return r["sweeps"]
+
+    def synchronize(self):
+        self._check()
+
+    def kernel_time(self):
+        self._check()
+        return 0.01 * self._solves, (1 if self.persistent else self._solves)
+
+    def serve_clock(self):
+        self._check()
+        return {"sclk_mhz": 2400.0, "server_us": 10.0 * self._solves, "launches": 1}
+
+    def grid_sweeps(self):
+        self._check()
+        return self._own
+
+    def close(self):
+        self._open = False
+
+
+@pytest.fixture
+def bench(monkeypatch):
+    import torch
+
+    import minigrid_dynamicprogramming_amd as mg
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    monkeypatch.setattr(mg, "ValueIteration", FakeVI)
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    monkeypatch.setattr(b, "PRIME_MIN_S", 0.01)
+    monkeypatch.setattr(b, "PRIME_WIN", 8)
+    return b
+
+
+def _args(workload, steps=3, warmup=2):
+    return argparse.Namespace(workload=workload, steps=steps, warmup=warmup, gamma=0.99, tol=1e-6,
+                              method="fused", mapping="cell")
+
+
+def test_measure_lone_grid_priming_and_latency(bench):
+    import minigrid_dynamicprogramming_amd as mg
+
+    enc, _ = mg.make("MiniGrid-Empty-16x16-v0").generate(seed=0)
+    cells = np.ascontiguousarray(enc[..., 0].T)[None]
+    m = bench.measure(_args("empty16"), "f32", cells, 0, None, None, None, False)
+    assert m["sweeps"] == [29, 29, 29] and m["upd_total"] == 29 * 3 * 1024 * 7
+    lat = m["latency"]
+    assert lat["priming_solves"] >= 2 * bench.PRIME_WIN and lat["priming_solves"] % bench.PRIME_WIN == 0
+    assert len(lat["warmup_solves_us"]) == 2 and lat["first_solve_us"] > 0
+    assert lat["device_clock"]["sclk_mhz"] == 2400.0 and "windows of 8" in lat["steady_rule"]
+    assert m["executed"] is None and m["info"]["persistent"] is True
+
+
+def test_measure_batch_executed_sweeps(bench):
+    from minigrid_dynamicprogramming_amd import make
+
+    env = make("MiniGrid-FourRooms-v0")
+    cells = np.stack([np.ascontiguousarray(env.generate(seed=s)[0][..., 0].T) for s in range(6)])
+    m = bench.measure(_args("fourrooms4096"), "f32", cells, 0, None, None, None, False)
+    K = m["sweeps"][-1]
+    ex = m["executed"]
+    assert ex["global_sweeps"] == K and 0 < ex["frac_of_global_rule"] <= 1.0
+    assert m["latency"] is None and m["primed"] == 0
