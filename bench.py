@@ -703,7 +703,7 @@ def numpy_baseline(cells, model, gamma, tol, dtype, budget_s):
     from oracle.numpy_vi import NumpyVI
 
     # 32 grids per thread (a threaded batch solve needs work for every thread), 32 for one thread
-    sample = cells[: min(len(cells), 32 * max(1, nthreads))]
+    sample = cells[: min(len(cells), 32)]
     n = NumpyVI(0 if model == "xyd" else 1, sample, gamma, tol, dtype)
     solves, upd, k = 0, 0, 0
     t0 = time.perf_counter()

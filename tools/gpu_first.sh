@@ -19,6 +19,6 @@ grep stamps $OUT/bench_$i.err | tail -1
 done
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/rocprof_default -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --no-hbm > $OUT/rocprof_bench.json 2> $OUT/rocprof.err || { echo "rocprof failed"; tail $OUT/rocprof.err; exit 1; }
 python -c "import json; d=json.load(open('$OUT/rocprof_bench.json')); r=d['roofline']; print('rocprof run', '%.4g'%d['value'], '%.3f us'%(d['ms_per_step']*1e3), 'launch us', r['avg_launch_us'], 'solves', r['solves_per_launch'])"
-timeout -k 10 400 python -u -m pytest tests/test_gpu_fixedpoint.py tests/test_gpu_wave2.py tests/test_gpu_fullsize.py tests/test_gpu_serve_ew.py tests/test_gpu_serve_grids.py tests/test_gpu_vi.py tests/test_gpu_resume.py tests/test_gpu_distributed.py tests/test_gpu_options.py tests/test_gpu_dk_half.py -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
 echo "all ok"
