@@ -556,14 +556,22 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded):
         reducer.reset_counters()
     barrier()
     torch.cuda.synchronize()
-    # Priming to a steady state (persistent lone-grid server): solves for at least PRIME_MIN_S, then
-    # windows of PRIME_WIN solves until a window's median latency is within PRIME_TOL of the
-    # previous window's (at most PRIME_MAX_S in all).  The first solves after the relaunch run
-    # 3-4 us slower, and a device or host core that was idle ramps its clock over milliseconds
-    # (the driver's fresh box: 11.3 us per solve after 16 priming solves; warm boxes 8.2-8.8 us).
+    # Priming to a steady state (persistent lone-grid server), in two phases.
+    # (1) warm: solves for at least PRIME_MIN_S, then windows of PRIME_WIN solves until a window's
+    #     median latency is within PRIME_TOL of the previous window's (at most PRIME_MAX_S in all):
+    #     a device or host core that was idle ramps its clock over milliseconds (the driver's fresh
+    #     box, round 3: 11.3 us per solve after 16 priming solves; warm boxes 7.9-8.8 us).  That
+    #     server then leaves: a launch that lived ~0.2 s closes slowly and erratically (the stream's
+    #     completion 9-65 us after its exit word vs 6-8 us for a young one, tools/probe_edge.py,
+    #     profiles/r04_edge/), which would land in the region's closing edge.
+    # (2) relaunch: PRIME_RELAUNCH solves on a new server launch (the first solves after a relaunch
+    #     run 3-4 us slower), timed from here, the last one right before the region -- the first
+    #     timed solve must find the server busy-polling (the solve fast path wants the last request
+    #     < 50 us old; past that it takes the general path and may relaunch).
     primed = 0
     pstamps = [time.perf_counter()]
     prime_meds = []
+    warm_clock = None
     if vi.persistent:
         t_prime = pstamps[0]
         while time.perf_counter() - t_prime < PRIME_MAX_S:
@@ -577,12 +585,17 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded):
             prime_meds.append(float(np.median(w)))
             if len(prime_meds) >= 2 and abs(prime_meds[-1] - prime_meds[-2]) <= PRIME_TOL * prime_meds[-2]:
                 break
-        # the window bookkeeping above took tens of us: one more solve right before the region, so
-        # the first timed solve finds the server busy-polling (the solve fast path requires the last
-        # request to be < 50 us old; past that it takes the general path and may relaunch)
-        one_solve()
+        one_solve(last=True)
         primed += 1
+        vi.synchronize()
+        warm_clock = vi.serve_clock()
+        vi.enable_timing(True)  # the timed launch is the relaunch below
+        torch.cuda.synchronize()
         pstamps.append(time.perf_counter())
+        for _ in range(PRIME_RELAUNCH):
+            one_solve()
+            primed += 1
+            pstamps.append(time.perf_counter())
     stamps = [] if os.environ.get("MGDP_BENCH_STAMPS") else None  # diagnostics: where the region's time goes
     t0 = time.perf_counter()
     sweeps = []
@@ -649,10 +662,13 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded):
                "priming_last_window_median_us": prime_meds[-1] if prime_meds else None,
                "steady_rule": f"solves for >= {PRIME_MIN_S * 1e3:.0f} ms, then windows of {PRIME_WIN} solves "
                               f"until a window's median is within {PRIME_TOL:.0%} of the previous "
-                              f"(at most {PRIME_MAX_S * 1e3:.0f} ms)"}
+                              f"(at most {PRIME_MAX_S * 1e3:.0f} ms); that server leaves, then "
+                              f"{PRIME_RELAUNCH} solves on the relaunched (timed) server before the region"}
+        if warm_clock and warm_clock["launches"]:
+            lat["warm_phase_clock"] = warm_clock
         if clock and clock["launches"]:
-            lat["device_clock"] = {**clock, "source": "vi_serve_kernel s_memtime cycles / s_memrealtime over its "
-                                                      "launches (priming + timed solves)"}
+            lat["device_clock"] = {**clock, "source": "vi_serve_kernel s_memtime cycles / s_memrealtime over the "
+                                                      "timed launch (relaunch priming + timed solves)"}
     executed = None
     if gsw is not None and sweeps[-1] > 0:
         executed = {"mean_grid_sweeps": round(float(gsw.mean()), 3), "global_sweeps": int(sweeps[-1]),
@@ -932,7 +948,7 @@ def gen_cpu_baseline(env, budget_s):
 
 BLOCK_CPU_S = 2.0  # seconds of oracle sampling per BASELINE-config block (1 thread, then all cores)
 # steady-state priming of a resident lone-grid server (measure(): the stated criterion)
-PRIME_MIN_S, PRIME_WIN, PRIME_TOL, PRIME_MAX_S = 0.2, 512, 0.02, 1.0
+PRIME_MIN_S, PRIME_WIN, PRIME_TOL, PRIME_MAX_S, PRIME_RELAUNCH = 0.2, 512, 0.02, 1.0, 16
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9  # MI355X_MICROARCH.md: 4 SIMD-32 per CU, one wave64 VALU op per 2 cycles
 
 

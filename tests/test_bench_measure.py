@@ -103,8 +103,10 @@ def test_measure_lone_grid_priming_and_latency(bench):
     m = bench.measure(_args("empty16"), "f32", cells, 0, None, None, None, False)
     assert m["sweeps"] == [29, 29, 29] and m["upd_total"] == 29 * 3 * 1024 * 7
     lat = m["latency"]
-    # whole windows, then the one solve right before the region
-    assert lat["priming_solves"] > 2 * bench.PRIME_WIN and (lat["priming_solves"] - 1) % bench.PRIME_WIN == 0
+    # whole windows, the warm server's last solve, then the relaunch priming
+    n = lat["priming_solves"] - 1 - bench.PRIME_RELAUNCH
+    assert n >= 2 * bench.PRIME_WIN and n % bench.PRIME_WIN == 0
+    assert lat["warm_phase_clock"]["sclk_mhz"] == 2400.0
     assert len(lat["warmup_solves_us"]) == 2 and lat["first_solve_us"] > 0
     assert lat["device_clock"]["sclk_mhz"] == 2400.0 and "windows of 8" in lat["steady_rule"]
     assert m["executed"] is None and m["info"]["persistent"] is True
