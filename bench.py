@@ -260,7 +260,7 @@ def workload_roofline(args, dtype, m, workload, grids):
     avg_launch_s = (m["kern_ms"] / 1000.0) / max(launches, 1)
     # solves inside the timed launches: the K timed solves plus the priming solves a resident
     # server's launch also spans
-    solves_in_launches = args.steps + m["primed"]
+    solves_in_launches = args.steps + m["timed_primed"]  # the timed launches: relaunch priming + region
     upd_per_solve = float(vi_info["updates_per_sweep"]) * float(np.mean(m["sweeps"]))
     alg_bytes_launch = upd_per_solve * solves_in_launches * bpu / max(launches, 1)
     achieved = alg_bytes_launch / avg_launch_s / 1e9 if launches else 0.0
@@ -678,7 +678,8 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded):
                             "K - k_e sweeps are not executed; value counts B*S*A*K as the metric defines"}
     return {"elapsed_max": elapsed_max, "upd_total": upd_total, "sweeps": sweeps, "kern_ms": kern_ms,
             "executed": executed,
-            "launches": launches, "primed": primed, "info": info, "collectives": collectives, "latency": lat}
+            "launches": launches, "primed": primed, "timed_primed": PRIME_RELAUNCH if info["persistent"] else 0,
+            "info": info, "collectives": collectives, "latency": lat}
 
 
 def host_cores() -> int:
