@@ -103,6 +103,7 @@ struct mgdp_vi {
     int dkhalf = 0;               // batched DoorKey, states split by has_key over two threads (MGDP_DK_HALF; fused_dk_half)
     int pair2 = 1;                // batched plain XYD with cpt 2: adjacent-cell pairs (MGDP_PAIR2=0: fused_fast_xyd_soa_xn)
     int wave2 = 0;                // batched plain XYD on one wave per grid: cells per lane P (fused_wave2_xyd; 0 = off)
+    int wave2n = 0;               // ... on two waves per grid instead: blocks per wave PW (fused_wave2n_xyd; 0 = off)
     int sweep_block = 256;
     int sweep_m = 1;              // grids staged per workgroup iteration (measured: m>1 no faster)
     int sweep_pipe = 2;           // register-pipelined sweep kernel: grids fetched ahead (0 = staged kernel)
@@ -306,6 +307,16 @@ F pick_wave2(int P, F dflt) {
     }
     return dflt;
 }
+// The two-waves-per-grid instantiation for PW blocks per wave (2..4); `dflt` if out of range.
+template <template <typename, int, bool, int, int> class K, typename T, int MODEL, bool SLIP, int MAP, typename F>
+F pick_wave2n(int PW, F dflt) {
+    switch (PW) {
+    case 2: return K<T, MODEL, SLIP, MAP, kWpWave2n - 2>::fn;
+    case 3: return K<T, MODEL, SLIP, MAP, kWpWave2n - 3>::fn;
+    case 4: return K<T, MODEL, SLIP, MAP, kWpWave2n - 4>::fn;
+    default: return dflt;
+    }
+}
 template <typename T, int MODEL, bool SLIP, int MAP, int WP>
 struct ServeK { static constexpr auto fn = vi_serve_kernel<T, MODEL, SLIP, MAP, WP>; };
 // fused_dk_half variants by plane stride HWs = 64 * n (the host allows n <= 8)
@@ -364,7 +375,10 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
     }
     int smem = L.total();
     if constexpr (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL && !SLIP) {
-        if (vi->wave2) {
+        if (vi->wave2n) {
+            kern = pick_wave2n<FusedK, T, MODEL, SLIP, MAP>(vi->wave2n, kern);
+            smem = wave2n_smem_bytes(vi->HWp, vi->d.W, 2 * vi->wave2n, (int)sizeof(T));
+        } else if (vi->wave2) {
             kern = pick_wave2<FusedK, T, MODEL, SLIP, MAP>(vi->wave2, kern);
             smem = wave2_smem_bytes(vi->HWp, vi->d.W, vi->wave2, (int)sizeof(T));
         }
@@ -877,18 +891,39 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
             vi->HWs = (int)round_up(vi->HW, 64);
             vi->Ss = vi->S / vi->HW * vi->HWs;
         }
-        if (vi->wave2) {  // the in-launch reduction (GkCtx) when the batch is resident at once
+        if (vi->wave2) {
+            int cus = 0;
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d.device);
+            // Two waves per grid when one wave per grid leaves the SIMDs short of waves (B <= one
+            // wave per SIMD... four per SIMD: FourRooms x 4096) and a grid has >= 4 blocks of 64
+            // cells to split (MGDP_WAVE2N=0 / 1 forces it off / on where it applies).
+            int w2n = d.B <= 4 * 4 * cus && vi->wave2 >= 4 ? 1 : 0;
+            if (const char *ev = std::getenv("MGDP_WAVE2N")) w2n = std::atoi(ev) != 0 && vi->wave2 >= 3;
+            if (w2n) {
+                vi->wave2n = (vi->wave2 + 1) / 2;
+                vi->fused_block = 128;
+            }
+            // the in-launch reduction (GkCtx) when the batch is resident at once
             int gk_on = 1;
             if (const char *ev = std::getenv("MGDP_GK")) gk_on = std::atoi(ev);
-            const int smem2 = wave2_smem_bytes(vi->HWp, d.W, vi->wave2, vi->tsize);
-            const void *k2 = d.dtype == MGDP_F32
-                ? (const void *)pick_wave2<FusedK, float, MGDP_MODEL_XYD, false, MGDP_MAP_CELL>(
-                      vi->wave2, FusedK<float, MGDP_MODEL_XYD, false, MGDP_MAP_CELL, 0>::fn)
-                : (const void *)pick_wave2<FusedK, double, MGDP_MODEL_XYD, false, MGDP_MAP_CELL>(
-                      vi->wave2, FusedK<double, MGDP_MODEL_XYD, false, MGDP_MAP_CELL, 0>::fn);
-            int per_cu = 0, cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k2, 64, smem2) == hipSuccess &&
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d.device) == hipSuccess)
+            const bool f32 = d.dtype == MGDP_F32;
+            const void *k2 = nullptr;
+            int smem2 = 0;
+            if (vi->wave2n) {
+                smem2 = wave2n_smem_bytes(vi->HWp, d.W, 2 * vi->wave2n, vi->tsize);
+                k2 = f32 ? (const void *)pick_wave2n<FusedK, float, MGDP_MODEL_XYD, false, MGDP_MAP_CELL>(
+                               vi->wave2n, FusedK<float, MGDP_MODEL_XYD, false, MGDP_MAP_CELL, 0>::fn)
+                         : (const void *)pick_wave2n<FusedK, double, MGDP_MODEL_XYD, false, MGDP_MAP_CELL>(
+                               vi->wave2n, FusedK<double, MGDP_MODEL_XYD, false, MGDP_MAP_CELL, 0>::fn);
+            } else {
+                smem2 = wave2_smem_bytes(vi->HWp, d.W, vi->wave2, vi->tsize);
+                k2 = f32 ? (const void *)pick_wave2<FusedK, float, MGDP_MODEL_XYD, false, MGDP_MAP_CELL>(
+                               vi->wave2, FusedK<float, MGDP_MODEL_XYD, false, MGDP_MAP_CELL, 0>::fn)
+                         : (const void *)pick_wave2<FusedK, double, MGDP_MODEL_XYD, false, MGDP_MAP_CELL>(
+                               vi->wave2, FusedK<double, MGDP_MODEL_XYD, false, MGDP_MAP_CELL, 0>::fn);
+            }
+            int per_cu = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k2, vi->fused_block, smem2) == hipSuccess)
                 vi->gk_capacity = per_cu * cus;
             vi->gk = gk_on != 0 && d.B <= vi->gk_capacity;
         }

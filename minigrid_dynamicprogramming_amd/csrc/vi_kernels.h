@@ -18,6 +18,10 @@ __host__ __device__ constexpr bool wp_is_pair(int wp) { return wp <= kWpPair - 1
 // (fused_wave2_xyd, its own compact LDS layout; vi_fused_kernel only).
 constexpr int kWpWave2 = -400;
 __host__ __device__ constexpr bool wp_is_wave2(int wp) { return wp <= kWpWave2 - 1 && wp >= kWpWave2 - 8; }
+// Tags -702 .. -704: batched deterministic XYD, TWO waves per grid, PW = -tag - 700 blocks of 64
+// cells per wave (fused_wave2n_xyd; 128-thread workgroups, vi_fused_kernel only).
+constexpr int kWpWave2n = -700;
+__host__ __device__ constexpr bool wp_is_wave2n(int wp) { return wp <= kWpWave2n - 2 && wp >= kWpWave2n - 4; }
 // Minimum waves per SIMD the one-wave kernels are compiled for.  Left alone, the fp32 P <= 2
 // variants (LavaS11N5: 121 cells) take 57 VGPRs but 106 SGPRs, and the SGPRs cap them at 7 waves
 // per SIMD (28 workgroups / CU, 7168 grids resident): 8 makes the compiler fit 8 waves' SGPRs too
@@ -85,6 +89,29 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     const bool work = k_target < 0 ? (!(k > 0 && dvl < geo.tol) && k < geo.max_sweeps) : (k < k_target);
     if (!work) return false;
     const long long vb = (long long)e * geo.S;
+    if constexpr (wp_is_wave2n(WP)) {  // two waves per grid: cells, then two N/S tiles (wave2n_*)
+        static_assert(MODEL == MGDP_MODEL_XYD && !SLIP && MAP == MGDP_MAP_CELL && !SERVED, "wave2n: batched plain XYD");
+        constexpr int PW = kWpWave2n - WP;
+        uint8_t *cl2 = smem + 256;
+        copy16(cl2, cells + (long long)e * geo.HWp, geo.HWp);
+        __syncthreads();
+        T *tile = reinterpret_cast<T *>(smem + wave2_tile_off(geo.HWp));
+        auto done2 = [&](int kk, double dv) {
+            if (lone && threadIdx.x == 0)
+                publish(host_out, (unsigned long long)kk, (unsigned long long)__double_as_longlong(dv),
+                        (unsigned long long)kk, epoch);
+        };
+        if (k_target < 0)
+            fused_wave2n_xyd<T, true, PW>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2,
+                                          GkCtx{gk, epoch, e, geo.B, host_out});
+        else
+            fused_wave2n_xyd<T, false, PW>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
+        if (threadIdx.x == 0) {
+            kenv[e] = k;
+            dvenv[e] = dvl;
+        }
+        return true;
+    }
     if constexpr (wp_is_wave2(WP)) {  // its own LDS layout (wave2_*): cells, then the N/S tile
         static_assert(MODEL == MGDP_MODEL_XYD && !SLIP && MAP == MGDP_MAP_CELL && !SERVED, "wave2: batched plain XYD");
         constexpr int P = kWpWave2 - WP;
@@ -247,7 +274,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
 // WP > 0: the one-wave lone-grid variant (fused_wave_xyd), 64 threads, so its WP cells per lane
 // may use the whole register file.
 template <typename T, int MODEL, bool SLIP, int MAP, int WP = 0>
-__global__ void __launch_bounds__(WP > 0 || wp_is_wave2(WP) ? 64 : 1024, wave2_min_waves<T>(WP))
+__global__ void __launch_bounds__(WP > 0 || wp_is_wave2(WP) ? 64 : (wp_is_wave2n(WP) ? 128 : 1024), wave2_min_waves<T>(WP))
 vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
@@ -256,7 +283,7 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
                 unsigned long long *__restrict__ host_mirror, unsigned long long *__restrict__ gk) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
-    T *slots = reinterpret_cast<T *>(smem + (wp_is_wave2(WP) ? 0 : L.slots_off()));
+    T *slots = reinterpret_cast<T *>(smem + (wp_is_wave2(WP) || wp_is_wave2n(WP) ? 0 : L.slots_off()));
     // multi-GPU protocol (mgdp_vi_run_to_dev): the target sweep is the all-reduced K in device
     // memory, written by a collective ordered before this launch on the stream
     if (k_target_dev) {
@@ -274,9 +301,9 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
     const bool lone = in_kernel_reduce && gridDim.x == 1;
     const bool work = fused_grid<T, MODEL, SLIP, MAP, false, WP>(geo, cf, cells, V, pi, kenv, dvenv, host_out, k_target,
                                                                  fresh, lone, epoch, blockIdx.x, k, dvl, nullptr,
-                                                                 wp_is_wave2(WP) ? gk : nullptr);
+                                                                 wp_is_wave2(WP) || wp_is_wave2n(WP) ? gk : nullptr);
     // a launch-wide-rule launch (wave2 with gk) reduces and publishes through its own counter tree
-    const bool gk_pub = wp_is_wave2(WP) && gk != nullptr && k_target < 0 && !k_target_dev;
+    const bool gk_pub = (wp_is_wave2(WP) || wp_is_wave2n(WP)) && gk != nullptr && k_target < 0 && !k_target_dev;
     if (in_kernel_reduce && !gk_pub)
         fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16), epoch, work);
 }

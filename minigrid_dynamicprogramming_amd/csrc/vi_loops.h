@@ -1049,6 +1049,211 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
     }
 }
 
+// Batched deterministic XYD grids on TWO waves per grid (fused_wave2n_xyd): wave w owns blocks
+// w*PW .. w*PW + PW - 1 of the P = 2*PW 64-cell blocks, so a grid's sweep is two chains of PW
+// blocks instead of one of P -- for batches too small to fill the GPU with one wave per grid
+// (FourRooms x 4096: 4096 waves on 1024 SIMDs).  The waves meet at one barrier per sweep: V_k's
+// planes 1 / 3 alternate between two tiles (sweep k reads tile (k - k_start) & 1, writes the
+// other), the two east / west values that cross the wave boundary (plane 0 of wave 1's first
+// cell, plane 2 of wave 0's last cell) go through two LDS words per tile, and each wave's stop
+// ballot through a flag word per tile, read with the next sweep's fronts -- so both waves take
+// the same stop decision.  Arithmetic, rule and pi pass as fused_wave2_xyd: bit-identical results.
+// LDS: [slots 256 B][cells HWp][tile 0][tile 1][edges 4 T | dV 2 T | flags 4 u32] (wave2n_*).
+__host__ __device__ inline int wave2n_tile_elems(int W, int P) { return 2 * 64 * P + 2 * wave2_padw(W); }
+__host__ __device__ inline int wave2n_smem_bytes(int HWp, int W, int P, int tsize) {
+    return wave2_tile_off(HWp) + 2 * wave2n_tile_elems(W, P) * tsize + 64;
+}
+template <int B> struct WaveBuf { static constexpr int value = B; };
+
+template <typename T, bool LOCAL, int PW, typename Done>
+__device__ __forceinline__ void fused_wave2n_xyd(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *tile,
+                                                 const T *Vg, T *Vg_out, int8_t *pig, int &k, int k_target,
+                                                 double &dvl, const Done &done, const GkCtx gk = GkCtx{}) {
+    static_assert(PW >= 1 && PW <= 8, "goal bits: 4 per cell, 32 per lane");
+    constexpr int P = 2 * PW;
+    const int w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+    const int W = geo.W, padw = wave2_padw(W);
+    const int TS = wave2n_tile_elems(W, P);
+    T *const edge = tile + 2 * TS;  // [tile][0: plane 0 of cell 64 PW, 1: plane 2 of cell 64 PW - 1]
+    T *const dvx = edge + 4;        // [wave] |dV| of the last sweep
+    uint32_t *const flag = reinterpret_cast<uint32_t *>(reinterpret_cast<unsigned char *>(edge) + 48);  // [tile][wave]
+    T ge[PW];
+    uint32_t goal = 0;
+    T own[PW][4];
+    {
+        T *const N3 = tile + padw, *const S1 = tile + padw + 64 * P;
+#pragma unroll
+        for (int j = 0; j < PW; ++j) {
+            const int c = (w * PW + j) * 64 + lane;
+            const int cc = c < geo.HW ? c : 0;  // idle slots shadow cell 0 (a wall) and never write HBM
+            const bool valid = xyd_free(cl[cc]);
+            ge[j] = valid ? cf.g : (T)0;
+#pragma unroll
+            for (int d = 0; d < 4; ++d)
+                goal |= (uint32_t)(valid && cl[valid ? cc + geo.off[d] : cc] == T_GOAL) << (4 * j + d);
+            const V4<T> x = k == 0 ? V4<T>{{(T)0, (T)0, (T)0, (T)0}} : *reinterpret_cast<const V4<T> *>(Vg + cc * 4);
+#pragma unroll
+            for (int d = 0; d < 4; ++d) own[j][d] = x.v[d];
+            N3[c] = own[j][3];
+            S1[c] = own[j][1];
+        }
+        if (w == 1 && lane == 0) edge[0] = own[0][0];
+        if (w == 0 && lane == 63) edge[1] = own[PW - 1][2];
+        for (int i = (int)threadIdx.x; i < padw; i += 128) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                tile[t * TS + i] = (T)0;
+                tile[t * TS + padw + 128 * P + i] = (T)0;
+            }
+        }
+    }
+    uint32_t goal_blocks = 0;
+#pragma unroll
+    for (int j = 0; j < PW; ++j)
+        goal_blocks |= (__builtin_amdgcn_ballot_w64(((goal >> (4 * j)) & 15u) != 0u) != 0ull ? 1u : 0u) << j;
+    __syncthreads();
+    const int k_start = k;
+    T diff = (T)0;
+    // sweep k_start + i reads tile i & 1 and writes the other (b: compile-time in the unrolled pair)
+    auto sweep = [&](auto bc, const T (&in)[PW][4], T (&out)[PW][4]) -> bool {
+        constexpr int b = decltype(bc)::value;
+        const T *const N3r = tile + b * TS + padw, *const S1r = N3r + 64 * P;
+        T *const N3w = tile + (b ^ 1) * TS + padw, *const S1w = N3w + 64 * P;
+        T FS[PW], FN[PW];
+#pragma unroll
+        for (int j = 0; j < PW; ++j) {
+            const int c = (w * PW + j) * 64 + lane;
+            FS[j] = S1r[c + W];
+            FN[j] = N3r[c - W];
+        }
+        const T eE = edge[2 * b], eW = edge[2 * b + 1];
+        const uint32_t fl = flag[2 * b] | flag[2 * b + 1];
+        if (LOCAL) {
+            if (k >= geo.max_sweeps || (k > k_start && fl == 0u)) return false;
+        } else if (k >= k_target) {
+            return false;
+        }
+        T R[PW], L[PW];
+#pragma unroll
+        for (int j = 0; j < PW; ++j) {
+            R[j] = dpp_mov<0x134>(in[j][0]);  // wave_rol:1 -- lane i gets lane (i+1) mod 64
+            L[j] = dpp_mov<0x13C>(in[j][2]);  // wave_ror:1 -- lane i gets lane (i-1) mod 64
+        }
+        T o[PW][4];
+        T dm = (T)0;
+#pragma unroll
+        for (int j = 0; j < PW; ++j) {
+            // across the wave boundary: wave 0's last cell and wave 1's first cell through LDS
+            const T FE = lane == 63 ? (j + 1 < PW ? R[j + 1] : (w == 0 ? eE : R[j])) : R[j];
+            const T FW = lane == 0 ? (j > 0 ? L[j - 1] : (w == 1 ? eW : L[j])) : L[j];
+            const T m02 = vmax(in[j][0], in[j][2]), m13 = vmax(in[j][1], in[j][3]);
+            const T m[4] = {vmax(vmax(in[j][0], m13), FE), vmax(vmax(in[j][1], m02), FS[j]),
+                            vmax(vmax(in[j][2], m13), FW), vmax(vmax(in[j][3], m02), FN[j])};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[j][q] = ge[j] * m[q];
+        }
+#pragma unroll
+        for (int j = 0; j < PW; ++j) {
+            if ((goal_blocks >> j) & 1u) {  // max(fl(g * m), 1): the goal's reward
+#pragma unroll
+                for (int q = 0; q < 4; ++q) o[j][q] = ((goal >> (4 * j + q)) & 1u) ? vmax(o[j][q], (T)1) : o[j][q];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < PW; ++j) {
+            const int c = (w * PW + j) * 64 + lane;
+            S1w[c] = o[j][1];
+            N3w[c] = o[j][3];
+        }
+        if (w == 1 && lane == 0) edge[2 * (b ^ 1)] = o[0][0];
+        if (w == 0 && lane == 63) edge[2 * (b ^ 1) + 1] = o[PW - 1][2];
+        if (LOCAL || MGDP_RUNTO_DV_ALL || k + 1 == k_target) {
+#pragma unroll
+            for (int j = 0; j < PW; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) dm = vmax(dm, vabs(o[j][q] - in[j][q]));
+        }
+        diff = dm;
+        if (LOCAL) {
+            const bool more_w = __ballot(dm >= cf.tol) != 0ull;
+            if (lane == 0) flag[2 * (b ^ 1) + w] = more_w ? 1u : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < PW; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) out[j][q] = o[j][q];
+        ++k;
+        __syncthreads();  // this sweep's tile, edges and flags before the next sweep reads them
+        return true;
+    };
+    T alt[PW][4], prev[PW][4];
+    while (true) {
+        if (!sweep(WaveBuf<0>{}, own, alt)) {
+#pragma unroll
+            for (int j = 0; j < PW; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) prev[j][q] = alt[j][q];
+            break;
+        }
+        if (!sweep(WaveBuf<1>{}, alt, own)) {
+#pragma unroll
+            for (int j = 0; j < PW; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    prev[j][q] = own[j][q];
+                    own[j][q] = alt[j][q];
+                }
+            break;
+        }
+    }
+    {
+        const T dw = wave_max(diff);
+        if (lane == 0) dvx[w] = dw;
+    }
+    __syncthreads();  // both waves' |dV|; past this no sweep reads a tile
+    dvl = (double)vmax(dvx[0], dvx[1]);
+    if (LOCAL && gk.buf != nullptr && w == 0) gk_exit(gk, k, dvl);  // the launch's reduction (one wave per grid)
+    done(k, dvl);
+    // pi of the last sweep = argmax on V_{k-1} (`prev`), per action with the usual topology
+    T *const N3 = tile + padw, *const S1 = tile + padw + 64 * P;
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+        const int c = (w * PW + j) * 64 + lane;
+        S1[c] = prev[j][1];
+        N3[c] = prev[j][3];
+    }
+    if (w == 1 && lane == 0) edge[0] = prev[0][0];
+    if (w == 0 && lane == 63) edge[1] = prev[PW - 1][2];
+    __syncthreads();
+    const T eE = edge[0], eW = edge[1];
+    T R[PW], L[PW];
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+        R[j] = dpp_mov<0x134>(prev[j][0]);
+        L[j] = dpp_mov<0x13C>(prev[j][2]);
+    }
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+        const int c = (w * PW + j) * 64 + lane;
+        const T front[4] = {lane == 63 ? (j + 1 < PW ? R[j + 1] : (w == 0 ? eE : R[j])) : R[j], S1[c + W],
+                            lane == 0 ? (j > 0 ? L[j - 1] : (w == 1 ? eW : L[j])) : L[j], N3[c - W]};
+        if (c < geo.HW) {
+            const XydTopo<T> tp = xyd_topo<T>(cl, geo, c);
+            V4<T> op, tmp;
+            T nbv[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                op.v[d] = prev[j][d];
+                nbv[d] = (tp.nbi[d] >> 2) != c ? front[d] : prev[j][d];  // blocked / terminal: own state
+            }
+            uint32_t pk;
+            xyd_step<T, false, true>(tp, cf, op, nbv, tmp, pk);
+            *reinterpret_cast<uint32_t *>(pig + c * 4) = pk;
+            *reinterpret_cast<V4<T> *>(Vg_out + c * 4) = V4<T>{{own[j][0], own[j][1], own[j][2], own[j][3]}};
+        }
+    }
+}
+
 // Lone XYD grid on ONE wave, P cells per lane (cell j*64 + lane, same direction-major tiles with
 // HWs = 64*P).  A wave's LDS instructions execute in issue order, so the writes of sweep k are
 // seen by the reads of sweep k+1 without a workgroup barrier, and the stopping rule is the wave's
