@@ -159,6 +159,13 @@ def load():
         raise MgdpError(
             f"{LIB_PATH} is missing: build the HIP library first "
             "(python -c 'import __graft_entry__ as g; g.build()')")
+    # PyTorch-ROCm bundles its own HIP runtime under the same SONAME (libamdhip64.so.7) as the one
+    # libmgdp links; whichever is loaded first serves both, and torch's GPU init fails ("No HIP GPUs
+    # are available") if ours came first -- so torch, when present, is loaded before libmgdp.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(L, name)

@@ -3,6 +3,11 @@ import sys
 
 import pytest
 
+try:  # before libmgdp: PyTorch-ROCm's bundled HIP runtime must be the one loaded (see _lib.load)
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
