@@ -37,9 +37,13 @@ __host__ __device__ constexpr bool wp_is_wave2n(int wp) { return wp <= kWpWave2n
 #ifndef MGDP_WAVE2_P4_W6  // A/B builds: fp32 P = 4 (Empty-16) at 6 waves instead of its 91-VGPR 5
 #define MGDP_WAVE2_P4_W6 0
 #endif
+#ifndef MGDP_WAVE2N_MINW  // A/B builds: minimum waves per SIMD of the two-waves-per-grid kernels
+#define MGDP_WAVE2N_MINW 1
+#endif
 template <typename T>
 __host__ __device__ constexpr int wave2_min_waves(int wp) {
-    return (MGDP_WAVE2_W8 && wp_is_wave2(wp) && kWpWave2 - wp <= (sizeof(T) == 4 ? 2 : 1)) ? 8
+    return wp_is_wave2n(wp) ? MGDP_WAVE2N_MINW
+           : (MGDP_WAVE2_W8 && wp_is_wave2(wp) && kWpWave2 - wp <= (sizeof(T) == 4 ? 2 : 1)) ? 8
            : (MGDP_WAVE2_P4_W6 && wp_is_wave2(wp) && sizeof(T) == 4 && kWpWave2 - wp == 4) ? 6
                                                                                             : 1;
 }
