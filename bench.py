@@ -383,14 +383,15 @@ def main():
             reducer_box.append(Reducer(timing=True))  # built once; its stream carries the shards' launches
         return reducer_box[0]
 
-    def run_workload(name, dtype=None):
+    def run_workload(name, dtype=None, split_events=False):
         spec = WORKLOADS[name]
         t_gen = time.perf_counter()
         cells, (lo, hi) = make_cells(spec, rank, world)
         log(f"[rank {rank}] {name}: grids [{lo},{hi}) generated in {time.perf_counter() - t_gen:.1f}s")
         sharded = spec["sharded"] and (world > 1 or force_dist)
         wargs = argparse.Namespace(**{**vars(args), "workload": name})
-        m = measure(wargs, dtype or args.dtype, cells, local, dist, red_dev, get_reducer() if sharded else None, sharded)
+        m = measure(wargs, dtype or args.dtype, cells, local, dist, red_dev, get_reducer() if sharded else None, sharded,
+                    split_events=split_events)
         return spec, cells, (lo, hi), sharded, m
 
     # the BASELINE configs 3-5 beside the default line (every rank takes part), run BEFORE the
@@ -403,7 +404,7 @@ def main():
         # LavaS11N5 / DoorKey-16 x 65536 sharded over the N ranks; each with the oracle timed on a
         # bounded sample of the same grids at N = 1
         for name in ("fourrooms4096", "lava65536", "doorkey65536"):
-            bspec, bcells, (blo, bhi), bsharded, bm = run_workload(name)
+            bspec, bcells, (blo, bhi), bsharded, bm = run_workload(name, split_events=True)
             if rank == 0:
                 blk = {"value": bm["upd_total"] / bm["elapsed_max"], "unit": "updates/s",
                        "ms_per_solve": bm["elapsed_max"] * 1000.0 / args.steps, "sweeps": int(bm["sweeps"][-1]),
@@ -416,6 +417,10 @@ def main():
                     blk.update({"global_grids": (bhi - blo) * world, "scaling": "weak",
                                 "parallelism": f"independent batches x{world}"})
                 blk["roofline"] = workload_roofline(args, args.dtype, bm, name, bhi - blo)
+                if not bm["events_in_region"]:
+                    blk["roofline"]["events"] = ("launch durations from a second pass of the same solves with "
+                                                 "per-launch HIP events (they cost 6-9 us of host time per "
+                                                 "launch, so the timed region runs without them)")
                 if bm.get("executed"):
                     blk["executed_rank0"] = bm["executed"]
                 if bm.get("collectives"):
@@ -507,8 +512,12 @@ def compulsory_bytes_per_solve(info, tsize, method, sweeps):
     return B * (compulsory_bytes_per_sweep(S, HW, tsize) * sweeps + S * tsize + HW + S)
 
 
-def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded):
-    """W warmup solves, then K timed solves (barrier + synchronize on both sides, max over ranks)."""
+def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded, split_events=False):
+    """W warmup solves, then K timed solves (barrier + synchronize on both sides, max over ranks).
+    split_events (the BASELINE-config blocks beside the headline): the timed region runs without the
+    library's per-launch HIP events -- on a batched solve they cost 6-9 us of host time per launch
+    (tools/probe_timing_cost.py, profiles/r04_tcost/) -- and the launch durations for the roofline
+    come from a second pass of the same K solves with the events on."""
     import torch
 
     import minigrid_dynamicprogramming_amd as mg
@@ -539,7 +548,8 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded):
     # Warmup runs the timed sequence itself, edges included: timing on, W solves, then the same
     # end-of-region teardown (a resident lone-grid server leaves, stream and device drained), so
     # no first-time cost of that path lands in the timed region.
-    vi.enable_timing(True)
+    split = split_events and not vi.persistent
+    vi.enable_timing(not split)
     wstamps = [time.perf_counter()]
     for i in range(args.warmup):
         one_solve(last=i == args.warmup - 1)
@@ -550,7 +560,7 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded):
     # Re-enabling timing drops the warmup's launches; a persistent handle then gets untimed
     # priming solves, which relaunch the server (its launch is timed from here), so the timed
     # region holds no relaunch and its length does not depend on --steps.
-    vi.enable_timing(True)
+    vi.enable_timing(not split)
     if reducer is not None:
         reducer.collect()
         reducer.reset_counters()
@@ -626,6 +636,11 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded):
                                       "gap": round((t0 - pstamps[-1]) * 1e6, 2),
                                       "solves": [round(x, 2) for x in us[:-2]], "vi_sync": round(us[-2], 2),
                                       "dev_sync": round(us[-1], 2), "region": round(elapsed * 1e6, 2)}}))
+    if split:  # the roofline's launch durations: the same K solves again, per-launch events on
+        vi.enable_timing(True)
+        for i in range(args.steps):
+            one_solve()
+        vi.synchronize()
     kern_ms, launches = vi.kernel_time()
     clock = vi.serve_clock() if vi.persistent else None
     gsw = vi.grid_sweeps() if vi.B > 1 else None  # sweeps each grid executed in the last solve
@@ -677,6 +692,7 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded):
                             "(|dV| = 0) is complete for the global K (V, pi bit-identical), its remaining "
                             "K - k_e sweeps are not executed; value counts B*S*A*K as the metric defines"}
     return {"elapsed_max": elapsed_max, "upd_total": upd_total, "sweeps": sweeps, "kern_ms": kern_ms,
+            "events_in_region": not split,
             "executed": executed,
             "launches": launches, "primed": primed, "timed_primed": PRIME_RELAUNCH if info["persistent"] else 0,
             "info": info, "collectives": collectives, "latency": lat}

@@ -122,3 +122,16 @@ def test_measure_batch_executed_sweeps(bench):
     ex = m["executed"]
     assert ex["global_sweeps"] == K and 0 < ex["frac_of_global_rule"] <= 1.0
     assert m["latency"] is None and m["primed"] == 0
+
+
+def test_measure_split_events_pass(bench):
+    # the blocks' timed region runs without per-launch events; the roofline's launch count comes
+    # from the second pass of the same K solves
+    from minigrid_dynamicprogramming_amd import make
+
+    env = make("MiniGrid-FourRooms-v0")
+    cells = np.stack([np.ascontiguousarray(env.generate(seed=s)[0][..., 0].T) for s in range(4)])
+    m = bench.measure(_args("fourrooms4096", steps=4), "f32", cells, 0, None, None, None, False, split_events=True)
+    assert m["events_in_region"] is False and m["launches"] == 4 and len(m["sweeps"]) == 4
+    m = bench.measure(_args("fourrooms4096", steps=4), "f32", cells, 0, None, None, None, False)
+    assert m["events_in_region"] is True
