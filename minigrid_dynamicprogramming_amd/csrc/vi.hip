@@ -894,10 +894,11 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
         if (vi->wave2) {
             int cus = 0;
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d.device);
-            // Two waves per grid when one wave per grid leaves the SIMDs short of waves (B <= one
-            // wave per SIMD... four per SIMD: FourRooms x 4096) and a grid has >= 4 blocks of 64
-            // cells to split (MGDP_WAVE2N=0 / 1 forces it off / on where it applies).
-            int w2n = d.B <= 4 * 4 * cus && vi->wave2 >= 4 ? 1 : 0;
+            // Two waves per grid (MGDP_WAVE2N=1, grids of >= 3 blocks of 64 cells): measured slower
+            // than one wave per grid even where one wave per grid leaves the SIMDs short of waves --
+            // FourRooms x 4096: 64-65 us per solve (74 VGPRs, 6 waves / SIMD) or 57 us compiled for
+            // 8 waves / SIMD, vs 55-56 us on one wave (profiles/r04_w2nab/) -- so it is off by default.
+            int w2n = 0;
             if (const char *ev = std::getenv("MGDP_WAVE2N")) w2n = std::atoi(ev) != 0 && vi->wave2 >= 3;
             if (w2n) {
                 vi->wave2n = (vi->wave2 + 1) / 2;
