@@ -431,7 +431,10 @@ def main():
                     blk["cpu_baseline_all_cores"] = cpu_baseline(bcells, model, args.gamma, args.tol, args.dtype,
                                                                  BLOCK_CPU_S, nthreads=host_cores())
                 (blocks if bspec["sharded"] else batched)[name] = blk
-    spec, cells, (lo, hi), sharded, m = run_workload(args.workload)
+    # MGDP_BENCH_SPLIT_EVENTS=1 (rehearsal knob, tools/gpu_shard_prof.sh): the main line's region
+    # without per-launch events too, as the blocks beside the headline run it
+    spec, cells, (lo, hi), sharded, m = run_workload(args.workload,
+                                                     split_events=os.environ.get("MGDP_BENCH_SPLIT_EVENTS") == "1")
     if rank != 0:  # the fp64 side line and the CPU baselines are N = 1 only
         if dist is not None:
             dist.barrier()
@@ -564,6 +567,7 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded, split_ev
     if reducer is not None:
         reducer.collect()
         reducer.reset_counters()
+        reducer.timing = reducer.device.type == "cuda" and not split  # its events too: the events pass
     barrier()
     torch.cuda.synchronize()
     # Priming to a steady state (persistent lone-grid server), in two phases.
@@ -636,8 +640,14 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded, split_ev
                                       "gap": round((t0 - pstamps[-1]) * 1e6, 2),
                                       "solves": [round(x, 2) for x in us[:-2]], "vi_sync": round(us[-2], 2),
                                       "dev_sync": round(us[-1], 2), "region": round(elapsed * 1e6, 2)}}))
+    red_region = None
+    if reducer is not None:  # the region's protocol counters (the events pass below adds its own)
+        red_region = (reducer.calls, reducer.host_reads, reducer.wall_s)
     if split:  # the roofline's launch durations: the same K solves again, per-launch events on
         vi.enable_timing(True)
+        if reducer is not None:
+            reducer.reset_counters()
+            reducer.timing = reducer.device.type == "cuda"
         for i in range(args.steps):
             one_solve()
         vi.synchronize()
@@ -652,12 +662,14 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded, split_ev
     collectives = None
     if reducer is not None:
         dev_ms = reducer.collect()
-        collectives = {"allreduces_per_solve": reducer.calls / args.steps,
-                       "host_reads_per_solve": reducer.host_reads / args.steps,
+        calls, reads, wall_s = red_region
+        collectives = {"allreduces_per_solve": calls / args.steps,
+                       "host_reads_per_solve": reads / args.steps,
                        "allreduce_us_per_solve_rank0": dev_ms * 1000.0 / args.steps,
-                       "protocol_host_us_per_solve_rank0": reducer.wall_s * 1e6 / args.steps,
+                       "protocol_host_us_per_solve_rank0": wall_s * 1e6 / args.steps,
                        "note": "device time of the RCCL all-reduces (events on the protocol stream, includes "
-                               "waiting for the slowest rank) and host time of the one read per solve"}
+                               "waiting for the slowest rank; from the events pass when the region runs "
+                               "without events) and host time of the one read per solve"}
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         u = torch.tensor([upd_rank], dtype=torch.float64, device=red_dev)
