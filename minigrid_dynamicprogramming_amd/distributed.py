@@ -75,6 +75,8 @@ class Reducer:
         self.buf = torch.zeros(1, dtype=torch.float64, device=self.device)
         self.buf2 = torch.zeros(2, dtype=torch.float64, device=self.device)
         self.proto = torch.zeros(8, dtype=torch.int64, device=self.device)
+        # the protocol's views of it, made once (a slice is a new tensor object on every use)
+        self.p_local, self.p_kd, self.p_dv = self.proto[0:4], self.proto[0:2], self.proto[5:6]
         self.stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
         self.timing = timing and self.device.type == "cuda"
         self._events = []
@@ -178,10 +180,10 @@ def _device_capable(vi, red) -> bool:
 def _device_protocol(vi, red):
     p = red.proto
     vi.reset()
-    vi.run_local_dev(p[0:4])              # {k max, own-rule dV bits, k min, epoch}
-    red.max_(p[0:2])                      # K = the slowest grid anywhere, E = the largest own-rule dV
+    vi.run_local_dev(red.p_local)         # {k max, own-rule dV bits, k min, epoch}
+    red.max_(red.p_kd)                    # K = the slowest grid anywhere, E = the largest own-rule dV
     t = time.perf_counter()
-    k, dv, rule = vi.run_to_dev_sync(p[0:2])  # every grid to exactly K; the solve's one host wait
+    k, dv, rule = vi.run_to_dev_sync(red.p_kd)  # the gate (or run_to K); the solve's one host wait
     red.wall_s += time.perf_counter() - t
     red.host_reads += 1
     if rule == 0.0:                       # every grid everywhere at an exact fixed point: dV(K) = 0
@@ -189,8 +191,8 @@ def _device_protocol(vi, red):
             raise RuntimeError(f"fixed-point invariant violated: dV at sweep {k} is {dv!r} after an exact "
                                "fixed point on every rank")
     else:
-        p[5:6].fill_(double_to_bits(dv))
-        red.max_(p[5:6])                  # dV at K over every rank
+        red.p_dv.fill_(double_to_bits(dv))
+        red.max_(red.p_dv)                # dV at K over every rank
         t = time.perf_counter()
         dv = bits_to_double(int(p[5].item()))
         red.wall_s += time.perf_counter() - t
@@ -208,9 +210,9 @@ def _host_protocol(vi, red):
     vi.reset()
     k_loc, e_loc = _local(vi)
     p[0:2].copy_(red.torch.tensor([int(k_loc), double_to_bits(e_loc)], dtype=red.torch.int64))
-    red.max_(p[0:2])
+    red.max_(red.p_kd)
     t = time.perf_counter()
-    K, e_bits = p[0:2].tolist()
+    K, e_bits = red.p_kd.tolist()
     red.wall_s += time.perf_counter() - t
     red.host_reads += 1
     k = int(K)
@@ -219,8 +221,8 @@ def _host_protocol(vi, red):
         if dv != 0.0:
             raise RuntimeError(f"fixed-point invariant violated: dV at sweep {k} is {dv!r}")
     else:
-        p[5:6].fill_(double_to_bits(dv))
-        red.max_(p[5:6])
+        red.p_dv.fill_(double_to_bits(dv))
+        red.max_(red.p_dv)
         t = time.perf_counter()
         dv = bits_to_double(int(p[5].item()))
         red.wall_s += time.perf_counter() - t

@@ -298,9 +298,12 @@ class ValueIteration:
         runs the host protocol only: sweep method, horizon or NoDeath options)."""
         if self.desc.method != _lib.METHOD_FUSED or self.horizon > 0 or self.desc.lava_mode != 0:
             return None
-        import torch
+        dev = getattr(self, "_protocol_dev", None)
+        if dev is None:
+            import torch
 
-        return torch.device("cuda", self.desc.device)
+            dev = self._protocol_dev = torch.device("cuda", self.desc.device)
+        return dev
 
     def bind_stream(self, stream_ptr: int):
         """Launch on this hipStream_t from now on (no-op when it already does)."""
@@ -310,7 +313,11 @@ class ValueIteration:
 
     def run_local_dev(self, pub):
         """pub: int64 CUDA tensor (or pointer) of 4 words <- {k max, dV bits, k min, epoch}."""
-        _lib.check(self.L.mgdp_vi_run_local_dev(self.h, _lib.ptr(pub)), "mgdp_vi_run_local_dev")
+        if getattr(self, "_rld_fn", None) is None:
+            self._rld_fn = _lib.raw_fn("mgdp_vi_run_local_dev")
+        rc = self._rld_fn(self.h, _lib.ptr(pub))
+        if rc:
+            _lib.check(rc, "mgdp_vi_run_local_dev")
 
     def run_to_dev(self, k, pub):
         """Every grid to exactly the sweep held by the int64 device word k; results into pub."""

@@ -227,6 +227,7 @@ class _FakeReducer:
         self.stream = None
         self.device = torch.device("cpu")
         self.proto = torch.zeros(8, dtype=torch.int64)
+        self.p_local, self.p_kd, self.p_dv = self.proto[0:4], self.proto[0:2], self.proto[5:6]
 
     def max(self, x):
         self.calls += 1
