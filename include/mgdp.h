@@ -221,9 +221,11 @@ int mgdp_vi_enable_timing(mgdp_vi *vi, int32_t on);
 int mgdp_vi_kernel_time(mgdp_vi *vi, double *total_ms, int64_t *launches);
 /* Clock of the persistent lone-grid servers (vi_serve_kernel) that ran since enable_timing: each
  * launch reports its shader-clock cycles (s_memtime) and 100 MHz ticks (s_memrealtime) when it
- * leaves; sclk_mhz = cycles / time, server_us = their summed lifetimes.  0 launches: no server ran.
- * A diagnostic of the device's clock state (the bench line reports it); no cost per solve. */
-int mgdp_vi_serve_clock(mgdp_vi *vi, double *sclk_mhz, double *server_us, int64_t *launches);
+ * leaves; sclk_mhz = cycles / time, server_us = their summed lifetimes; solve_us = the mean
+ * GPU-side time of their solves (the poll that saw a request -> the solve's end), over `solves`.
+ * 0 launches: no server ran.  A diagnostic (the bench line reports it); no cost per solve. */
+int mgdp_vi_serve_clock(mgdp_vi *vi, double *sclk_mhz, double *server_us, int64_t *launches, double *solve_us,
+                        int64_t *solves);
 
 /* ---------------------------------------------------------------------------------------------- */
 /* Batched env stepping: the gymnasium Env reset()/step() surface (minigrid_env.py:119-157,         */

@@ -99,7 +99,7 @@ SIGNATURES = {
     "mgdp_vi_synchronize": (ctypes.c_int, [_P]),
     "mgdp_vi_enable_timing": (ctypes.c_int, [_P, _I32]),
     "mgdp_vi_kernel_time": (ctypes.c_int, [_P, _DP, _I64P]),
-    "mgdp_vi_serve_clock": (ctypes.c_int, [_P, _DP, _DP, _I64P]),
+    "mgdp_vi_serve_clock": (ctypes.c_int, [_P, _DP, _DP, _I64P, _DP, _I64P]),
     "mgdp_vi_persistent": (ctypes.c_int, [_P, _I32P]),
     "mgdp_vi_kernel_name": (ctypes.c_char_p, [_P]),
     "mgdp_vi_get_policy_t": (ctypes.c_int, [_P, _P]),

@@ -134,7 +134,7 @@ struct mgdp_vi {
     // clock of the departed servers since enable_timing (mgdp_vi_serve_clock): shader-clock cycles and
     // 100 MHz ticks of their lives, summed as each one's exit word is seen (kHoutClk)
     unsigned long long clk_tag = 0;  // the last server launch whose clock words were added
-    double clk_cycles = 0.0, clk_ticks = 0.0;
+    double clk_cycles = 0.0, clk_ticks = 0.0, clk_busy = 0.0, clk_solves = 0.0;
     long long clk_launches = 0;
     // launch-wide global rule (GkCtx, fused_wave2_xyd): one launch per batched solve when every grid
     // wave of the batch can be resident at once (MGDP_GK=0 turns it off)
@@ -623,6 +623,8 @@ void account_server_clock(mgdp_vi *vi) {
     std::atomic_thread_fence(std::memory_order_acquire);
     vi->clk_cycles += (double)h[kHoutClk];
     vi->clk_ticks += (double)h[kHoutClk + 1];
+    vi->clk_busy += (double)h[kHoutClk + 2];
+    vi->clk_solves += (double)h[kHoutClk + 3];
     ++vi->clk_launches;
     vi->clk_tag = vi->serve_tag;
 }
@@ -1554,12 +1556,13 @@ int mgdp_vi_enable_timing(mgdp_vi *vi, int32_t on) {
     vi->timing = on != 0;
     vi->total_ms = 0.0;
     vi->launches = 0;
-    vi->clk_cycles = vi->clk_ticks = 0.0;
+    vi->clk_cycles = vi->clk_ticks = vi->clk_busy = vi->clk_solves = 0.0;
     vi->clk_launches = 0;
     return 0;
 }
 
-int mgdp_vi_serve_clock(mgdp_vi *vi, double *sclk_mhz, double *server_us, int64_t *launches) {
+int mgdp_vi_serve_clock(mgdp_vi *vi, double *sclk_mhz, double *server_us, int64_t *launches, double *solve_us,
+                        int64_t *solves) {
     MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
     DeviceGuard guard(vi->d.device);
     if (int rc = server_stop(vi)) return rc;
@@ -1567,6 +1570,8 @@ int mgdp_vi_serve_clock(mgdp_vi *vi, double *sclk_mhz, double *server_us, int64_
     if (sclk_mhz) *sclk_mhz = vi->clk_ticks > 0 ? vi->clk_cycles / (vi->clk_ticks * 0.01) : 0.0;
     if (server_us) *server_us = vi->clk_ticks * 0.01;
     if (launches) *launches = vi->clk_launches;
+    if (solve_us) *solve_us = vi->clk_solves > 0 ? vi->clk_busy * 0.01 / vi->clk_solves : 0.0;
+    if (solves) *solves = (int64_t)vi->clk_solves;
     return 0;
 }
 

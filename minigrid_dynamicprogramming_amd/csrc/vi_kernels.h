@@ -338,7 +338,8 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
 // (s_memrealtime, 100 MHz); the host relaunches the server if a request finds it gone.
 constexpr int kHoutWords = 32;  // host-mapped words of a handle (mgdp_vi::h_out)
 constexpr int kHoutReq = 16;    // request word; its source word follows (one 16-B pair)
-constexpr int kHoutClk = 24;    // a departing server's {shader-clock cycles, 100 MHz ticks} of its life
+constexpr int kHoutClk = 24;    // a departing server's {shader-clock cycles, 100 MHz ticks} of its life,
+                                // then {100 MHz ticks inside its solves, solves served}
 constexpr unsigned long long kServeQuit = ~0ull;
 constexpr unsigned long long kServeNewCells = 1ull << 62;
 constexpr unsigned long long kServeLast = 1ull << 61;  // request flag: leave after serving it
@@ -386,6 +387,9 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     const unsigned long long c_start = __builtin_amdgcn_s_memtime();  // shader-clock cycles
     unsigned long long t_last = t_start;
+    // GPU-side time of the solves (thread 0: the poll that saw the request -> the solve's end,
+    // s_memrealtime ticks already read for the idle limit, so no extra counter read per solve)
+    unsigned long long t_seen = t_start, busy = 0, solves = 0;
     __syncthreads();
     // the grid stays put between kServeNewCells requests: resolve this thread's cell topology once
     typename TopoOf<T, MODEL>::type topo;
@@ -415,6 +419,7 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
                 }
                 const unsigned long long now = __builtin_amdgcn_s_memrealtime();
                 if (cmd != served) {
+                    t_seen = now;
                     if (cmd != kServeQuit && (cmd & kServeNewCells)) {
                         // the host wrote the source word before the request word; its tag proves it
                         // belongs to this request (a stale read is simply repeated)
@@ -465,8 +470,12 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
             publish_tagged(host_out, k, dvl, (unsigned int)cmd);
         if (ew == 2) ew = 1;  // the tiles' pads stay +0 until the next grid
         served = cmd;
-        if (cmd & kServeLast) break;
         t_last = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0) {
+            busy += t_last - t_seen;
+            ++solves;
+        }
+        if (cmd & kServeLast) break;
         // Every wave is past s_cmd and the LDS tiles before the next request: an LDS-only barrier.
         // The V / pi stores of this solve stay in flight while the next request is polled (a
         // __syncthreads would drain them first); the host reads V / pi only after server_stop
@@ -485,6 +494,8 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
         __hip_atomic_store(host_out + kHoutClk, __builtin_amdgcn_s_memtime() - c_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(host_out + kHoutClk + 1, __builtin_amdgcn_s_memrealtime() - t_start, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host_out + kHoutClk + 2, busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host_out + kHoutClk + 3, solves, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(host_out + 11, exit_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }

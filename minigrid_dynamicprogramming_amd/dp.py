@@ -454,9 +454,11 @@ class ValueIteration:
         """Shader clock of the persistent lone-grid servers that ran since enable_timing(): each
         launch's s_memtime cycles over its s_memrealtime lifetime (mgdp_vi_serve_clock)."""
         mhz, us, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
-        _lib.check(self.L.mgdp_vi_serve_clock(self.h, ctypes.byref(mhz), ctypes.byref(us), ctypes.byref(n)),
-                   "mgdp_vi_serve_clock")
-        return {"sclk_mhz": mhz.value, "server_us": us.value, "launches": n.value}
+        sus, ns = ctypes.c_double(), ctypes.c_int64()
+        _lib.check(self.L.mgdp_vi_serve_clock(self.h, ctypes.byref(mhz), ctypes.byref(us), ctypes.byref(n),
+                                              ctypes.byref(sus), ctypes.byref(ns)), "mgdp_vi_serve_clock")
+        return {"sclk_mhz": mhz.value, "server_us": us.value, "launches": n.value, "gpu_solve_us": sus.value,
+                "solves": ns.value}
 
     def kernel_time(self) -> tuple[float, int]:
         ms = ctypes.c_double(0)
