@@ -696,6 +696,11 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded, split_ev
         if clock and clock["launches"]:
             lat["device_clock"] = {**clock, "source": "vi_serve_kernel s_memtime cycles / s_memrealtime over the "
                                                       "timed launch (relaunch priming + timed solves)"}
+            if clock.get("gpu_solve_us"):
+                # where a solve's time goes: on the GPU (request seen -> solve end) vs the rest
+                # (host call, request / result over PCIe, the region's edges)
+                lat["gpu_solve_us"] = round(clock["gpu_solve_us"], 3)
+                lat["host_and_handoff_us"] = round(elapsed * 1e6 / args.steps - clock["gpu_solve_us"], 3)
     executed = None
     if gsw is not None and sweeps[-1] > 0:
         executed = {"mean_grid_sweeps": round(float(gsw.mean()), 3), "global_sweeps": int(sweeps[-1]),
