@@ -77,10 +77,38 @@ class Reducer:
         self.proto = torch.zeros(8, dtype=torch.int64, device=self.device)
         # the protocol's views of it, made once (a slice is a new tensor object on every use)
         self.p_local, self.p_kd, self.p_dv = self.proto[0:4], self.proto[0:2], self.proto[5:6]
+        # the group's allreduce with prebuilt options: dist.all_reduce's argument checks cost more host
+        # time per call than issuing the collective (same collective, same stream ordering: wait())
+        self._pg = group if group is not None else dist.group.WORLD
+        self._opts_max = dist.AllreduceOptions()
+        self._opts_max.reduceOp = dist.ReduceOp.MAX
         self.stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        # entering / leaving the protocol stream per solve: torch's StreamContext costs ~6 us of
+        # Python per solve; its two C calls directly (the context manager when they are absent)
+        self._get_stream = getattr(torch._C, "_cuda_getCurrentStream", None)
+        self._set_stream = getattr(torch._C, "_cuda_setStream", None)
+        if self.stream is not None:
+            self.stream_ptr = int(self.stream.cuda_stream)
+            self._stream_ids = (self.stream.stream_id, self.stream.device_index, self.stream.device_type)
         self.timing = timing and self.device.type == "cuda"
         self._events = []
         self.reset_counters()
+
+    def enter_stream(self):
+        """Make the protocol stream current; returns what exit_stream needs to restore the caller's."""
+        if self._get_stream is None or self._set_stream is None:
+            ctx = self.torch.cuda.stream(self.stream)
+            ctx.__enter__()
+            return ctx
+        prev = self._get_stream(self.device.index)
+        self._set_stream(*self._stream_ids)
+        return prev
+
+    def exit_stream(self, prev):
+        if isinstance(prev, tuple):
+            self._set_stream(*prev)
+        else:
+            prev.__exit__(None, None, None)
 
     def reset_counters(self):
         self.calls = 0
@@ -93,7 +121,7 @@ class Reducer:
         """Host round trip: all-reduce one scalar and read it back."""
         t = time.perf_counter()
         self.buf.fill_(float(x))
-        self.dist.all_reduce(self.buf, op=self.dist.ReduceOp.MAX, group=self.group)
+        self._all_reduce_max(self.buf)
         self.calls += 1
         self.host_reads += 1
         v = float(self.buf.item())
@@ -106,11 +134,14 @@ class Reducer:
             a = self.torch.cuda.Event(enable_timing=True)
             b = self.torch.cuda.Event(enable_timing=True)
             a.record()
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+        self._all_reduce_max(t)
         if self.timing:
             b.record()
             self._events.append((a, b))
         self.calls += 1
+
+    def _all_reduce_max(self, t):
+        self._pg.allreduce([t], self._opts_max).wait()
 
     def collect(self) -> float:
         """Fold the recorded all-reduce event pairs into device_ms (after a synchronize)."""
@@ -249,9 +280,12 @@ def solve_sharded(vi, group=None, reducer=None) -> dict:
     calls0, reads0 = red.calls, red.host_reads
     if device:
         if red.stream is not None:
-            vi.bind_stream(red.stream.cuda_stream)
-            with red.torch.cuda.stream(red.stream):
+            vi.bind_stream(red.stream_ptr)
+            prev = red.enter_stream()
+            try:
                 k, dv = _device_protocol(vi, red)
+            finally:
+                red.exit_stream(prev)
         else:
             k, dv = _device_protocol(vi, red)
     else:

@@ -31,21 +31,21 @@ def main():
     torch.cuda.synchronize()
     n = 200
     t = np.zeros((n, 8))
-    p = red.proto
     for i in range(n):
         a = time.perf_counter()
-        vi.bind_stream(red.stream.cuda_stream)
-        with torch.cuda.stream(red.stream):
-            b = time.perf_counter()
-            vi.reset()
-            c = time.perf_counter()
-            vi.run_local_dev(p[0:4])
-            d = time.perf_counter()
-            dist.all_reduce(p[0:2], op=dist.ReduceOp.MAX)
-            e = time.perf_counter()
-            k, dv, rule = vi.run_to_dev_sync(p[0:2])
-            f = time.perf_counter()
-            vi.set_result(k, dv)
+        vi.bind_stream(red.stream_ptr)
+        prev = red.enter_stream()
+        b = time.perf_counter()
+        vi.reset()
+        c = time.perf_counter()
+        vi.run_local_dev(red.p_local)
+        d = time.perf_counter()
+        red.max_(red.p_kd)
+        e = time.perf_counter()
+        k, dv, rule = vi.run_to_dev_sync(red.p_kd)
+        f = time.perf_counter()
+        vi.set_result(k, dv)
+        red.exit_stream(prev)
         g = time.perf_counter()
         vi.finish(k, dv)
         h = time.perf_counter()
@@ -66,6 +66,24 @@ def main():
         vi.solve()
         ts.append(time.perf_counter() - a)
     out["direct_solve_us"] = round(float(np.median(ts)) * 1e6, 2)
+    # the host cost of the two steps made cheaper in round 4, old way beside new way
+    def med(f):
+        ts = []
+        for _ in range(n):
+            a = time.perf_counter()
+            f()
+            ts.append(time.perf_counter() - a)
+        return round(float(np.median(ts)) * 1e6, 2)
+
+    def ctx():
+        with torch.cuda.stream(red.stream):
+            pass
+
+    out["torch_stream_ctx_us"] = med(ctx)
+    out["enter_exit_stream_us"] = med(lambda: red.exit_stream(red.enter_stream()))
+    out["dist_all_reduce_us"] = med(lambda: dist.all_reduce(red.p_kd, op=dist.ReduceOp.MAX))
+    out["pg_allreduce_us"] = med(lambda: red._all_reduce_max(red.p_kd))
+    torch.cuda.synchronize()
     print(json.dumps(out), flush=True)
     vi.close()
     dist.destroy_process_group()
