@@ -82,6 +82,8 @@ class Reducer:
         self._pg = group if group is not None else dist.group.WORLD
         self._opts_max = dist.AllreduceOptions()
         self._opts_max.reduceOp = dist.ReduceOp.MAX
+        if hasattr(self._opts_max, "asyncOp"):  # synchronous: RCCL runs on the current stream itself
+            self._opts_max.asyncOp = False
         self.stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
         # entering / leaving the protocol stream per solve: torch's StreamContext costs ~6 us of
         # Python per solve; its two C calls directly (the context manager when they are absent)
@@ -141,7 +143,9 @@ class Reducer:
         self.calls += 1
 
     def _all_reduce_max(self, t):
-        self._pg.allreduce([t], self._opts_max).wait()
+        work = self._pg.allreduce([t], self._opts_max)
+        if work is not None:
+            work.wait()
 
     def collect(self) -> float:
         """Fold the recorded all-reduce event pairs into device_ms (after a synchronize)."""
