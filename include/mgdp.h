@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MGDP_ABI_VERSION 9
+#define MGDP_ABI_VERSION 10
 
 enum {
     MGDP_OK = 0,
@@ -265,9 +265,20 @@ int mgdp_envs_kernel_time(mgdp_envs *envs, double *total_ms, int64_t *launches);
  * step_count B.  Any pointer may be NULL. */
 int mgdp_envs_get_state(mgdp_envs *envs, uint8_t *enc, int32_t *agent, int32_t *carry,
                         int32_t *step_count);
-/* Overwrite agent (B*3), carry (B*2) and step_count (B) of the masked envs (NULL = unchanged). */
+/* Overwrite agent (B*3), carry (B*2) and step_count (B) of the masked envs (NULL = unchanged).
+ * A new carry clears that env's carried Box contents (set them again with set_contents). */
 int mgdp_envs_set_state(mgdp_envs *envs, const int32_t *agent, const int32_t *carry,
                         const int32_t *step_count, const uint8_t *mask);
+/* Box(contains=...) (ABI 10; world_object.py:272-294, replaces the `contains` attribute of the
+ * reference's Box): what each Box cell holds, contents B*W*H*3 (x-major (type, colour, state) like
+ * Grid.encode(); type 0 / 1 = holds nothing), and what a carried Box holds, carry_contents B*3
+ * (NULL = unchanged).  Toggling a Box puts its contents in its cell (None: empty), pickup carries
+ * them with the Box, drop puts them back.  A held object must be a Grid.encode() cell on a Box cell
+ * (a carried one needs a carried Box); one level: a held Box holds nothing.  mgdp_envs_load clears
+ * the loaded envs' contents.  The step kernel touches the contents planes only once they exist. */
+int mgdp_envs_set_contents(mgdp_envs *envs, const uint8_t *contents, const int32_t *carry_contents);
+/* Read back contents (B*W*H*3) and carry_contents (B*3); zeros where nothing is held. */
+int mgdp_envs_get_contents(mgdp_envs *envs, uint8_t *contents, int32_t *carry_contents);
 
 /* ---------------------------------------------------------------------------------------------- */
 /* Batched reset(seed) grid generation on the GPU.  Env b gets seed seed0 + b */

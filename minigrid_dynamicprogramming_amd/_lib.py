@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # MGDP_LIB: an alternative build of the same sources (tools/ experiments with compile-time knobs)
 LIB_PATH = os.environ.get("MGDP_LIB") or os.path.join(HERE, "libmgdp.so")
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 MGDP_OK = 0
 MGDP_E_INVALID = -1
 MGDP_E_HIP = -2
@@ -117,6 +117,8 @@ SIGNATURES = {
     "mgdp_envs_kernel_time": (ctypes.c_int, [_P, _DP, _I64P]),
     "mgdp_envs_get_state": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "mgdp_envs_set_state": (ctypes.c_int, [_P, _P, _P, _P, _P]),
+    "mgdp_envs_set_contents": (ctypes.c_int, [_P, _P, _P]),
+    "mgdp_envs_get_contents": (ctypes.c_int, [_P, _P, _P]),
 }
 
 _lib = None

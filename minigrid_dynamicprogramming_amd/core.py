@@ -6,7 +6,9 @@ Mirrors the reference's core layer so that user code reads the same:
   WorldObj &c. minigrid/core/world_object.py:27-294 (data + predicates only; no rendering)
   Grid         minigrid/core/grid.py:20-143, 244-289 (no rendering)
 The grid is stored as three uint8 planes (type, colour, state), row-major [y][x] -- the same flat
-int8 layout that is uploaded to HBM for the HIP kernels.
+int8 layout that is uploaded to HBM for the HIP kernels -- plus three "held" planes: the object a
+Box holds (Box(contains=...), world_object.py:272-294; type 0 = nothing), the HIP step's contents
+plane (mgdp_envs_set_contents).
 """
 from __future__ import annotations
 
@@ -167,8 +169,8 @@ class Ball(WorldObj):
 
 
 class Box(WorldObj):
-    """Box; the HIP step models an empty box (toggling it leaves an empty cell).  Grid.set refuses a
-    box that holds an object."""
+    """Box (world_object.py:272-294): toggling it puts `contains` in its cell (None: empty), and a
+    carried Box keeps what it holds.  One level: a held Box holds nothing (Grid.set refuses more)."""
 
     def __init__(self, color, contains: WorldObj | None = None):
         super().__init__("box", color)
@@ -194,31 +196,38 @@ class Grid:
         self.type = np.full((height, width), OBJECT_TO_IDX["empty"], np.uint8)
         self.color = np.zeros((height, width), np.uint8)
         self.state = np.zeros((height, width), np.uint8)
+        # what a Box cell holds: (type, colour, state) planes, type 0 = nothing
+        self.held = np.zeros((3, height, width), np.uint8)
         self._owner = None
 
     # -- element access
     def set(self, i: int, j: int, v: WorldObj | None):
         assert 0 <= i < self.width, f"column index {i} outside of grid of width {self.width}"
         assert 0 <= j < self.height, f"row index {j} outside of grid of height {self.height}"
+        held = (0, 0, 0)
         if v is None:
             t, c, s = OBJECT_TO_IDX["empty"], 0, 0
         else:
-            if getattr(v, "contains", None) is not None:
-                # the grid is (type, colour, state) per cell, in HBM one byte per cell: a Box holding
-                # an object (world_object.py:272-294, toggle replaces the box by its contents)
-                # cannot be expressed, and no target family places one -- refuse it rather than
-                # step a different env
-                raise NotImplementedError("Box(contains=...) is not modelled: boxes are stepped as "
-                                          "empty (toggle leaves an empty cell); see DESIGN.md")
+            inner = getattr(v, "contains", None)
+            if inner is not None:
+                # the device holds one contents byte per cell (csrc/envs.hip): a Box's object, one level
+                if v.type != "box" or getattr(inner, "contains", None) is not None:
+                    raise NotImplementedError("only a Box holds an object, and a held Box holds nothing "
+                                              "(one contents level; see DESIGN.md)")
+                held = inner.encode()
             t, c, s = v.encode()
         self.type[j, i], self.color[j, i], self.state[j, i] = t, c, s
+        self.held[:, j, i] = held
         if self._owner is not None:
             self._owner._grid_edited()
 
     def get(self, i: int, j: int) -> WorldObj | None:
         assert 0 <= i < self.width
         assert 0 <= j < self.height
-        return WorldObj.decode(self.type[j, i], self.color[j, i], self.state[j, i])
+        v = WorldObj.decode(self.type[j, i], self.color[j, i], self.state[j, i])
+        if v is not None and self.held[0, j, i] > OBJECT_TO_IDX["empty"]:
+            v.contains = WorldObj.decode(*self.held[:, j, i])
+        return v
 
     def is_empty(self, i: int, j: int) -> bool:
         return self.type[j, i] == OBJECT_TO_IDX["empty"]
@@ -251,6 +260,13 @@ class Grid:
             arr = np.where(np.asarray(vis_mask, bool)[:, :, None], arr, 0).astype(np.uint8)
         return arr
 
+    def encode_held(self) -> np.ndarray:
+        """(W, H, 3) x-major: what each Box cell holds (zeros elsewhere); mgdp_envs_set_contents' layout."""
+        return np.ascontiguousarray(self.held.transpose(2, 1, 0))
+
+    def load_held(self, array: np.ndarray):
+        self.held[...] = np.asarray(array, np.uint8).transpose(2, 1, 0)
+
     @staticmethod
     def decode(array: np.ndarray) -> tuple["Grid", np.ndarray]:
         width, height, channels = array.shape
@@ -268,6 +284,7 @@ class Grid:
         self.type[...] = t
         self.color[...] = np.where(empty, 0, a[:, :, 1].T)
         self.state[...] = np.where(empty, 0, a[:, :, 2].T)
+        self.held[...] = 0
 
     def cells(self) -> np.ndarray:
         """(H, W) OBJECT_TO_IDX codes, row-major: the DP kernels' input layout."""
@@ -300,6 +317,7 @@ class Grid:
         g.type[...] = self.type
         g.color[...] = self.color
         g.state[...] = self.state
+        g.held[...] = self.held
         return g
 
     def __getstate__(self):

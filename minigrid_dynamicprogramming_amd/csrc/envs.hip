@@ -11,6 +11,9 @@
 //   cell        uint8 [B][HWp]   one-byte cell code (type, colour, state), row-major, see cell_code
 //   agent       int32 [B][4]     x, y, dir, step_count
 //   carry       int32 [B][2]     carried (type, colour); type 0 = nothing
+//   contents    uint8 [B][HWp]   optional (mgdp_envs_set_contents): the cell code of the object a
+//                                Box at that cell holds (Box(contains=...), world_object.py:272-294),
+//                                0 = none; ccontents uint8 [B]: the same for a carried Box
 //   max_steps   int32 [B], see uint8 [B] (see_through_walls)
 // One step = one envs_step_kernel launch: 2 lanes per env (see the kernel).  The V x V view is
 // never materialised: view cell (i, j) maps to world top_left - f*j + r*i (f = DIR_TO_VEC[dir],
@@ -101,9 +104,10 @@ __device__ __forceinline__ void view_box(int ax, int ay, int d, int vs, int &tlx
 // of pickup / drop / toggle is returned (mut, nt/nc/ns) instead of written, so the caller orders it
 // against the window it stages.
 struct StepOut {
-    int x, y, d, sc, ct, cc, stat, term, trunc, mut, fi, nt, nc, ns;
+    int x, y, d, sc, ct, cc, stat, term, trunc, mut, fi, nt, nc, ns, op;  // op: kOp* (front-cell action)
     double r;
 };
+enum { kOpNone = 0, kOpPickup = 1, kOpDrop = 2, kOpToggleBox = 3 };
 
 // Rd: cell reader, rd(x, y) -> (type, colour, state) of in-grid cell (x, y) of this env.
 template <typename Rd>
@@ -112,7 +116,7 @@ __device__ __forceinline__ StepOut step_core(const EnvGeo &g, const Rd &rd, int 
     // Branch-free over the action (a wave steps envs with different actions): every effect is
     // computed and selected.  step_count += 1 first (:523); an out-of-grid front cell fails before
     // the action branch (Grid.get assert, :533), an unknown action after it (:579-580).
-    StepOut o{x, y, d, sc + 1, ct, cc, MGDP_OK, 0, 0, 0, 0, 0, 0, 0, 0.0};
+    StepOut o{x, y, d, sc + 1, ct, cc, MGDP_OK, 0, 0, 0, 0, 0, 0, 0, kOpNone, 0.0};
     const int fx = x + kDX[d], fy = y + kDY[d];
     const bool inb = (unsigned)fx < (unsigned)g.W && (unsigned)fy < (unsigned)g.H;
     const bool act_ok = (unsigned)a <= 6u;
@@ -139,11 +143,13 @@ __device__ __forceinline__ StepOut step_core(const EnvGeo &g, const Rd &rd, int 
     // drop (:564-568): front empty, carrying
     const bool drop = ok && a == 4 && fnone && ct != 0;
     // toggle (:571-575): Door.toggle (locked: needs the carried Key of its colour, unlocks and
-    // opens; else flips is_open, world_object.py:185-195); Box(contains=None).toggle -> empty
+    // opens; else flips is_open, world_object.py:185-195); Box.toggle -> its contents (:291-294):
+    // empty here, the caller puts a held object from the contents plane in its place
     const bool tdoor = ok && a == 5 && ft == T_DOOR && (fs != D_LOCKED || (ct == T_KEY && cc == fc));
     const bool tbox = ok && a == 5 && ft == T_BOX;
     const bool clear = pickup || tbox;
     o.mut = clear || drop || tdoor;
+    o.op = pickup ? kOpPickup : drop ? kOpDrop : tbox ? kOpToggleBox : kOpNone;
     o.fi = fi;
     o.nt = clear ? T_EMPTY : drop ? ct : ft;
     o.nc = clear ? 0 : drop ? cc : fc;
@@ -234,7 +240,7 @@ __device__ __forceinline__ unsigned long long group_or(unsigned long long v) {
 template <int VS, int G>
 __global__ void __launch_bounds__(kGroupBlock)
 envs_step_kernel(EnvGeo g, uint8_t *__restrict__ CELL, int32_t *__restrict__ agent, int32_t *__restrict__ carry,
-                 const int32_t *__restrict__ max_steps, const uint8_t *__restrict__ see,
+                 uint8_t *__restrict__ cont, uint8_t *__restrict__ ccont, const int32_t *__restrict__ max_steps, const uint8_t *__restrict__ see,
                  const int32_t *__restrict__ actions, uint8_t *__restrict__ obs,
                  int32_t *__restrict__ direction, double *__restrict__ reward,
                  uint8_t *__restrict__ terminated, uint8_t *__restrict__ truncated,
@@ -303,7 +309,7 @@ envs_step_kernel(EnvGeo g, uint8_t *__restrict__ CELL, int32_t *__restrict__ age
             }
         }
         asm volatile("" ::: "memory");  // the group's rows are written before any lane reads them
-        StepOut o{ag.x, ag.y, ag.z, ag.w, cr.x, cr.y, MGDP_OK, 0, 0, 0, 0, 0, 0, 0, 0.0};
+        StepOut o{ag.x, ag.y, ag.z, ag.w, cr.x, cr.y, MGDP_OK, 0, 0, 0, 0, 0, 0, 0, kOpNone, 0.0};
         if (!observe_only) {
             // cells outside the staged box are only asked for by turns (whose result ignores them)
             const auto rd = [&](int cx, int cy, int &t, int &c, int &s) {
@@ -319,7 +325,21 @@ envs_step_kernel(EnvGeo g, uint8_t *__restrict__ CELL, int32_t *__restrict__ age
             asm volatile("" ::: "memory");
             if (o.mut && r == 0) {  // the front cell as the step left it (in the view: the agent did not move)
                 const int fy = o.fi / g.W, fx = o.fi - fy * g.W;
-                const uint8_t code = (uint8_t)cell_code(o.nt, o.nc, o.ns);
+                uint8_t code = (uint8_t)cell_code(o.nt, o.nc, o.ns);
+                if (cont) {  // contents plane present (a uniform test): what Boxes hold moves with them
+                    uint8_t *cf = cont + (long long)e * g.HWp + o.fi;
+                    if (o.op == kOpToggleBox) {  // the box is replaced by what it held (None: empty)
+                        const uint8_t held = *cf;
+                        code = held ? held : code;
+                        *cf = 0;
+                    } else if (o.op == kOpPickup) {  // a carried Box keeps its contents
+                        ccont[e] = *cf;
+                        *cf = 0;
+                    } else if (o.op == kOpDrop) {
+                        *cf = ccont[e];
+                        ccont[e] = 0;
+                    }
+                }
                 wb[(fy - by) * RB + (fx - bx)] = code;
                 cell[o.fi] = code;
             }
@@ -388,6 +408,7 @@ struct mgdp_envs {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     uint8_t *d_cell = nullptr, *d_see = nullptr;  // d_cell: one-byte cell codes [B][HWp]
+    uint8_t *d_cont = nullptr, *d_ccont = nullptr;  // Box contents planes (mgdp_envs_set_contents), else null
     int32_t *d_agent = nullptr, *d_carry = nullptr, *d_max = nullptr, *d_act = nullptr, *d_dir = nullptr,
             *d_status = nullptr;
     uint8_t *d_obs = nullptr, *d_term = nullptr, *d_trunc = nullptr;
@@ -447,7 +468,7 @@ int launch_step(mgdp_envs *E, const int32_t *d_act, uint8_t *d_obs, int32_t *d_d
         tb = p.second;
     }
     hipExtLaunchKernelGGL(k, dim3(grid), dim3(kGroupBlock), smem, E->stream, ta, tb, 0, env_geo(E), E->d_cell, E->d_agent,
-                       E->d_carry, E->d_max, E->d_see, d_act, d_obs, d_dir, d_rew, d_term, d_trunc, d_status,
+                       E->d_carry, E->d_cont, E->d_ccont, E->d_max, E->d_see, d_act, d_obs, d_dir, d_rew, d_term, d_trunc, d_status,
                        observe_only);
     MGDP_HIP(hipGetLastError());
     return 0;
@@ -507,7 +528,7 @@ int mgdp_envs_destroy(mgdp_envs *E) {
     DeviceGuard guard(E->device);
     if (E->stream) (void)hipStreamSynchronize(E->stream);
     void *ps[] = {E->d_cell, E->d_see, E->d_agent, E->d_carry, E->d_max, E->d_act,
-                  E->d_dir, E->d_status, E->d_obs, E->d_term, E->d_trunc, E->d_rew};
+                  E->d_dir, E->d_status, E->d_obs, E->d_term, E->d_trunc, E->d_rew, E->d_cont, E->d_ccont};
     for (void *p : ps) (void)hipFree(p);
     for (auto &p : E->ev) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
     for (auto &p : E->ev_pool) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
@@ -566,6 +587,13 @@ int mgdp_envs_load(mgdp_envs *E, const uint8_t *enc, const int32_t *agent, const
     }
     std::vector<int32_t> ms(max_steps, max_steps + B);
     std::vector<uint8_t> se(see_through, see_through + B);
+    if (E->d_cont) {  // new grids hold no contents until mgdp_envs_set_contents says so
+        for (int b = 0; b < B; ++b) {
+            if (mask && !mask[b]) continue;
+            MGDP_HIP(hipMemsetAsync(E->d_cont + (size_t)b * HWp, 0, HWp, E->stream));
+            MGDP_HIP(hipMemsetAsync(E->d_ccont + b, 0, 1, E->stream));
+        }
+    }
     if (!mask) {
         MGDP_HIP(hipMemcpyAsync(E->d_cell, cl.data(), cl.size(), hipMemcpyHostToDevice, E->stream));
         MGDP_HIP(hipMemcpyAsync(E->d_agent, ag.data(), ag.size() * 4, hipMemcpyHostToDevice, E->stream));
@@ -700,11 +728,110 @@ int mgdp_envs_set_state(mgdp_envs *E, const int32_t *agent, const int32_t *carry
             ag[4 * b] = agent[3 * b]; ag[4 * b + 1] = agent[3 * b + 1]; ag[4 * b + 2] = agent[3 * b + 2];
         }
         if (step_count) ag[4 * b + 3] = step_count[b];
-        if (carry) { cr[2 * b] = carry[2 * b]; cr[2 * b + 1] = carry[2 * b + 1]; }
+        if (carry) {
+            cr[2 * b] = carry[2 * b]; cr[2 * b + 1] = carry[2 * b + 1];
+            if (E->d_ccont) MGDP_HIP(hipMemsetAsync(E->d_ccont + b, 0, 1, E->stream));  // see mgdp_envs_set_contents
+        }
     }
     MGDP_HIP(hipMemcpyAsync(E->d_agent, ag.data(), ag.size() * 4, hipMemcpyHostToDevice, E->stream));
     MGDP_HIP(hipMemcpyAsync(E->d_carry, cr.data(), cr.size() * 4, hipMemcpyHostToDevice, E->stream));
     MGDP_HIP(hipStreamSynchronize(E->stream));
+    return 0;
+}
+
+// Box(contains=...) (world_object.py:272-294): toggle puts the held object in the box's cell,
+// pickup carries the box with it, drop puts it back.  Contents are (type, colour, state) triples in
+// Grid.encode() layout, type <= 1 (unseen / empty) = nothing held; each must be a cell code (see
+// cell_code) and sit on a Box cell of the current grid; a carried one needs a carried Box.
+int mgdp_envs_set_contents(mgdp_envs *E, const uint8_t *contents, const int32_t *carry_contents) {
+    MGDP_CHECK(E, MGDP_E_INVALID, "null handle");
+    DeviceGuard guard(E->device);
+    const int B = E->B, W = E->W, H = E->H, HWp = E->HWp;
+    std::vector<uint8_t> cl((size_t)B * HWp);
+    std::vector<int32_t> cr((size_t)B * 2);
+    MGDP_HIP(hipMemcpyAsync(cl.data(), E->d_cell, cl.size(), hipMemcpyDeviceToHost, E->stream));
+    MGDP_HIP(hipMemcpyAsync(cr.data(), E->d_carry, cr.size() * 4, hipMemcpyDeviceToHost, E->stream));
+    MGDP_HIP(hipStreamSynchronize(E->stream));
+    auto code_of = [](int t, int c, int s, uint8_t &out) -> bool {  // a held object's cell code
+        if (t <= T_EMPTY) { out = 0; return true; }
+        if (t == T_AGENT || c > 5 || (t == T_DOOR ? s > D_LOCKED : s != 0)) return false;
+        out = (uint8_t)cell_code(t, c, s);
+        return true;
+    };
+    std::vector<uint8_t> co, cc;
+    if (contents) {
+        co.assign((size_t)B * HWp, 0);
+        for (int b = 0; b < B; ++b)
+            for (int x = 0; x < W; ++x)
+                for (int y = 0; y < H; ++y) {
+                    const uint8_t *c = contents + ((size_t)b * W * H + x * H + y) * 3;
+                    uint8_t code;
+                    MGDP_CHECK(code_of(c[0], c[1], c[2], code), MGDP_E_INVALID,
+                               "env %d cell (%d,%d): contents (%d,%d,%d) is not an object encoding", b, x, y, c[0], c[1], c[2]);
+                    const size_t i = (size_t)b * HWp + y * W + x;
+                    int t, col, st;
+                    cell_decode(cl[i], t, col, st);
+                    MGDP_CHECK(code == 0 || t == T_BOX, MGDP_E_INVALID, "env %d cell (%d,%d): contents on a non-box cell", b, x, y);
+                    co[i] = code;
+                }
+    }
+    if (carry_contents) {
+        cc.assign((size_t)B, 0);
+        for (int b = 0; b < B; ++b) {
+            const int32_t *c = carry_contents + 3 * b;
+            uint8_t code;
+            MGDP_CHECK(c[0] >= 0 && c[1] >= 0 && c[2] >= 0 && code_of(c[0], c[1], c[2], code), MGDP_E_INVALID,
+                       "env %d: carried contents (%d,%d,%d) is not an object encoding", b, c[0], c[1], c[2]);
+            MGDP_CHECK(code == 0 || cr[2 * b] == T_BOX, MGDP_E_INVALID, "env %d: contents for a carried non-box", b);
+            cc[b] = code;
+        }
+    }
+    if (!E->d_cont) {
+        hipError_t e = hipMalloc((void **)&E->d_cont, (size_t)B * HWp);
+        if (e == hipSuccess) e = hipMalloc((void **)&E->d_ccont, (size_t)B);
+        if (e == hipSuccess) e = hipMemsetAsync(E->d_cont, 0, (size_t)B * HWp, E->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(E->d_ccont, 0, (size_t)B, E->stream);
+        if (e != hipSuccess) {
+            (void)hipFree(E->d_cont);
+            (void)hipFree(E->d_ccont);
+            E->d_cont = E->d_ccont = nullptr;
+            return hip_fail(e, "mgdp_envs_set_contents allocation", __FILE__, __LINE__);
+        }
+    }
+    if (contents) MGDP_HIP(hipMemcpyAsync(E->d_cont, co.data(), co.size(), hipMemcpyHostToDevice, E->stream));
+    if (carry_contents) MGDP_HIP(hipMemcpyAsync(E->d_ccont, cc.data(), cc.size(), hipMemcpyHostToDevice, E->stream));
+    MGDP_HIP(hipStreamSynchronize(E->stream));
+    return 0;
+}
+
+int mgdp_envs_get_contents(mgdp_envs *E, uint8_t *contents, int32_t *carry_contents) {
+    MGDP_CHECK(E, MGDP_E_INVALID, "null handle");
+    DeviceGuard guard(E->device);
+    const int B = E->B, W = E->W, H = E->H, HWp = E->HWp;
+    std::vector<uint8_t> co((size_t)B * HWp, 0), cc((size_t)B, 0);
+    if (E->d_cont) {
+        MGDP_HIP(hipMemcpyAsync(co.data(), E->d_cont, co.size(), hipMemcpyDeviceToHost, E->stream));
+        MGDP_HIP(hipMemcpyAsync(cc.data(), E->d_ccont, cc.size(), hipMemcpyDeviceToHost, E->stream));
+        MGDP_HIP(hipStreamSynchronize(E->stream));
+    }
+    auto put = [](uint8_t code, int &t, int &c, int &s) {
+        if (code == 0) { t = c = s = 0; return; }
+        cell_decode(code, t, c, s);
+    };
+    for (int b = 0; b < B; ++b) {
+        int t, c, s;
+        if (contents)
+            for (int x = 0; x < W; ++x)
+                for (int y = 0; y < H; ++y) {
+                    put(co[(size_t)b * HWp + y * W + x], t, c, s);
+                    uint8_t *o = contents + ((size_t)b * W * H + x * H + y) * 3;
+                    o[0] = (uint8_t)t; o[1] = (uint8_t)c; o[2] = (uint8_t)s;
+                }
+        if (carry_contents) {
+            put(cc[b], t, c, s);
+            carry_contents[3 * b] = t; carry_contents[3 * b + 1] = c; carry_contents[3 * b + 2] = s;
+        }
+    }
     return 0;
 }
 

@@ -64,6 +64,7 @@ class _DeviceEnv:
         self.trunc = np.zeros(1, np.uint8)
         self.status = np.zeros(1, np.int32)
         self.act = np.zeros(1, np.int32)
+        self.held = False  # Box contents planes in use on the device
 
     def __del__(self):
         try:
@@ -144,6 +145,11 @@ class MiniGridEnv(Env):
         self._host_stale = False
         owner, self._grid._owner = self._grid._owner, None
         self._grid.load_encoding(enc[0])
+        held = np.zeros((1, self.width, self.height, 3), np.uint8)
+        carry_held = np.zeros((1, 3), np.int32)
+        if d.held:
+            _lib.check(d.L.mgdp_envs_get_contents(d.h, _lib.ptr(held), _lib.ptr(carry_held)), "mgdp_envs_get_contents")
+            self._grid.load_held(held[0])
         self._grid._owner = owner
         self._agent_pos = (int(agent[0, 0]), int(agent[0, 1]))
         self._agent_dir = int(agent[0, 2])
@@ -153,6 +159,8 @@ class MiniGridEnv(Env):
             if c is None or c.encode()[:2] != (int(carry[0, 0]), int(carry[0, 1])):
                 c = WorldObj.decode(int(carry[0, 0]), int(carry[0, 1]), 0)
                 c.cur_pos = np.array([-1, -1])
+            if d.held and c.type == "box":  # what the carried Box holds
+                c.contains = WorldObj.decode(*carry_held[0]) if carry_held[0, 0] > OBJECT_TO_IDX["empty"] else None
             self._carrying = c
         else:
             self._carrying = None
@@ -182,6 +190,17 @@ class MiniGridEnv(Env):
             carry[0] = (t, c)
         sc = np.array([self._step_count], np.int32)
         _lib.check(d.L.mgdp_envs_set_state(d.h, None, _lib.ptr(carry), _lib.ptr(sc), None), "mgdp_envs_set_state")
+        held = self._grid.encode_held()
+        carry_held = np.zeros((1, 3), np.int32)
+        inner = getattr(self._carrying, "contains", None) if self._carrying is not None else None
+        if inner is not None:
+            if self._carrying.type != "box" or getattr(inner, "contains", None) is not None:
+                raise NotImplementedError("only a Box holds an object, and a held Box holds nothing")
+            carry_held[0] = inner.encode()
+        if d.held or held.any() or carry_held.any():  # Box(contains=...) in play: the contents planes
+            _lib.check(d.L.mgdp_envs_set_contents(d.h, _lib.ptr(np.ascontiguousarray(held[None])), _lib.ptr(carry_held)),
+                       "mgdp_envs_set_contents")
+            d.held = True
         self._push_pending = False
 
     def _sync_to_device(self):

@@ -62,6 +62,7 @@ class MiniGridVecEnv:
         self._status = np.zeros(B, np.int32)
         self._seeds = np.zeros(B, np.int64)
         self._next_seed = 0
+        self._held = False  # Box contents planes in use (set_contents)
 
     def close(self):
         if getattr(self, "h", None):
@@ -75,8 +76,9 @@ class MiniGridVecEnv:
             pass
 
     # ---------------------------------------------------------------- raw state upload
-    def load(self, enc: np.ndarray, agent: np.ndarray, max_steps=None, see_through=None, mask=None):
-        """Upload grids (B, W, H, 3) x-major encodings and agents (B, 3) = (x, y, dir)."""
+    def load(self, enc: np.ndarray, agent: np.ndarray, max_steps=None, see_through=None, mask=None, held=None):
+        """Upload grids (B, W, H, 3) x-major encodings and agents (B, 3) = (x, y, dir).  held: what
+        each Box cell holds (Box(contains=...)), the same layout, type 0 = nothing (set_contents)."""
         B = self.num_envs
         enc = np.ascontiguousarray(enc, np.uint8)
         agent = np.ascontiguousarray(agent, np.int32)
@@ -90,6 +92,34 @@ class MiniGridVecEnv:
         m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
         _lib.check(self.L.mgdp_envs_load(self.h, _lib.ptr(enc), _lib.ptr(agent), _lib.ptr(ms), _lib.ptr(see),
                                          _lib.ptr(m)), "mgdp_envs_load")
+        if held is not None:
+            if mask is not None:  # the other envs keep theirs
+                cur = self.get_contents()[0]
+                sel = np.asarray(mask, bool)
+                cur[sel] = np.asarray(held, np.uint8)[sel]
+                held = cur
+            self.set_contents(held)
+
+    def set_contents(self, held=None, carry_held=None):
+        """Box(contains=...) (world_object.py:272-294): held (B, W, H, 3) = the (type, colour, state)
+        each Box cell holds, carry_held (B, 3) = what a carried Box holds (None = unchanged).  Toggling
+        a Box then puts its object in the cell, and a carried Box keeps it (mgdp_envs_set_contents)."""
+        B = self.num_envs
+        h = None if held is None else np.ascontiguousarray(held, np.uint8)
+        c = None if carry_held is None else np.ascontiguousarray(carry_held, np.int32)
+        assert h is None or h.shape == (B, self.W, self.H, 3)
+        assert c is None or c.shape == (B, 3)
+        _lib.check(self.L.mgdp_envs_set_contents(self.h, _lib.ptr(h), _lib.ptr(c)), "mgdp_envs_set_contents")
+        self._held = True
+
+    def get_contents(self):
+        """(held (B, W, H, 3), carry_held (B, 3)): what the Boxes hold now (zeros: nothing)."""
+        B = self.num_envs
+        held = np.zeros((B, self.W, self.H, 3), np.uint8)
+        carry_held = np.zeros((B, 3), np.int32)
+        _lib.check(self.L.mgdp_envs_get_contents(self.h, _lib.ptr(held), _lib.ptr(carry_held)),
+                   "mgdp_envs_get_contents")
+        return held, carry_held
 
     def _generate(self, seeds):
         seeds = np.asarray(seeds, np.int64)
@@ -182,4 +212,7 @@ class MiniGridVecEnv:
         sc = np.zeros(B, np.int32)
         _lib.check(self.L.mgdp_envs_get_state(self.h, _lib.ptr(enc), _lib.ptr(agent), _lib.ptr(carry), _lib.ptr(sc)),
                    "mgdp_envs_get_state")
-        return {"enc": enc, "agent": agent, "carry": carry, "step_count": sc}
+        st = {"enc": enc, "agent": agent, "carry": carry, "step_count": sc}
+        if self._held:
+            st["held"], st["carry_held"] = self.get_contents()
+        return st

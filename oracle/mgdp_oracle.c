@@ -16,7 +16,7 @@
  *                                                                        :114,129,142,165,178-195,244,266,278-294
  *   orc_vi                            Jacobi value iteration (build-defined, DESIGN.md "A9"; the
  *                                     reference has no DP code -- SURVEY.md section 0)
- *   orc_step / orc_gen_obs            step() + gen_obs()                 minigrid/minigrid_env.py:520-645,
+ *   orc_step(_held) / orc_gen_obs     step() + gen_obs()                 minigrid/minigrid_env.py:520-645,
  *                                       Grid.slice/rotate_left/encode/process_vis
  *                                                                        minigrid/core/grid.py:110-143,244-328
  *   orc_reward                        _reward()                         minigrid/minigrid_env.py:235-240
@@ -509,12 +509,15 @@ double orc_reward(int step_count, int max_steps) {
 
 /* MiniGridEnv.step, minigrid_env.py:520-590.  Mutates the planes / agent / carry in place.
  * state[4] = {x, y, dir, step_count}; carry[2] = {type, color} (type 0 = nothing).
- * Box contents are not modelled: toggling a Box leaves an empty cell (Box(contains=None)).
+ * held (may be NULL): Box(contains=...) (world_object.py:272-294) as three more planes, the
+ * (type, colour, state) of the object each Box cell holds (type 0 = nothing), and hc[3] the same
+ * for a carried Box: pickup carries a Box with its contents (:556-561 keeps the object), drop puts
+ * them back (:564-568), Box.toggle puts the held object in the cell (:291-294; None: empty).
  * Returns 0, or -1 for an unknown action (after step_count += 1, as the reference does), or -2
  * when the front cell is outside the grid (the reference's Grid.get assertion). */
-int orc_step(int W, int H, uint8_t *ty, uint8_t *co, uint8_t *st, int32_t *state, int32_t *carry,
-             int max_steps, int see_through, int vs, int action, uint8_t *image, double *reward,
-             int *terminated, int *truncated) {
+int orc_step_held(int W, int H, uint8_t *ty, uint8_t *co, uint8_t *st, uint8_t *hty, uint8_t *hco, uint8_t *hst,
+                  int32_t *hc, int32_t *state, int32_t *carry, int max_steps, int see_through, int vs, int action,
+                  uint8_t *image, double *reward, int *terminated, int *truncated) {
     int ax = state[0], ay = state[1], d = state[2];
     state[3] += 1;
     *reward = 0.0;
@@ -540,12 +543,20 @@ int orc_step(int W, int H, uint8_t *ty, uint8_t *co, uint8_t *st, int32_t *state
             if (carry[0] == 0) {
                 carry[0] = ft; carry[1] = co[fi];
                 ty[fi] = T_EMPTY; co[fi] = 0; st[fi] = 0;
+                if (hty) {
+                    hc[0] = hty[fi]; hc[1] = hco[fi]; hc[2] = hst[fi];
+                    hty[fi] = 0; hco[fi] = 0; hst[fi] = 0;
+                }
             }
         }
     } else if (action == 4) {
         if (fnone && carry[0] != 0) {
             ty[fi] = (uint8_t)carry[0]; co[fi] = (uint8_t)carry[1]; st[fi] = 0;
             carry[0] = 0; carry[1] = 0;
+            if (hty) {
+                hty[fi] = (uint8_t)hc[0]; hco[fi] = (uint8_t)hc[1]; hst[fi] = (uint8_t)hc[2];
+                hc[0] = 0; hc[1] = 0; hc[2] = 0;
+            }
         }
     } else if (action == 5) {
         if (ft == T_DOOR) {
@@ -555,7 +566,12 @@ int orc_step(int W, int H, uint8_t *ty, uint8_t *co, uint8_t *st, int32_t *state
                 st[fi] = st[fi] == D_OPEN ? D_CLOSED : D_OPEN;
             }
         } else if (ft == T_BOX) {
-            ty[fi] = T_EMPTY; co[fi] = 0; st[fi] = 0;
+            if (hty && hty[fi] > T_EMPTY) {
+                ty[fi] = hty[fi]; co[fi] = hco[fi]; st[fi] = hst[fi];
+            } else {
+                ty[fi] = T_EMPTY; co[fi] = 0; st[fi] = 0;
+            }
+            if (hty) { hty[fi] = 0; hco[fi] = 0; hst[fi] = 0; }
         }
     }
     if (state[3] >= max_steps) *truncated = 1;
@@ -563,22 +579,40 @@ int orc_step(int W, int H, uint8_t *ty, uint8_t *co, uint8_t *st, int32_t *state
     return 0;
 }
 
+/* orc_step_held without Box contents (every Box holds nothing). */
+int orc_step(int W, int H, uint8_t *ty, uint8_t *co, uint8_t *st, int32_t *state, int32_t *carry,
+             int max_steps, int see_through, int vs, int action, uint8_t *image, double *reward,
+             int *terminated, int *truncated) {
+    return orc_step_held(W, H, ty, co, st, NULL, NULL, NULL, NULL, state, carry, max_steps, see_through, vs, action,
+                         image, reward, terminated, truncated);
+}
+
 /* B envs stepped once each (the CPU baseline of the batched step path; same per-env semantics as
  * orc_step above, i.e. MiniGridEnv.step minigrid_env.py:520-590).  Planes are [B][HWp] row-major,
  * state [B][4], carry [B][2], obs [B][vs*vs*3]; status[b] is orc_step's return code.
  * nthreads > 1 splits the envs over OpenMP threads. */
-void orc_step_batch(int B, int W, int H, int HWp, uint8_t *ty, uint8_t *co, uint8_t *st, int32_t *state,
-                    int32_t *carry, const int32_t *max_steps, const uint8_t *see, int vs, const int32_t *actions,
-                    uint8_t *obs, double *reward, uint8_t *terminated, uint8_t *truncated, int32_t *status,
-                    int nthreads) {
+void orc_step_batch_held(int B, int W, int H, int HWp, uint8_t *ty, uint8_t *co, uint8_t *st, uint8_t *hty,
+                         uint8_t *hco, uint8_t *hst, int32_t *hc, int32_t *state, int32_t *carry,
+                         const int32_t *max_steps, const uint8_t *see, int vs, const int32_t *actions, uint8_t *obs,
+                         double *reward, uint8_t *terminated, uint8_t *truncated, int32_t *status, int nthreads) {
     const int ob = vs * vs * 3;
 #pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
     for (int b = 0; b < B; ++b) {
         int te = 0, tr = 0;
         const size_t o = (size_t)b * HWp;
-        status[b] = orc_step(W, H, ty + o, co + o, st + o, state + 4 * b, carry + 2 * b, max_steps[b], see[b], vs,
-                             actions[b], obs + (size_t)b * ob, reward + b, &te, &tr);
+        status[b] = orc_step_held(W, H, ty + o, co + o, st + o, hty ? hty + o : NULL, hty ? hco + o : NULL,
+                                  hty ? hst + o : NULL, hty ? hc + 3 * b : NULL, state + 4 * b, carry + 2 * b,
+                                  max_steps[b], see[b], vs, actions[b], obs + (size_t)b * ob, reward + b, &te, &tr);
         terminated[b] = (uint8_t)te;
         truncated[b] = (uint8_t)tr;
     }
+}
+
+/* orc_step_batch_held without Box contents. */
+void orc_step_batch(int B, int W, int H, int HWp, uint8_t *ty, uint8_t *co, uint8_t *st, int32_t *state,
+                    int32_t *carry, const int32_t *max_steps, const uint8_t *see, int vs, const int32_t *actions,
+                    uint8_t *obs, double *reward, uint8_t *terminated, uint8_t *truncated, int32_t *status,
+                    int nthreads) {
+    orc_step_batch_held(B, W, H, HWp, ty, co, st, NULL, NULL, NULL, NULL, state, carry, max_steps, see, vs, actions,
+                        obs, reward, terminated, truncated, status, nthreads);
 }

@@ -44,6 +44,10 @@ def lib():
         L.orc_reward.argtypes = [_I, _I]
         L.orc_step_batch.argtypes = [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _I]
         L.orc_step_batch.restype = None
+        L.orc_step_held.argtypes = [_I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]
+        L.orc_step_batch_held.argtypes = [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P,
+                                          _P, _P, _P, _P, _I]
+        L.orc_step_batch_held.restype = None
         L.orc_reward.restype = _D
         _lib = L
     return _lib
@@ -142,15 +146,24 @@ class OracleBatch:
     """B envs in the GPU engine's layout (row-major planes [B][HWp], agent [B][4]) stepped by the
     oracle's MiniGridEnv.step restatement (orc_step_batch); the step path's CPU baseline."""
 
-    def __init__(self, enc: np.ndarray, agent: np.ndarray, max_steps, see_through, view=7):
+    def __init__(self, enc: np.ndarray, agent: np.ndarray, max_steps, see_through, view=7, held=None):
+        """held: optional (B, W, H, 3) encodings of what each Box cell holds (type 0 = nothing)."""
         enc = np.asarray(enc, np.uint8)  # (B, W, H, 3) x-major encodings
         B, W, H, _ = enc.shape
         self.B, self.W, self.H, self.view = B, W, H, view
         self.HWp = (W * H + 15) // 16 * 16
-        planes = np.zeros((3, B, self.HWp), np.uint8)
-        for p in range(3):
-            planes[p, :, : W * H] = enc[..., p].transpose(0, 2, 1).reshape(B, W * H)
-        self.ty, self.co, self.st = (np.ascontiguousarray(planes[p]) for p in range(3))
+
+        def planes_of(e):
+            planes = np.zeros((3, B, self.HWp), np.uint8)
+            for p in range(3):
+                planes[p, :, : W * H] = e[..., p].transpose(0, 2, 1).reshape(B, W * H)
+            return tuple(np.ascontiguousarray(planes[p]) for p in range(3))
+
+        self.ty, self.co, self.st = planes_of(enc)
+        self.hty = self.hco = self.hst = None
+        self.held_carry = np.zeros((B, 3), np.int32)
+        if held is not None:
+            self.hty, self.hco, self.hst = planes_of(np.asarray(held, np.uint8))
         self.state = np.zeros((B, 4), np.int32)
         self.state[:, :3] = np.asarray(agent, np.int32)[:, :3]
         self.carry = np.zeros((B, 2), np.int32)
@@ -164,22 +177,43 @@ class OracleBatch:
 
     def step(self, actions: np.ndarray, nthreads: int = 1):
         a = np.ascontiguousarray(actions, np.int32)
+        if self.hty is not None:
+            lib().orc_step_batch_held(self.B, self.W, self.H, self.HWp, _ptr(self.ty), _ptr(self.co), _ptr(self.st),
+                                      _ptr(self.hty), _ptr(self.hco), _ptr(self.hst), _ptr(self.held_carry),
+                                      _ptr(self.state), _ptr(self.carry), _ptr(self.max_steps), _ptr(self.see),
+                                      self.view, _ptr(a), _ptr(self.obs), _ptr(self.reward), _ptr(self.terminated),
+                                      _ptr(self.truncated), _ptr(self.status), int(nthreads))
+            return
         lib().orc_step_batch(self.B, self.W, self.H, self.HWp, _ptr(self.ty), _ptr(self.co), _ptr(self.st),
                              _ptr(self.state), _ptr(self.carry), _ptr(self.max_steps), _ptr(self.see), self.view,
                              _ptr(a), _ptr(self.obs), _ptr(self.reward), _ptr(self.terminated),
                              _ptr(self.truncated), _ptr(self.status), int(nthreads))
 
+    def held_encoding(self) -> np.ndarray:
+        """(B, W, H, 3) x-major encodings of what each Box cell holds (zeros without held planes)."""
+        W, H = self.W, self.H
+        if self.hty is None:
+            return np.zeros((self.B, W, H, 3), np.uint8)
+        return np.stack([p[:, : W * H].reshape(self.B, H, W).transpose(0, 2, 1) for p in (self.hty, self.hco, self.hst)],
+                        axis=-1)
+
 
 class OracleEnv:
     """Single env stepped by the oracle's restatement of MiniGridEnv.step (mutable state)."""
 
-    def __init__(self, enc: np.ndarray, agent, max_steps: int, see_through: bool, view=7):
-        # enc is the reference's x-major (W, H, 3) encode; planes are row-major (H, W)
+    def __init__(self, enc: np.ndarray, agent, max_steps: int, see_through: bool, view=7, held=None):
+        # enc is the reference's x-major (W, H, 3) encode; planes are row-major (H, W).  held: the
+        # same layout for what each Box cell holds (Box(contains=...), type 0 = nothing), optional
         enc = np.asarray(enc, np.uint8)
         self.ty = np.ascontiguousarray(enc[:, :, 0].T)
         self.co = np.ascontiguousarray(enc[:, :, 1].T)
         self.st = np.ascontiguousarray(enc[:, :, 2].T)
         self.H, self.W = self.ty.shape
+        self.hty = self.hco = self.hst = None
+        self.held_carry = np.zeros(3, np.int32)
+        if held is not None:
+            held = np.asarray(held, np.uint8)
+            self.hty, self.hco, self.hst = (np.ascontiguousarray(held[:, :, p].T) for p in range(3))
         self.state = np.array([agent[0], agent[1], agent[2], 0], np.int32)
         self.carry = np.zeros(2, np.int32)
         self.max_steps = int(max_steps)
@@ -191,10 +225,16 @@ class OracleEnv:
         r = ctypes.c_double(0)
         te = ctypes.c_int(0)
         tr = ctypes.c_int(0)
-        rc = lib().orc_step(self.W, self.H, _ptr(self.ty), _ptr(self.co), _ptr(self.st),
-                            _ptr(self.state), _ptr(self.carry), self.max_steps,
-                            int(self.see_through), self.view, int(action), _ptr(img),
-                            ctypes.byref(r), ctypes.byref(te), ctypes.byref(tr))
+        if self.hty is not None:
+            rc = lib().orc_step_held(self.W, self.H, _ptr(self.ty), _ptr(self.co), _ptr(self.st), _ptr(self.hty),
+                                     _ptr(self.hco), _ptr(self.hst), _ptr(self.held_carry), _ptr(self.state),
+                                     _ptr(self.carry), self.max_steps, int(self.see_through), self.view, int(action),
+                                     _ptr(img), ctypes.byref(r), ctypes.byref(te), ctypes.byref(tr))
+        else:
+            rc = lib().orc_step(self.W, self.H, _ptr(self.ty), _ptr(self.co), _ptr(self.st),
+                                _ptr(self.state), _ptr(self.carry), self.max_steps,
+                                int(self.see_through), self.view, int(action), _ptr(img),
+                                ctypes.byref(r), ctypes.byref(te), ctypes.byref(tr))
         if rc == -1:
             raise ValueError(f"Unknown action: {action}")
         if rc != 0:
@@ -203,6 +243,11 @@ class OracleEnv:
 
     def encode(self) -> np.ndarray:
         return np.stack([self.ty.T, self.co.T, self.st.T], axis=-1)
+
+    def held_encoding(self) -> np.ndarray:
+        if self.hty is None:
+            return np.zeros((self.W, self.H, 3), np.uint8)
+        return np.stack([self.hty.T, self.hco.T, self.hst.T], axis=-1)
 
     def obs(self):
         return gen_obs((self.ty, self.co, self.st), self.state[:3], self.carry, self.see_through,

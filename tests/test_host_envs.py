@@ -107,15 +107,24 @@ def test_grid_api_round_trip():
         g.get(8, 0)
 
 
-def test_box_with_contents_is_refused():
-    # world_object.py:272-294: Box.toggle replaces the box by its contents, which the one-byte cell
-    # code cannot hold; an empty box is modelled (toggle -> empty cell)
-    import pytest
-
-    from minigrid_dynamicprogramming_amd.core import Ball, Box, Grid
+def test_grid_box_contents_on_the_host():
+    """Grid keeps what a Box holds (Box(contains=...), world_object.py:272-294) beside its planes:
+    encode() is unchanged (a Box encodes as (7, colour, 0)), get() returns the Box with its object,
+    copy() keeps it, and more than one level is refused."""
+    from minigrid_dynamicprogramming_amd.core import Ball, Box, Grid, Key
 
     g = Grid(5, 5)
-    g.set(2, 2, Box("red"))
-    assert g.get(2, 2).type == "box"
+    g.set(1, 2, Box("red", contains=Key("blue")))
+    b = g.get(1, 2)
+    assert b.type == "box" and b.contains.type == "key" and b.contains.color == "blue"
+    assert tuple(g.encode()[1, 2]) == (7, 0, 0)
+    assert tuple(g.encode_held()[1, 2]) == (5, 2, 0)
+    assert g.copy().get(1, 2).contains.type == "key"
+    g.set(1, 2, None)
+    assert not g.encode_held().any()
     with pytest.raises(NotImplementedError):
-        g.set(2, 3, Box("red", contains=Ball("blue")))
+        g.set(2, 2, Box("red", contains=Box("blue", contains=Ball("red"))))
+    with pytest.raises(NotImplementedError):
+        k = Key("red")
+        k.contains = Ball("blue")
+        g.set(3, 3, k)

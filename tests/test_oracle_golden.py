@@ -195,3 +195,62 @@ def test_numpy_restatement_matches_golden_and_oracle(name):
         assert r["sweeps"] == o["sweeps"]
         np.testing.assert_array_equal(r["V"], o["V"])
         np.testing.assert_array_equal(r["pi"], o["pi"])
+
+
+def _digest(a):
+    import hashlib
+
+    return np.frombuffer(hashlib.sha256(np.ascontiguousarray(a).tobytes()).digest()[:8], dtype=np.uint64)[0]
+
+
+def test_box_contents_trajectory_matches_reference():
+    """Box(contains=...) (world_object.py:272-294) through orc_step_held: a Box's held object
+    appears on toggle, travels with a carried Box and returns on drop -- every obs byte, reward,
+    flag, agent, carry, carried contents and the per-step digests of encode() and of the held
+    encoding equal the reference's 256-step rollouts (tests/golden/traj_box.npz, make_golden_box.py)."""
+    t = load("traj_box.npz")
+    for k in range(t["actions"].shape[0]):
+        env = oracle.OracleEnv(t["init_enc"][k], t["init_agent"][k], int(t["max_steps"][k]), False,
+                               held=t["init_held"][k])
+        np.testing.assert_array_equal(env.obs(), t["init_image"][k])
+        for i, a in enumerate(t["actions"][k]):
+            img, r, te, tr = env.step(int(a))
+            ctx = f"box traj {k} step {i} action {a}"
+            np.testing.assert_array_equal(img, t["image"][k, i], err_msg=ctx)
+            assert r == t["reward"][k, i] and te == bool(t["terminated"][k, i]) and tr == bool(t["truncated"][k, i]), ctx
+            assert tuple(env.state[:3]) == tuple(t["agent"][k, i]), ctx
+            assert tuple(env.carry) == tuple(t["carry"][k, i]), ctx
+            assert tuple(env.held_carry) == tuple(t["carry_held"][k, i]), ctx
+            assert _digest(env.encode()) == t["grid_digest"][k, i], ctx
+            assert _digest(env.held_encoding()) == t["held_digest"][k, i], ctx
+        np.testing.assert_array_equal(env.encode(), t["final_enc"][k])
+        np.testing.assert_array_equal(env.held_encoding(), t["final_held"][k])
+
+
+def test_box_contents_batched_oracle_matches_reference():
+    t = load("traj_box.npz")
+    ob = oracle.OracleBatch(t["init_enc"], t["init_agent"], t["max_steps"], False, held=t["init_held"])
+    for i in range(t["actions"].shape[1]):
+        ob.step(t["actions"][:, i])
+        ctx = f"box step {i}"
+        np.testing.assert_array_equal(ob.obs, t["image"][:, i], err_msg=ctx)
+        np.testing.assert_array_equal(ob.reward, t["reward"][:, i], err_msg=ctx)
+        np.testing.assert_array_equal(ob.carry, t["carry"][:, i], err_msg=ctx)
+        np.testing.assert_array_equal(ob.held_carry, t["carry_held"][:, i], err_msg=ctx)
+    np.testing.assert_array_equal(ob.held_encoding(), t["final_held"])
+
+
+def test_without_held_planes_a_box_opens_empty():
+    """The contents-free oracle (orc_step) is the reference with every Box holding nothing."""
+    enc = np.zeros((5, 5, 3), np.uint8)
+    enc[..., 0] = 1
+    enc[0, :, 0] = enc[-1, :, 0] = enc[:, 0, 0] = enc[:, -1, 0] = 2
+    enc[2, 1] = (7, 0, 0)  # a red box north of the agent
+    env = oracle.OracleEnv(enc, (2, 2, 3), 100, False)
+    env.step(5)
+    assert env.encode()[2, 1, 0] == 1
+    held = np.zeros_like(enc)
+    held[2, 1] = (5, 2, 0)  # a blue key in it
+    env = oracle.OracleEnv(enc, (2, 2, 3), 100, False, held=held)
+    env.step(5)
+    assert tuple(env.encode()[2, 1]) == (5, 2, 0) and not env.held_encoding().any()
