@@ -19,6 +19,7 @@ grep stamps $OUT/bench_$i.err | tail -1
 done
 [ -n "$SKIP_PROF" ] || timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/rocprof_default -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --no-hbm > $OUT/rocprof_bench.json 2> $OUT/rocprof.err || { echo "rocprof failed"; tail $OUT/rocprof.err; exit 1; }
 [ -n "$SKIP_PROF" ] || python -c "import json; d=json.load(open('$OUT/rocprof_bench.json')); r=d['roofline']; print('rocprof run', '%.4g'%d['value'], '%.3f us'%(d['ms_per_step']*1e3), 'launch us', r['avg_launch_us'], 'solves', r['solves_per_launch'])"
+[ -n "$SKIP_PROF" ] || python tools/rocprof_timed.py $OUT/rocprof_default/run_kernel_trace.csv $OUT/rocprof_bench.json $OUT/rocprof_timed_launch.json > /dev/null
 [ -n "$SKIP_TESTS" ] || timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
 [ -n "$SKIP_TESTS" ] || tail -1 $OUT/pytest.log
 echo "all ok"
