@@ -588,10 +588,15 @@ int mgdp_envs_load(mgdp_envs *E, const uint8_t *enc, const int32_t *agent, const
     std::vector<int32_t> ms(max_steps, max_steps + B);
     std::vector<uint8_t> se(see_through, see_through + B);
     if (E->d_cont) {  // new grids hold no contents until mgdp_envs_set_contents says so
-        for (int b = 0; b < B; ++b) {
-            if (mask && !mask[b]) continue;
-            MGDP_HIP(hipMemsetAsync(E->d_cont + (size_t)b * HWp, 0, HWp, E->stream));
-            MGDP_HIP(hipMemsetAsync(E->d_ccont + b, 0, 1, E->stream));
+        if (!mask) {
+            MGDP_HIP(hipMemsetAsync(E->d_cont, 0, (size_t)B * HWp, E->stream));
+            MGDP_HIP(hipMemsetAsync(E->d_ccont, 0, (size_t)B, E->stream));
+        } else {
+            for (int b = 0; b < B; ++b) {
+                if (!mask[b]) continue;
+                MGDP_HIP(hipMemsetAsync(E->d_cont + (size_t)b * HWp, 0, HWp, E->stream));
+                MGDP_HIP(hipMemsetAsync(E->d_ccont + b, 0, 1, E->stream));
+            }
         }
     }
     if (!mask) {
@@ -716,8 +721,10 @@ int mgdp_envs_set_state(mgdp_envs *E, const int32_t *agent, const int32_t *carry
     DeviceGuard guard(E->device);
     const int B = E->B;
     std::vector<int32_t> ag((size_t)B * 4), cr((size_t)B * 2);
+    std::vector<uint8_t> cc((carry && E->d_ccont) ? (size_t)B : 0);  // carried Box contents
     MGDP_HIP(hipMemcpyAsync(ag.data(), E->d_agent, ag.size() * 4, hipMemcpyDeviceToHost, E->stream));
     MGDP_HIP(hipMemcpyAsync(cr.data(), E->d_carry, cr.size() * 4, hipMemcpyDeviceToHost, E->stream));
+    if (!cc.empty()) MGDP_HIP(hipMemcpyAsync(cc.data(), E->d_ccont, cc.size(), hipMemcpyDeviceToHost, E->stream));
     MGDP_HIP(hipStreamSynchronize(E->stream));
     for (int b = 0; b < B; ++b) {
         if (mask && !mask[b]) continue;
@@ -730,11 +737,12 @@ int mgdp_envs_set_state(mgdp_envs *E, const int32_t *agent, const int32_t *carry
         if (step_count) ag[4 * b + 3] = step_count[b];
         if (carry) {
             cr[2 * b] = carry[2 * b]; cr[2 * b + 1] = carry[2 * b + 1];
-            if (E->d_ccont) MGDP_HIP(hipMemsetAsync(E->d_ccont + b, 0, 1, E->stream));  // see mgdp_envs_set_contents
+            if (!cc.empty()) cc[b] = 0;  // a new carry holds nothing (see mgdp_envs_set_contents)
         }
     }
     MGDP_HIP(hipMemcpyAsync(E->d_agent, ag.data(), ag.size() * 4, hipMemcpyHostToDevice, E->stream));
     MGDP_HIP(hipMemcpyAsync(E->d_carry, cr.data(), cr.size() * 4, hipMemcpyHostToDevice, E->stream));
+    if (!cc.empty()) MGDP_HIP(hipMemcpyAsync(E->d_ccont, cc.data(), cc.size(), hipMemcpyHostToDevice, E->stream));
     MGDP_HIP(hipStreamSynchronize(E->stream));
     return 0;
 }

@@ -150,4 +150,12 @@ def test_contents_are_validated():
     assert tuple(h[0, 2, 2]) == (5, 1, 0) and not ch.any()
     venv.load(enc, st["agent"])  # a load clears the contents of the loaded envs
     assert not venv.get_contents()[0].any()
+    carry = np.array([[7, 3], [0, 0]], np.int32)  # env 0 carries a purple Box
+    venv.L.mgdp_envs_set_state(venv.h, None, carry.ctypes.data, None, None)
+    with pytest.raises(ValueError):  # env 1 carries nothing: it cannot hold contents
+        venv.set_contents(carry_held=np.array([[5, 1, 0], [6, 2, 0]], np.int32))
+    venv.set_contents(carry_held=np.array([[5, 1, 0], [0, 0, 0]], np.int32))
+    assert tuple(venv.get_contents()[1][0]) == (5, 1, 0)
+    venv.L.mgdp_envs_set_state(venv.h, None, carry.ctypes.data, None, None)  # a new carry holds nothing
+    assert not venv.get_contents()[1].any()
     venv.close()
