@@ -126,9 +126,12 @@ def make_cells(spec, rank, world):
     return cells, (lo, hi)
 
 
-def cpu_baseline(cells, model, gamma, tol, dtype, budget_s=8.0, nthreads=1, lone=False):
+def cpu_baseline(cells, model, gamma, tol, dtype, budget_s=8.0, nthreads=1, lone=False, fixed_point=False):
     """Time the oracle (oracle/, a C restatement of the same algorithm) on a bounded sample.
-    lone: the workload solves its grids one at a time (each its own stopping sweep)."""
+    lone: the workload solves its grids one at a time (each its own stopping sweep).
+    fixed_point: orc_vi_fp, the literal loop with the GPU's per-grid fixed-point stop (a grid whose
+    sweep changed nothing is not swept again; same K, V, pi) -- the like-for-like CPU leg of a
+    batched config; updates are still counted as B*S*A*K, as the metric defines them."""
     import threading
 
     from oracle import oracle
@@ -152,7 +155,7 @@ def cpu_baseline(cells, model, gamma, tol, dtype, budget_s=8.0, nthreads=1, lone
         while True:
             g = sample[i % len(sample)][None] if lone else sample
             i += 1
-            r = oracle.value_iteration(model_id, g, gamma, tol, dtype=dtype, nthreads=per_call)
+            r = oracle.value_iteration(model_id, g, gamma, tol, dtype=dtype, nthreads=per_call, fixed_point=fixed_point)
             c[0] += len(g) * S * A * r["sweeps"]
             c[1] += 1
             c[2] = r["sweeps"]
@@ -173,9 +176,10 @@ def cpu_baseline(cells, model, gamma, tol, dtype, budget_s=8.0, nthreads=1, lone
     how = f", {loops} threads each solving its own replica" if replicated else ""
     what = (f"{solves} lone-grid solves cycling over {len(sample)} distinct grids" if lone else
             f"{solves} full solves of {len(sample)} grid(s)")
+    fn = "orc_vi_fp (per-grid fixed-point stop)" if fixed_point else "orc_vi (literal global loop)"
     return {"value": updates / el, "unit": "updates/s", "cores": nthreads, "kind": "port",
             "sample": f"{what} of the same workload ({counts[0][2]} sweeps in the last, {dtype}{how}), "
-                      f"oracle/mgdp_oracle.c, {el:.1f} s"}
+                      f"oracle/mgdp_oracle.c {fn}, {el:.1f} s"}
 
 
 def load_traffic(key, solves_per_launch, grids=None):
@@ -261,7 +265,11 @@ def workload_roofline(args, dtype, m, workload, grids):
     # solves inside the timed launches: the K timed solves plus the priming solves a resident
     # server's launch also spans
     solves_in_launches = args.steps + m["timed_primed"]  # the timed launches: relaunch priming + region
-    upd_per_solve = float(vi_info["updates_per_sweep"]) * float(np.mean(m["sweeps"]))
+    # algorithmic bytes of the work EXECUTED: with fixed-point completion a grid at an exact fixed
+    # point is not swept past its own stop, so the batched launches run mean_grid_sweeps per grid, not K
+    ex = m.get("executed")
+    swept = ex["mean_grid_sweeps"] if ex else float(np.mean(m["sweeps"]))
+    upd_per_solve = float(vi_info["updates_per_sweep"]) * float(swept)
     alg_bytes_launch = upd_per_solve * solves_in_launches * bpu / max(launches, 1)
     achieved = alg_bytes_launch / avg_launch_s / 1e9 if launches else 0.0
     comp_launch = compulsory_bytes_per_solve(vi_info, tsize, args.method, m["sweeps"][-1]) * solves_in_launches / max(launches, 1)
@@ -275,8 +283,9 @@ def workload_roofline(args, dtype, m, workload, grids):
         "solves_per_launch": solves_in_launches / max(launches, 1),
         "compulsory_bytes_per_launch": comp_launch,
         "compulsory_frac": comp_launch / max(avg_launch_s, 1e-30) / 1e9 / HBM_PEAK_GBS,
-        "note": ("achieved = SURVEY 8(d) algorithmic bytes (sizeof V + 1 + sizeof V / A per (s,a) update) per launch "
-                 "/ the launch's HIP-event duration; compulsory = the bytes this kernel must move per launch "
+        "basis": "executed updates (grid-sweeps run)" if ex else "B*S*A*K",
+        "note": ("achieved = SURVEY 8(d) algorithmic bytes (sizeof V + 1 + sizeof V / A per executed (s,a) update) "
+                 "per launch / the launch's HIP-event duration; compulsory = the bytes this kernel must move per launch "
                  "(fused/served: cells in + V and pi out once per solve, spread over the solve's launches; sweep: "
                  "2*S*sizeof V + W*H per grid-sweep); traffic = PMC HBM bytes per launch (profiles/pmc_traffic.json), "
                  "scaled to this rank's grids"),
@@ -288,7 +297,8 @@ def workload_roofline(args, dtype, m, workload, grids):
         lane_ops = sq["valu_insts_per_launch"] * scale * 64.0 / avg_launch_s
         roofline["valu"] = {"achieved": lane_ops, "peak": VALU_PEAK_LANE_OPS, "unit": "lane-ops/s",
                             "frac": lane_ops / VALU_PEAK_LANE_OPS, "lds_array_busy": sq.get("lds_array_busy"),
-                            "wave_split": sq.get("wave_split"), "source": sq.get("source")}
+                            "wave_split": sq.get("wave_split"), "source": sq.get("source"),
+                            "work": "executed VALU instructions (PMC SQ_INSTS_VALU), not B*S*A*K"}
     if workload == "empty16":
         roofline["regime"] = ("single 4 KiB V grid on one resident workgroup: latency bound (barrier + LDS round trip "
                               "per sweep, host hand-off per solve); HBM is not the limit here (SURVEY 8(d) "
@@ -377,6 +387,12 @@ def main():
     reducer_box = []
 
     def get_reducer():
+        # the library's own communicator (mgdp_vi_solve_sharded: RCCL called from libmgdp, one C call
+        # per solve) under RCCL; MGDP_BENCH_LIB_COMM=0 keeps the torch.distributed protocol
+        if not reducer_box and backend == "nccl" and os.environ.get("MGDP_BENCH_LIB_COMM", "1") != "0":
+            from minigrid_dynamicprogramming_amd.distributed import LibComm
+
+            reducer_box.append(LibComm(device=local))
         if not reducer_box:
             from minigrid_dynamicprogramming_amd.distributed import Reducer
 
@@ -423,6 +439,7 @@ def main():
                                                  "launch, so the timed region runs without them)")
                 if bm.get("executed"):
                     blk["executed_rank0"] = bm["executed"]
+                    blk["executed_updates_per_s"] = blk["value"] * bm["executed"]["frac_of_global_rule"]
                 if bm.get("collectives"):
                     blk["collectives"] = bm["collectives"]
                 if world == 1 and not args.no_cpu:
@@ -430,6 +447,12 @@ def main():
                     blk["cpu_baseline"] = cpu_baseline(bcells, model, args.gamma, args.tol, args.dtype, BLOCK_CPU_S)
                     blk["cpu_baseline_all_cores"] = cpu_baseline(bcells, model, args.gamma, args.tol, args.dtype,
                                                                  BLOCK_CPU_S, nthreads=host_cores())
+                    # like-for-like: the oracle with the same per-grid fixed-point stop as the GPU
+                    blk["cpu_baseline_fp"] = cpu_baseline(bcells, model, args.gamma, args.tol, args.dtype,
+                                                          BLOCK_CPU_S, fixed_point=True)
+                    blk["cpu_baseline_fp_all_cores"] = cpu_baseline(bcells, model, args.gamma, args.tol, args.dtype,
+                                                                    BLOCK_CPU_S, nthreads=host_cores(),
+                                                                    fixed_point=True)
                 (blocks if bspec["sharded"] else batched)[name] = blk
     # MGDP_BENCH_SPLIT_EVENTS=1 (rehearsal knob, tools/gpu_shard_prof.sh): the main line's region
     # without per-launch events too, as the blocks beside the headline run it
@@ -499,10 +522,82 @@ def main():
             nthreads=out["host"]["cores_used"], lone=lone)
         out["cpu_baseline_numpy"] = numpy_baseline(cells, vi_info["model"], args.gamma, args.tol, args.dtype,
                                                    max(2.0, args.cpu_budget / 4))
-    print(json.dumps(out), flush=True)
+    emit(out)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _g(x, n=4):
+    """x rounded to n significant digits (None passes)."""
+    return None if x is None else float(f"{x:.{n}g}")
+
+
+def compact_line(out: dict) -> dict:
+    """The stdout line: the contract's keys, a short roofline and CPU leg, and one summary per BASELINE
+    config measured beside the headline -- small enough (< 2000 chars) that a driver keeping only the
+    tail of stdout still holds all of it.  The full record goes to stderr / MGDP_BENCH_DETAIL."""
+    c = {k: out[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                             "higher_is_better", "scaling", "vs_baseline", "dtype") if k in out}
+    c["value"], c["ms_per_step"] = _g(out["value"], 6), _g(out["ms_per_step"], 5)
+    c["data"] = out["data"].split(" grids from")[0] + " grids, reference-exact generator"
+    cfg = out["config"]
+    c["config"] = {k: cfg[k] for k in ("workload", "env_id", "grids_per_gpu", "global_grids", "states_per_grid",
+                                       "actions", "gamma", "tol", "method", "parallelism") if k in cfg}
+    c["sweeps"] = out.get("sweeps")
+    r = out["roofline"]
+    c["roofline"] = {"bound": r["bound"], "kernel": r["kernel"], "achieved": _g(r["achieved"]), "peak": r["peak"],
+                     "unit": r["unit"], "frac": _g(r["frac"], 3), "traffic": _g(r.get("traffic")),
+                     "avg_launch_us": _g(r.get("avg_launch_us"), 5), "launches": r.get("launches"),
+                     "solves_per_launch": r.get("solves_per_launch")}
+    cb = out.get("cpu_baseline")
+    if cb:
+        c["cpu_baseline"] = {"value": _g(cb["value"]), "unit": cb["unit"], "cores": cb["cores"], "kind": cb["kind"],
+                             "sample": cb["sample"].split(" of the same workload")[0] + ", oracle C"}
+    lat = out.get("latency") or {}
+    if lat.get("gpu_solve_us") is not None:
+        c["lat_us"] = {"gpu": lat["gpu_solve_us"], "host": lat.get("host_and_handoff_us")}
+    cfgs = {}
+    if out.get("cpu_baseline_all_cores"):
+        cfgs[cfg["workload"]] = {"v": _g(out["value"]), "ms": _g(out["ms_per_step"]), "k": out.get("sweeps"),
+                                 "c1": _g(cb["value"]) if cb else None, "c16": _g(out["cpu_baseline_all_cores"]["value"])}
+    for grp in ("batched", "sharded"):
+        for name, b in (out.get(grp) or {}).items():
+            e = b.get("executed_rank0") or {}
+            v = (b.get("roofline") or {}).get("valu") or {}
+            d = {"v": _g(b["value"]), "x": _g(b.get("executed_updates_per_s")), "ms": _g(b["ms_per_solve"]),
+                 "k": b["sweeps"], "xf": _g(e.get("frac_of_global_rule"), 3), "valu": _g(v.get("frac"), 2)}
+            for key, src in (("c1", "cpu_baseline"), ("c16", "cpu_baseline_all_cores"), ("f1", "cpu_baseline_fp"),
+                             ("f16", "cpu_baseline_fp_all_cores")):
+                if b.get(src):
+                    d[key] = _g(b[src]["value"])
+            cfgs[name] = {k: x for k, x in d.items() if x is not None}
+    if cfgs:
+        c["configs"] = cfgs
+        c["configs_keys"] = ("v updates/s as the metric counts (B*S*A*K); x executed updates/s (grid-sweeps run); "
+                             "ms per solve; k sweeps; xf executed/K; valu VALU-issue frac; c1/c16 CPU oracle, "
+                             "literal global loop, 1/16 threads; f1/f16 same with the per-grid fixed-point stop")
+    return c
+
+
+def emit(out: dict):
+    """Full record to stderr (and MGDP_BENCH_DETAIL=path), then the compact line on stdout, last."""
+    detail = json.dumps(out)
+    log("bench detail: " + detail)
+    path = os.environ.get("MGDP_BENCH_DETAIL")
+    if path:
+        with open(path, "w") as f:
+            f.write(detail + "\n")
+    print(compact_dumps(compact_line(out)), flush=True)
+
+
+def compact_dumps(obj) -> str:
+    """json.dumps without spaces, large numbers in exponent form (the values are already rounded to
+    <= 6 significant digits): 24443600000.0 -> 2.44436e+10."""
+    import re
+
+    txt = json.dumps(obj, separators=(",", ":"))
+    return re.sub(r'(?<=[:\[,])(\d{7,}(?:\.\d+)?)(?=[,}\]])', lambda m: f"{float(m.group(1)):.6g}", txt)
 
 
 def compulsory_bytes_per_solve(info, tsize, method, sweeps):
@@ -538,6 +633,8 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded, split_ev
 
     def one_solve(last=False):
         if sharded:
+            if type(reducer).__name__ == "LibComm":
+                return solve_sharded(vi, comm=reducer)["sweeps"]
             return solve_sharded(vi, reducer=reducer)["sweeps"]
         if distinct:
             vi.load_device(base + (nxt[0] % n_grids) * hw)
@@ -663,13 +760,19 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded, split_ev
     if reducer is not None:
         dev_ms = reducer.collect()
         calls, reads, wall_s = red_region
-        collectives = {"allreduces_per_solve": calls / args.steps,
-                       "host_reads_per_solve": reads / args.steps,
-                       "allreduce_us_per_solve_rank0": dev_ms * 1000.0 / args.steps,
-                       "protocol_host_us_per_solve_rank0": wall_s * 1e6 / args.steps,
-                       "note": "device time of the RCCL all-reduces (events on the protocol stream, includes "
-                               "waiting for the slowest rank; from the events pass when the region runs "
-                               "without events) and host time of the one read per solve"}
+        if type(reducer).__name__ == "LibComm":
+            collectives = {"allreduces_per_solve": calls / args.steps, "host_reads_per_solve": reads / args.steps,
+                           "path": "libmgdp communicator (mgdp_vi_solve_sharded: RCCL enqueued by the library on "
+                                   "the handle's stream, one C call and one host wait per solve)"}
+        else:
+            collectives = {"allreduces_per_solve": calls / args.steps,
+                           "host_reads_per_solve": reads / args.steps,
+                           "allreduce_us_per_solve_rank0": dev_ms * 1000.0 / args.steps,
+                           "protocol_host_us_per_solve_rank0": wall_s * 1e6 / args.steps,
+                           "path": "torch.distributed ProcessGroupNCCL (distributed.Reducer)",
+                           "note": "device time of the RCCL all-reduces (events on the protocol stream, includes "
+                                   "waiting for the slowest rank; from the events pass when the region runs "
+                                   "without events) and host time of the one read per solve"}
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         u = torch.tensor([upd_rank], dtype=torch.float64, device=red_dev)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MGDP_ABI_VERSION 10
+#define MGDP_ABI_VERSION 11
 
 enum {
     MGDP_OK = 0,
@@ -142,6 +142,9 @@ int mgdp_vi_persistent(const mgdp_vi *vi, int32_t *on);
 /* Name of the kernel mgdp_vi_kernel_time times on this handle (as rocprofv3 lists it): vi_serve_kernel,
  * vi_fused_kernel, vi_fused_opts_kernel, vi_sweep_pipe_kernel or vi_sweep_kernel; NULL on error. */
 const char *mgdp_vi_kernel_name(const mgdp_vi *vi);
+/* Which loop of that kernel the handle runs (ABI 11), e.g. "serve_ew", "wave2", "dk_rows", "dk_half",
+ * "dk_soa", "sweep_pipe" (DESIGN.md section 4 names each); NULL on error.  Diagnostics and tests. */
+const char *mgdp_vi_variant(const mgdp_vi *vi);
 
 /* Multi-device protocol: every rank calls
  *   mgdp_vi_reset -> mgdp_vi_run_local(&k_local) -> mgdp_vi_local_result(&k, &dv_own, &k_min)
@@ -197,6 +200,34 @@ int mgdp_vi_run_to_dev_sync(mgdp_vi *vi, const int64_t *d_kdv, int32_t *k_out, d
 /* Hand the all-reduced K and dV back to the handle (every grid is at sweep K). */
 int mgdp_vi_set_result(mgdp_vi *vi, int32_t k, double dv);
 
+/* The sharded solve behind the C ABI (ABI 11): the same protocol with its collectives issued by the
+ * library on a communicator it owns -- RCCL over xGMI (librccl, loaded at the first mgdp_comm_* call:
+ * MGDP_RCCL_LIB, else the copy already mapped into the process, e.g. PyTorch's, else librccl.so.1).
+ * Bootstrap: one rank calls mgdp_comm_unique_id and hands the 128 bytes to every rank through any
+ * side channel (a torch.distributed store, MPI, a file); every rank then calls mgdp_comm_create with
+ * its rank and device.  One communicator per process and device, shared by its handles. */
+typedef struct mgdp_comm mgdp_comm;
+int mgdp_comm_unique_id(uint8_t *id_out /* 128 bytes */);
+int mgdp_comm_create(const uint8_t *id /* 128 bytes */, int32_t nranks, int32_t rank, int32_t device,
+                     mgdp_comm **out);
+int mgdp_comm_destroy(mgdp_comm *comm);
+/* Synchronous MAX all-reduce of n int64 host values in place (for ranks that drive the protocol from
+ * the host: an empty shard, the sweep method, DP options -- they join the same collectives). */
+int mgdp_comm_allreduce_max(mgdp_comm *comm, int64_t *vals, int32_t n);
+/* All-reduces issued on the communicator so far, its size and this process's rank. */
+int mgdp_comm_stats(const mgdp_comm *comm, int64_t *allreduces, int32_t *nranks, int32_t *rank);
+/* One sharded solve of this rank's handle (fused method, no horizon / lava options), every rank of
+ * the communicator at once: reset -> run_local_dev -> MAX all-reduce of {K, own-rule dV bits} on the
+ * handle's stream -> gate / run_to(K) with one host wait on host-mapped words -> [only if the
+ * all-reduced own-rule dV != 0: MAX all-reduce of dV(K)] -> rounding-level fallback sweeps, each
+ * with one all-reduce -> finish.  Host-driven peers issue the same collectives in the same order
+ * through mgdp_comm_allreduce_max: {k, dV bits} (2 words), then dV(K) bits (1 word) only if the
+ * all-reduced dV bits are non-zero, then one word per fallback sweep while dV >= tol and
+ * k < max_sweeps.  Results as mgdp_vi_solve (V and pi of the global rule, bit-identical to one global
+ * Jacobi loop over every rank's grids). */
+int mgdp_vi_solve_sharded(mgdp_vi *vi, mgdp_comm *comm, int32_t *sweeps_out, double *dv_out,
+                          int32_t *converged_out);
+
 /* Results (host).  V: B*S of float or double per dtype; pi: B*S int8 (-1 = absorbing state). */
 int mgdp_vi_get_values(mgdp_vi *vi, void *V);
 int mgdp_vi_get_policy(mgdp_vi *vi, int8_t *pi);
@@ -204,10 +235,12 @@ int mgdp_vi_get_policy(mgdp_vi *vi, int8_t *pi);
 int mgdp_vi_get_policy_t(mgdp_vi *vi, int8_t *pi_t);
 /* Per-sweep global max|dV| (method SWEEP only; fused runs record only the last): n <= max_sweeps */
 int mgdp_vi_get_dv_trace(mgdp_vi *vi, double *trace, int32_t n);
-/* Sweeps each grid executed (ABI 9), B int32: a grid whose own rule stopped at an exact fixed
- * point (|dV| = 0) reports that sweep -- its V and pi are those of every later sweep, so the
- * global rule's remaining sweeps are not executed for it (fixed-point completion) -- any other grid
- * the sweep it was taken to (the global K).  The sweep method reports K for every grid. */
+/* Sweeps each grid executed (ABI 9; ABI 11: on every path), B int32: the sweep index each grid's
+ * last computed sweep reached.  A grid whose own rule stopped at an exact fixed point (|dV| = 0)
+ * reports that sweep -- its V and pi are those of every later sweep, so the global rule's remaining
+ * sweeps are not executed for it (fixed-point completion), and a later run_to only moves its
+ * protocol sweep count, not this one -- any other grid the sweep it was taken to (the global K).
+ * The sweep method reports K for every grid. */
 int mgdp_vi_get_grid_sweeps(mgdp_vi *vi, int32_t *k);
 /* Device pointers of the handle's V (current) and pi buffers, for zero-copy consumers. */
 int mgdp_vi_device_buffers(mgdp_vi *vi, void **d_V, void **d_pi);

@@ -6,12 +6,13 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 # MGDP_LIB: an alternative build of the same sources (tools/ experiments with compile-time knobs)
 LIB_PATH = os.environ.get("MGDP_LIB") or os.path.join(HERE, "libmgdp.so")
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 MGDP_OK = 0
 MGDP_E_INVALID = -1
 MGDP_E_HIP = -2
@@ -88,6 +89,12 @@ SIGNATURES = {
     "mgdp_vi_run_local_dev": (ctypes.c_int, [_P, _P]),
     "mgdp_vi_run_to_dev": (ctypes.c_int, [_P, _P, _P]),
     "mgdp_vi_set_result": (ctypes.c_int, [_P, _I32, ctypes.c_double]),
+    "mgdp_comm_unique_id": (ctypes.c_int, [_P]),
+    "mgdp_comm_create": (ctypes.c_int, [_P, _I32, _I32, _I32, ctypes.POINTER(_P)]),
+    "mgdp_comm_destroy": (ctypes.c_int, [_P]),
+    "mgdp_comm_allreduce_max": (ctypes.c_int, [_P, _P, _I32]),
+    "mgdp_comm_stats": (ctypes.c_int, [_P, _I64P, _I32P, _I32P]),
+    "mgdp_vi_solve_sharded": (ctypes.c_int, [_P, _P, _I32P, _DP, _I32P]),
     "mgdp_vi_run_to_dev_sync": (ctypes.c_int, [_P, _P, _I32P, _DP, _DP]),
     "mgdp_vi_local_result": (ctypes.c_int, [_P, _I32P, _DP, _I32P]),
     "mgdp_vi_get_values": (ctypes.c_int, [_P, _P]),
@@ -102,6 +109,7 @@ SIGNATURES = {
     "mgdp_vi_serve_clock": (ctypes.c_int, [_P, _DP, _DP, _I64P, _DP, _I64P]),
     "mgdp_vi_persistent": (ctypes.c_int, [_P, _I32P]),
     "mgdp_vi_kernel_name": (ctypes.c_char_p, [_P]),
+    "mgdp_vi_variant": (ctypes.c_char_p, [_P]),
     "mgdp_vi_get_policy_t": (ctypes.c_int, [_P, _P]),
     "mgdp_gen_grids": (ctypes.c_int, [ctypes.POINTER(GenDesc), _I32, _P, ctypes.c_int64, _I32, _P, _P, _P]),
     "mgdp_gen_grids_host": (ctypes.c_int, [ctypes.POINTER(GenDesc), _I32, ctypes.c_int64, _I32, _P, _P, _P]),
@@ -163,11 +171,15 @@ def load():
             "(python -c 'import __graft_entry__ as g; g.build()')")
     # PyTorch-ROCm bundles its own HIP runtime under the same SONAME (libamdhip64.so.7) as the one
     # libmgdp links; whichever is loaded first serves both, and torch's GPU init fails ("No HIP GPUs
-    # are available") if ours came first -- so torch, when present, is loaded before libmgdp.
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    # are available") if ours came first.  MGDP_HIP_RUNTIME picks: "torch" (default when torch is
+    # installed: torch is imported first, so a later torch import in the process still works),
+    # "system" (libmgdp binds /opt/rocm's runtime; torch must then not be used for the GPU in this
+    # process).  hip_runtime() reports which file was loaded (bench.py records it).
+    if os.environ.get("MGDP_HIP_RUNTIME", "torch") != "system" and "torch" not in sys.modules:
+        import importlib.util
+
+        if importlib.util.find_spec("torch") is not None:
+            import torch  # noqa: F401
     L = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(L, name)
@@ -177,6 +189,18 @@ def load():
         raise MgdpError("libmgdp ABI version mismatch")
     _lib = L
     return L
+
+
+def hip_runtime() -> str | None:
+    """Path of the HIP runtime (libamdhip64) mapped into this process, or None."""
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if "libamdhip64" in line:
+                    return line.split()[-1]
+    except OSError:
+        pass
+    return None
 
 
 def last_error() -> str:

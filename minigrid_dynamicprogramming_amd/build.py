@@ -8,7 +8,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.environ.get("MGDP_BUILD_OUT") or os.path.join(HERE, "libmgdp.so")
-SOURCES = ["lib.cpp", "vi.hip", "envs.hip", "gen.hip"]
+SOURCES = ["lib.cpp", "vi.hip", "envs.hip", "gen.hip", "comm.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MGDP_ARCH", "gfx950")
 
@@ -21,6 +21,7 @@ ARCH = os.environ.get("MGDP_ARCH", "gfx950")
 # profiles/r03_slp_gk/).
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Xarch_device", "-fno-honor-nans",
          "-Xarch_device", "-fno-slp-vectorize", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result"]
+LIBS = ["-ldl"]
 
 
 def _extra_flags() -> list:
@@ -79,7 +80,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     with ThreadPoolExecutor(max_workers=min(len(jobs), os.cpu_count() or 1)) as ex:
         list(ex.map(run, [c for _, c in jobs]))
     tmp = f"{OUT}.tmp{os.getpid()}"
-    run([HIPCC, *FLAGS, "-o", tmp, *[o for o, _ in jobs]])
+    run([HIPCC, *FLAGS, "-o", tmp, *[o for o, _ in jobs], *LIBS])
     os.replace(tmp, OUT)
     with open(_stamp_path(), "w") as f:
         f.write(" ".join(FLAGS + extra))

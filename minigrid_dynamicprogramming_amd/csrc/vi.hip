@@ -41,6 +41,7 @@
 #include <vector>
 
 #include "common.h"
+#include "comm.h"
 
 #include "vi_model.h"
 #include "vi_loops.h"
@@ -62,6 +63,7 @@ struct mgdp_vi {
     void *d_V[2] = {nullptr, nullptr};
     int8_t *d_pi = nullptr;
     int32_t *d_kenv = nullptr;
+    int32_t *d_kexec = nullptr;  // per grid: the sweep it last computed (fixed-point grids keep theirs)
     double *d_dvenv = nullptr;
     unsigned long long *d_shards = nullptr;
     unsigned long long *d_red = nullptr;    // fused reduction shards [64][4]
@@ -101,6 +103,7 @@ struct mgdp_vi {
     int serve_ew = 0;             // served lone deterministic XYD grid on fused_serve_xyd (MGDP_SERVE_EW=0: off)
     int dk1t = 0;                 // batched fp32 DoorKey on one LDS tile (MGDP_DK_1T; fused_fast_dk_1t)
     int dkhalf = 0;               // batched DoorKey, states split by has_key over two threads (MGDP_DK_HALF; fused_dk_half)
+    int dkrow = 0;                // batched DoorKey of width 16 on whole-row thread maps (MGDP_DK_ROWS; fused_dk_rows)
     int pair2 = 1;                // batched plain XYD with cpt 2: adjacent-cell pairs (MGDP_PAIR2=0: fused_fast_xyd_soa_xn)
     int wave2 = 0;                // batched plain XYD on one wave per grid: cells per lane P (fused_wave2_xyd; 0 = off)
     int wave2n = 0;               // ... on two waves per grid instead: blocks per wave PW (fused_wave2n_xyd; 0 = off)
@@ -164,6 +167,7 @@ Geo make_geo(const mgdp_vi *vi) {
     g.quad = vi->quad;
     g.pair = vi->pair;
     g.tol = vi->d.tol;
+    g.kexec = vi->d_kexec;
     return g;
 }
 
@@ -368,12 +372,16 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
     if constexpr (MODEL == MGDP_MODEL_DOORKEY && MAP == MGDP_MAP_CELL && !SLIP) {
         if (vi->dk1t) kern = FusedK<T, MODEL, SLIP, MAP, kWpDk1t>::fn;
         else if (vi->dkhalf) kern = pick_dkhalf<FusedK, T, MODEL, SLIP, MAP>(vi->HWs / 64, kern);
+        else if (vi->dkrow) kern = FusedK<T, MODEL, SLIP, MAP, kWpDkRow>::fn;
     }
     if constexpr (MAP == MGDP_MAP_CELL) {  // one cell per thread, direction-major: the stripped variant
         if (kern == FusedK<T, MODEL, SLIP, MAP, 0>::fn && !vi->pair && !vi->quad && vi->HW <= vi->fused_block)
             kern = FusedK<T, MODEL, SLIP, MAP, kWpSoa>::fn;
     }
     int smem = L.total();
+    if constexpr (MODEL == MGDP_MODEL_DOORKEY && MAP == MGDP_MAP_CELL && !SLIP) {
+        if (vi->dkrow && !vi->dk1t && !vi->dkhalf) smem = dkrow_smem_bytes(vi->HWp, vi->HWs, (int)sizeof(T));
+    }
     if constexpr (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL && !SLIP) {
         if (vi->wave2n) {
             kern = pick_wave2n<FusedK, T, MODEL, SLIP, MAP>(vi->wave2n, kern);
@@ -391,8 +399,10 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
     }
     TimedPair tp;
     if (int rc = timed_begin(vi, -1, &tp)) return rc;
-    // the launch-wide rule: a fresh own-rule launch of a resident batch (every grid then also does
-    // the sweeps up to the global K, and the run_to launch is skipped when all reached it)
+    // the in-launch reduction (GkCtx): a fresh own-rule launch of a resident one-wave batch folds
+    // each grid's {k_e, dV at k_e} through the counter tree and publishes {kmax, dV, kmin} itself (no
+    // reduce kernel); grids at an exact fixed point are complete for any K (fixed-point completion),
+    // so run_to has nothing to launch unless some grid stopped with dV > 0
     unsigned long long *gk = (vi->gk && k_target < 0 && vi->fresh && !k_dev) ? vi->d_gk : nullptr;
     hipExtLaunchKernelGGL(kern, dim3(vi->d.B), dim3(vi->fused_block), smem, vi->stream, tp.a, tp.b, 0, g,
                        make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv,
@@ -960,6 +970,20 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
             vi->Ss = vi->S / vi->HW * vi->HWs;
             vi->fused_block = 2 * vi->HWs;
         }
+        // Batched DoorKey grids of width 16 (DoorKey-16x16): whole grid rows per 16 lanes, east / west
+        // fronts by DPP, two conflict-free LDS planes (fused_dk_rows).  The special-first cell map of
+        // fused_fast_dk_soa spent half its LDS-array cycles on bank conflicts (round-4 counters).
+        // MGDP_DK_ROWS=0 keeps fused_fast_dk_soa.
+        int dkrow = 1;
+        if (const char *ev = std::getenv("MGDP_DK_ROWS")) dkrow = std::atoi(ev) != 0;
+        if (dkrow && !vi->dk1t && !vi->dkhalf && d.B > 1 && d.model == MGDP_MODEL_DOORKEY &&
+            d.method == MGDP_METHOD_FUSED && d.slip_p < 0.0 && !vi->opts && !vi->pair && !vi->quad && d.W == 16 &&
+            vi->HW <= 1024) {
+            vi->dkrow = 1;
+            vi->HWs = (int)round_up(vi->HW, 64);
+            vi->Ss = vi->S / vi->HW * vi->HWs;
+            vi->fused_block = vi->HWs;
+        }
     } else {
         int blk = d.B == 1 ? 1024 : 256;
         while (blk > 64 && blk / 2 >= vi->S * 8) blk /= 2;
@@ -974,6 +998,8 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     if (d.method == MGDP_METHOD_SWEEP) al(&vi->d_V[1], BS * vi->tsize);
     al((void **)&vi->d_pi, BS);
     al((void **)&vi->d_kenv, sizeof(int32_t) * d.B);
+    al((void **)&vi->d_kexec, sizeof(int32_t) * d.B);
+    if (e == hipSuccess) e = hipMemset(vi->d_kexec, 0, sizeof(int32_t) * d.B);
     al((void **)&vi->d_dvenv, sizeof(double) * d.B);
     al((void **)&vi->d_shards, sizeof(unsigned long long) * 8 * (size_t)(d.max_sweeps + 1));
     al((void **)&vi->d_red, sizeof(unsigned long long) * (kRedShards * 4 + 2));
@@ -1057,6 +1083,7 @@ int mgdp_vi_destroy(mgdp_vi *vi) {
     (void)hipFree(vi->d_V[1]);
     (void)hipFree(vi->d_pi);
     (void)hipFree(vi->d_kenv);
+    (void)hipFree(vi->d_kexec);
     (void)hipFree(vi->d_dvenv);
     (void)hipFree(vi->d_shards);
     (void)hipFree(vi->d_red);
@@ -1394,6 +1421,62 @@ int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *con
     return 0;
 }
 
+// The sharded solve with the library's own collectives (include/mgdp.h, ABI 11): the device
+// protocol of distributed.py with RCCL called from here on the handle's stream instead of through
+// torch.distributed -- run_local_dev publishes {K_r, E_r bits, kmin, epoch} into the communicator's
+// device words, ncclAllReduce(MAX) of the first two is enqueued right behind it, the gate (or
+// run_to(K)) reads them on the device, and the host waits once on host-mapped words.  Only when
+// some grid anywhere stopped its own rule with dV > 0 (E != 0: slip, rounding, a cap) is dV(K)
+// all-reduced too, and only a rounding-level breach of the contraction runs fallback sweeps.
+namespace {
+int comm_max_double(mgdp_comm *c, hipStream_t s, double *x) {
+    // one word through the communicator's device buffer: non-negative doubles order like their bits
+    int64_t *h = comm_host_word(c), *d = comm_proto(c) + 5;
+    std::memcpy(h, x, sizeof(double));
+    MGDP_HIP(hipMemcpyAsync(d, h, sizeof(int64_t), hipMemcpyHostToDevice, s));
+    if (int rc = comm_allreduce_max_dev(c, d, 1, s)) return rc;
+    MGDP_HIP(hipMemcpyAsync(h, d, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    MGDP_HIP(hipStreamSynchronize(s));
+    std::memcpy(x, h, sizeof(double));
+    return 0;
+}
+}  // namespace
+
+int mgdp_vi_solve_sharded(mgdp_vi *vi, mgdp_comm *comm, int32_t *sweeps_out, double *dv_out, int32_t *converged_out) {
+    MGDP_CHECK(vi && comm, MGDP_E_INVALID, "null argument");
+    MGDP_CHECK(vi->d.method == MGDP_METHOD_FUSED && !vi->opts, MGDP_E_UNSUPPORTED,
+               "the sharded solve runs the fused method without horizon / lava options");
+    MGDP_CHECK(comm_device(comm) == vi->d.device, MGDP_E_INVALID, "communicator on device %d, handle on device %d",
+               comm_device(comm), vi->d.device);
+    DeviceGuard guard(vi->d.device);
+    if (int rc = mgdp_vi_reset(vi)) return rc;
+    int64_t *p = comm_proto(comm);
+    if (int rc = mgdp_vi_run_local_dev(vi, p)) return rc;                  // {K_r, E_r bits, kmin, epoch}
+    if (int rc = comm_allreduce_max_dev(comm, p, 2, vi->stream)) return rc;  // {K, E} over every rank
+    int32_t k = 0;
+    double dv = 0.0, rule = 0.0;
+    if (int rc = mgdp_vi_run_to_dev_sync(vi, p, &k, &dv, &rule)) return rc;  // the solve's one host wait
+    if (rule == 0.0) {
+        // every grid of every rank stopped at an exact fixed point: dV at K is 0 everywhere
+        MGDP_CHECK(dv == 0.0, MGDP_E_INVALID, "fixed-point invariant violated: dV at sweep %d is %g", k, dv);
+    } else if (int rc = comm_max_double(comm, vi->stream, &dv)) {
+        return rc;
+    }
+    if (int rc = mgdp_vi_set_result(vi, k, dv)) return rc;
+    while (!(dv < vi->d.tol) && k < vi->d.max_sweeps) {  // contraction broken by rounding: global rule
+        if (int rc = mgdp_vi_sweep(vi, &dv)) return rc;
+        if (int rc = comm_max_double(comm, vi->stream, &dv)) return rc;
+        ++k;
+        vi->dv_red = dv;
+    }
+    if (int rc = mgdp_vi_finish(vi, k)) return rc;
+    vi->converged = dv < vi->d.tol;
+    if (sweeps_out) *sweeps_out = k;
+    if (dv_out) *dv_out = dv;
+    if (converged_out) *converged_out = vi->converged;
+    return 0;
+}
+
 // Checkpoint / resume (aux "checkpoint / resume"): Jacobi is memoryless given V_k,
 // so a solve stopped at sweep k (a max_sweeps cap) continues from {V_k, k, dV_k} -- on this handle
 // or on a new one in another process -- to the same global stopping sweep, V and pi, bit for bit,
@@ -1419,6 +1502,7 @@ int mgdp_vi_resume(mgdp_vi *vi, const void *V, int32_t k, double dv, int32_t *sw
     std::vector<int32_t> kk((size_t)vi->d.B, k);
     std::vector<double> dd((size_t)vi->d.B, dv);
     MGDP_HIP(hipMemcpy(vi->d_kenv, kk.data(), kk.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    MGDP_HIP(hipMemcpy(vi->d_kexec, kk.data(), kk.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     MGDP_HIP(hipMemcpy(vi->d_dvenv, dd.data(), dd.size() * sizeof(double), hipMemcpyHostToDevice));
     vi->fresh = 0;  // the next fused launch continues each grid from kenv / dvenv and V in HBM
     vi->cur = 0;
@@ -1470,6 +1554,29 @@ const char *mgdp_vi_kernel_name(const mgdp_vi *vi) {
     return vi->d.mapping == MGDP_MAP_CELL && vi->sweep_pipe ? "vi_sweep_pipe_kernel" : "vi_sweep_kernel";
 }
 
+const char *mgdp_vi_variant(const mgdp_vi *vi) {
+    if (!vi) { set_error("null handle"); return nullptr; }
+    if (vi->d.method != MGDP_METHOD_FUSED) return vi->d.mapping == MGDP_MAP_CELL && vi->sweep_pipe ? "sweep_pipe" : "sweep";
+    if (vi->opts) return "opts";
+    if (vi->d.mapping == MGDP_MAP_SA) return "sa";
+    if (serve_eligible(vi)) {
+        if (vi->dkhalf) return "serve_dk_half";
+        if (vi->serve_ew) return "serve_ew";
+        return vi->wave_p ? "serve_wave" : "serve";
+    }
+    if (vi->dkrow) return "dk_rows";
+    if (vi->dkhalf) return "dk_half";
+    if (vi->dk1t) return "dk_1t";
+    if (vi->wave2n) return "wave2n";
+    if (vi->wave2) return "wave2";
+    if (vi->wave_p) return "wave";
+    if (vi->pair) return "pair";
+    if (vi->quad) return "quad";
+    if (vi->cpt == 2) return vi->pair2 && vi->d.slip_p < 0.0 ? "xyd_pair2" : "xyd_x2";
+    if (vi->cpt == 4) return "xyd_x4";
+    return vi->d.model == MGDP_MODEL_DOORKEY ? "dk_soa" : "xyd_soa";
+}
+
 int mgdp_vi_get_values(mgdp_vi *vi, void *V) {
     MGDP_CHECK(vi && V, MGDP_E_INVALID, "null argument");
     DeviceGuard guard(vi->d.device);
@@ -1506,7 +1613,7 @@ int mgdp_vi_get_grid_sweeps(mgdp_vi *vi, int32_t *k) {
         std::fill(k, k + vi->d.B, (int32_t)vi->k_done);
         return 0;
     }
-    MGDP_HIP(hipMemcpyAsync(k, vi->d_kenv, sizeof(int32_t) * (size_t)vi->d.B, hipMemcpyDeviceToHost, vi->stream));
+    MGDP_HIP(hipMemcpyAsync(k, vi->d_kexec, sizeof(int32_t) * (size_t)vi->d.B, hipMemcpyDeviceToHost, vi->stream));
     MGDP_HIP(hipStreamSynchronize(vi->stream));
     return 0;
 }

@@ -54,6 +54,9 @@ constexpr int kWpDkHalf = -500;
 // vi_serve_kernel variant tag: the served lone deterministic XYD grid on fused_serve_xyd (east / west
 // fronts by DPP; <= 4 waves), fused_fast_xyd_soa for a grid whose wave edges do not allow it
 constexpr int kWpServeEw = -600;
+// vi_fused_kernel variant tag: batched DoorKey grids of width 16 on whole-row thread maps, DPP
+// east / west fronts and two conflict-free LDS planes (fused_dk_rows; its own LDS layout, dkrow_*)
+constexpr int kWpDkRow = -800;
 // MGDP_DK_PERM=0 (A/B builds): batched DoorKey grids keep thread t on cell t (no dk_class_perm)
 #ifndef MGDP_DK_PERM
 #define MGDP_DK_PERM 1
@@ -112,6 +115,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
             fused_wave2n_xyd<T, false, PW>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
         if (threadIdx.x == 0) {
             kenv[e] = k;
+            if (geo.kexec) geo.kexec[e] = k;
             dvenv[e] = dvl;
         }
         return true;
@@ -137,6 +141,32 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
         }
         if (threadIdx.x == 0) {
             kenv[e] = k;
+            if (geo.kexec) geo.kexec[e] = k;
+            dvenv[e] = dvl;
+        }
+        return true;
+    }
+    if constexpr (WP == kWpDkRow) {  // its own LDS layout (dkrow_*): slots, flags, row map, cells, tiles
+        static_assert(MODEL == MGDP_MODEL_DOORKEY && !SLIP && MAP == MGDP_MAP_CELL && !SERVED, "dkrow: batched DoorKey");
+        uint8_t *cl2 = smem + dkrow_cells_off();
+        copy16(cl2, cells + (long long)e * geo.HWp, geo.HWp);
+        __syncthreads();
+        T *tiles = reinterpret_cast<T *>(smem + dkrow_tile_off(geo.HWp));
+        T *slots2 = reinterpret_cast<T *>(smem);
+        auto done2 = [&](int kk, double dv) {
+            if (lone && threadIdx.x == 0)
+                publish(host_out, (unsigned long long)kk, (unsigned long long)__double_as_longlong(dv),
+                        (unsigned long long)kk, epoch);
+        };
+        if (k_target < 0)
+            fused_dk_rows<T, true>(geo, cf, cl2, tiles, slots2, smem + 256, smem + 320, V + vb, V + vb, pi + vb, k,
+                                   k_target, dvl, done2);
+        else
+            fused_dk_rows<T, false>(geo, cf, cl2, tiles, slots2, smem + 256, smem + 320, V + vb, V + vb, pi + vb, k,
+                                    k_target, dvl, done2);
+        if (threadIdx.x == 0) {
+            kenv[e] = k;
+            if (geo.kexec) geo.kexec[e] = k;
             dvenv[e] = dvl;
         }
         return true;
@@ -185,6 +215,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
             fused_wave_xyd<T, SLIP, false, WP>(geo, cf, cl, V0, V1, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
         if (threadIdx.x == 0) {
             kenv[e] = k;
+            if (geo.kexec) geo.kexec[e] = k;
             dvenv[e] = dvl;
         }
         return true;
@@ -228,6 +259,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
         }
         if (threadIdx.x == 0) {
             kenv[e] = k;
+            if (geo.kexec) geo.kexec[e] = k;
             dvenv[e] = dvl;
         }
         return true;  // V and pi were written by their owner threads
@@ -269,6 +301,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     copy_pi(pi + vb, pis, geo.S);
     if (threadIdx.x == 0) {
         kenv[e] = k;
+        if (geo.kexec) geo.kexec[e] = k;
         dvenv[e] = dvl;
     }
     return true;
@@ -287,7 +320,7 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
                 unsigned long long *__restrict__ host_mirror, unsigned long long *__restrict__ gk) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
-    T *slots = reinterpret_cast<T *>(smem + (wp_is_wave2(WP) || wp_is_wave2n(WP) ? 0 : L.slots_off()));
+    T *slots = reinterpret_cast<T *>(smem + (wp_is_wave2(WP) || wp_is_wave2n(WP) || WP == kWpDkRow ? 0 : L.slots_off()));
     // multi-GPU protocol (mgdp_vi_run_to_dev): the target sweep is the all-reduced K in device
     // memory, written by a collective ordered before this launch on the stream
     if (k_target_dev) {
@@ -566,6 +599,7 @@ vi_fused_opts_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *
         }
         if (threadIdx.x == 0) {
             kenv[e] = k;
+            if (geo.kexec) geo.kexec[e] = k;
             dvenv[e] = dvl;
         }
     }

@@ -1512,6 +1512,218 @@ __device__ __forceinline__ void fused_fast_dk_soa(const Geo &geo, const Coef<T> 
     }
 }
 
+// Batched DoorKey grids of width 16 (DoorKey-16x16: BASELINE config 5), one thread per cell, grid
+// ROWS as the unit of the thread -> cell map.  Why (round 5): fused_fast_dk_soa keeps the LDS tiles
+// indexed by cell while the special-first map hands threads scattered cells, so a 16-lane
+// ds_read_b128 group or an 8-lane ds_write_b128 group hits one bank slot with several addresses:
+// SQ_LDS_BANK_CONFLICT was 51 % of the LDS-array cycles (profiles/r04_counters/
+// summary_doorkey65536.json; tools/dk_bank_sim.py predicts 55 % for that map, 0 for this one).
+//  * Lane l of wave w owns cell (row[4w + l/16], l % 16): whole rows move, so a DPP row of 16 lanes is
+//    one grid row and the lanes of any 16-lane read group / 8-lane write group own cells of distinct
+//    x (mod 16 / mod 8): every tile access below is conflict-free.  Rows are ordered by the wave
+//    class their cells need (key / door ahead or under, goal ahead; dk_step_fast's KD / GOAL
+//    forms), so the special rows share as few waves as possible, and fully absorbing rows go last.
+//  * East / west fronts come from lane +- 1 by DPP (wave_shl / wave_shr, +0 shifted in at the wave's
+//    ends): x = 0 and x = 15 are border walls, whose fronts do not matter (ge = 0 below), so only
+//    planes 1 and 3 (south / north fronts) go through LDS: two ds_read_b128 and two ds_write_b128
+//    per thread and sweep instead of four each (fused_serve_xyd's scheme for DoorKey's V4 groups).
+//  * Fronts are geometric: a front state the agent cannot enter is an invalid state holding +0 and
+//    V >= +0 (dk_step_fast's argument); the own cell's walkability enters as ge = g or 0, so an
+//    absorbing cell yields +0 with no select.
+//  * The stop test of sweep k is read right after its barrier, before sweep k+1's arithmetic (the
+//    batched loop has other waves to hide it), so when the rule stops, the two register sets hold
+//    V_k and V_{k-1} and the tile sweep k read still holds V_{k-1}'s planes: the pi pass (dk_step's
+//    per-action form, lowest index on ties) reads its own values and east / west fronts from the
+//    V_{k-1} set and its north / south fronts from that tile.
+// Same candidates per state, same rule, same pi: V, pi, the stopping sweep and dV are bit-identical
+// to fused_fast_dk_soa / the oracle.  LDS (dkrow_*): [slots 256][flags 64][row map 128][cells HWp]
+// [tile 0: plane 1 | plane 3][tile 1: ...], each plane PL = HWs + 32 V4 entries, cell c at 16 + c
+// (16 zero entries either side: the border rows' north / south reads land there).
+__host__ __device__ inline int dkrow_cells_off() { return 256 + 64 + 128; }
+__host__ __device__ inline int dkrow_tile_off(int HWp) { return dkrow_cells_off() + (HWp + 15) / 16 * 16; }
+__host__ __device__ inline int dkrow_plane(int HWs) { return HWs + 32; }  // V4 entries per plane
+__host__ __device__ inline int dkrow_smem_bytes(int HWp, int HWs, int tsize) {
+    return dkrow_tile_off(HWp) + 2 * 2 * dkrow_plane(HWs) * 4 * tsize;
+}
+
+// Value sweep of one DoorKey cell from geometric fronts (fE / fW: the east / west neighbours' plane
+// 0 / 2 values, fS / fN: the south / north neighbours' plane 1 / 3 groups).  Candidates per state as
+// dk_step_fast (left, right, self, forward; KD: pickup / toggle targets), one multiply by ge.
+template <typename T, bool GOAL, bool KD, bool DV>
+__device__ __forceinline__ T dk_rows_step(uint32_t walk, const uint32_t (&f)[4], T ge, const T (&in)[16],
+                                          const T (&fE)[4], const V4<T> &fS, const T (&fW)[4], const V4<T> &fN,
+                                          T (&out)[16]) {
+    T df[16];
+#pragma unroll
+    for (int hd = 0; hd < 4; ++hd) {
+        const T m02 = vmax(in[hd], in[8 + hd]), m13 = vmax(in[4 + hd], in[12 + hd]);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const int l = d * 4 + hd;
+            const T F = d == 0 ? fE[hd] : (d == 1 ? fS.v[hd] : (d == 2 ? fW[hd] : fN.v[hd]));
+            const T xS = in[l];
+            T M = vmax(vmax((d & 1) ? m02 : m13, xS), F);
+            if (KD) {
+                const bool key = f[d] & 64u, door = f[d] & 128u;
+                const int hk = hd >> 1, dop = hd & 1;
+                T cand = (T)0;
+                if (!hk) cand = key ? in[d * 4 + 2 + dop] : cand;
+                if (dop) cand = door ? in[d * 4 + hk * 2] : cand;
+                else if (hk) cand = door ? in[d * 4 + 3] : cand;
+                M = vmax(M, cand);
+            }
+            T best = ge * M;
+            if (GOAL) best = vmax(best, (f[d] & 16u) ? (T)1 : (T)0);
+            if (KD) best = ((walk >> hd) & 1u) ? best : (T)0;
+            out[l] = best;
+            if (DV) df[l] = vabs(best - xS);
+        }
+    }
+    if constexpr (!DV) return (T)0;
+    const T a = vmax(vmax(df[0], df[1]), df[2]), b = vmax(vmax(df[3], df[4]), df[5]);
+    const T c = vmax(vmax(df[6], df[7]), df[8]), e = vmax(vmax(df[9], df[10]), df[11]);
+    const T h = vmax(vmax(df[12], df[13]), df[14]);
+    return vmax(vmax(vmax(a, b), c), vmax(vmax(e, h), df[15]));
+}
+
+template <typename T, bool LOCAL, typename Done>
+__device__ __forceinline__ void fused_dk_rows(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *tiles,
+                                              T *slots, uint8_t *flags, uint8_t *rowmap, const T *Vg, T *Vg_out,
+                                              int8_t *pig, int &k, int k_target, double &dvl, const Done &done) {
+    const int t = (int)threadIdx.x, lane = t & 63;
+    const int HW = geo.HW, HWs = (int)blockDim.x, PL = dkrow_plane(HWs);
+    const int nrow = HWs >> 4;  // row slots (rows past H are idle; <= 64: HWs <= 1024)
+    // 1. Row classes from the identity map (thread t on cell t): bit 1 KD, bit 0 GOAL, bit 2 walkable.
+    {
+        uint32_t key = 0;
+        if (t < HW) {
+            const DkTopo tp0 = dk_topo(cl, geo, t);
+            const DkFast q0 = dk_fast_topo(tp0, 0);
+            key = (dk_fast_class(q0) & 2u ? 8u : 0u) | (dk_fast_class(q0) & 1u ? 4u : 0u) | (tp0.walk != 0u ? 2u : 0u) |
+                  1u;  // 1: a real row (rows past H sort last)
+        }
+        const unsigned long long b3 = __builtin_amdgcn_ballot_w64(key & 8u), b2 = __builtin_amdgcn_ballot_w64(key & 4u);
+        const unsigned long long b1 = __builtin_amdgcn_ballot_w64(key & 2u), b0 = __builtin_amdgcn_ballot_w64(key & 1u);
+        if ((lane & 15) == 0) {
+            const int sh = lane;  // this lane's 16-lane row segment
+            const uint32_t rk = (((b3 >> sh) & 0xFFFFull) ? 8u : 0u) | (((b2 >> sh) & 0xFFFFull) ? 4u : 0u) |
+                                (((b1 >> sh) & 0xFFFFull) ? 2u : 0u) | (((b0 >> sh) & 0xFFFFull) ? 1u : 0u);
+            rowmap[64 + (t >> 4)] = (uint8_t)rk;
+        }
+        if (t < 64) flags[t] = 0;
+        // the LDS tiles start at +0 (pads included): nothing else writes the pads
+        V4<T> *tv = reinterpret_cast<V4<T> *>(tiles);
+        for (int i = t; i < 4 * PL; i += HWs) tv[i] = V4<T>{{(T)0, (T)0, (T)0, (T)0}};
+        __syncthreads();
+        if (t < nrow) {  // stable rank, larger class first
+            const uint32_t mine = rowmap[64 + t];
+            int rank = 0;
+            for (int r = 0; r < nrow; ++r) {
+                const uint32_t o = rowmap[64 + r];
+                rank += (o > mine || (o == mine && r < t)) ? 1 : 0;
+            }
+            rowmap[rank] = (uint8_t)t;
+        }
+        __syncthreads();
+    }
+    const int row = rowmap[t >> 4];
+    const int c = row * 16 + (t & 15);
+    const bool own_cell = c < HW;
+    const int cc = own_cell ? c : 0;  // idle threads shadow cell 0 (a border wall): they compute +0
+    const DkTopo tp = dk_topo(cl, geo, cc);
+    const DkFast q = dk_fast_topo(tp, 0);
+    const uint32_t cls = dk_fast_class(q);
+    const uint32_t wcls = (__builtin_amdgcn_ballot_w64(cls & 1u) ? 1u : 0u) | (__builtin_amdgcn_ballot_w64(cls & 2u) ? 2u : 0u);
+    const T ge = tp.walk != 0u ? cf.g : (T)0;
+    const int k_start = k;
+    T *const T0 = tiles, *const T1 = tiles + 2 * PL * 4;
+    const int o1 = (16 + c) * 4, o3 = (PL + 16 + c) * 4;  // own entries of planes 1 / 3 (T units)
+    T A[16], Bv[16];
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) {
+        const V4<T> x = k == 0 ? V4<T>{{(T)0, (T)0, (T)0, (T)0}} : *reinterpret_cast<const V4<T> *>(Vg + cc * 16 + 4 * qd);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) A[4 * qd + j] = own_cell ? x.v[j] : (T)0;
+    }
+    *reinterpret_cast<V4<T> *>(T0 + o1) = V4<T>{{A[4], A[5], A[6], A[7]}};
+    *reinterpret_cast<V4<T> *>(T0 + o3) = V4<T>{{A[12], A[13], A[14], A[15]}};
+    __syncthreads();
+    T diff = (T)0;
+    auto sweep = [&](const T *Tin, T *Tout, const T (&in)[16], T (&out)[16], const int par) -> bool {
+        if (LOCAL) {
+            if (k >= geo.max_sweeps) return false;
+            if (k > k_start) {  // the previous sweep's flags (<= 4 waves: one dword; else 16 bytes)
+                bool more;
+                if (HWs <= 256) more = *reinterpret_cast<const uint32_t *>(flags + (par ^ 1) * 16) != 0u;
+                else {
+                    const uint4 f4 = *reinterpret_cast<const uint4 *>(flags + (par ^ 1) * 16);
+                    more = (f4.x | f4.y | f4.z | f4.w) != 0u;
+                }
+                if (!more) return false;
+            }
+        } else if (k >= k_target) {
+            return false;
+        }
+        const V4<T> fS = *reinterpret_cast<const V4<T> *>(Tin + o1 + 64);  // cell c + 16, plane 1
+        const V4<T> fN = *reinterpret_cast<const V4<T> *>(Tin + o3 - 64);  // cell c - 16, plane 3
+        T fE[4], fW[4];
+#pragma unroll
+        for (int hd = 0; hd < 4; ++hd) {
+            fE[hd] = dpp_shl1_zero(in[hd]);
+            fW[hd] = dpp_shr1_zero(in[8 + hd]);
+        }
+        T d;
+        if (LOCAL || k + 1 == k_target) {
+            if (wcls == 0u) d = dk_rows_step<T, false, false, true>(tp.walk, q.f, ge, in, fE, fS, fW, fN, out);
+            else if (wcls == 1u) d = dk_rows_step<T, true, false, true>(tp.walk, q.f, ge, in, fE, fS, fW, fN, out);
+            else d = dk_rows_step<T, true, true, true>(tp.walk, q.f, ge, in, fE, fS, fW, fN, out);
+        } else {
+            if (wcls == 0u) d = dk_rows_step<T, false, false, false>(tp.walk, q.f, ge, in, fE, fS, fW, fN, out);
+            else if (wcls == 1u) d = dk_rows_step<T, true, false, false>(tp.walk, q.f, ge, in, fE, fS, fW, fN, out);
+            else d = dk_rows_step<T, true, true, false>(tp.walk, q.f, ge, in, fE, fS, fW, fN, out);
+        }
+        diff = d;
+        *reinterpret_cast<V4<T> *>(Tout + o1) = V4<T>{{out[4], out[5], out[6], out[7]}};
+        *reinterpret_cast<V4<T> *>(Tout + o3) = V4<T>{{out[12], out[13], out[14], out[15]}};
+        if (LOCAL) flag_write(d >= cf.tol, flags, par);
+        __syncthreads();
+        ++k;
+        return true;
+    };
+    // at the stop: pos 0 = V_k in A, V_{k-1} in Bv and tile 1; pos 1 = V_k in Bv, V_{k-1} in A and tile 0
+    int pos;
+    while (true) {
+        if (!sweep(T0, T1, A, Bv, 0)) { pos = 0; break; }
+        if (!sweep(T1, T0, Bv, A, 1)) { pos = 1; break; }
+    }
+    dvl = (double)block_max(diff, slots, 0);
+    done(k, dvl);
+    T vk[16], vp[16];
+#pragma unroll
+    for (int l = 0; l < 16; ++l) {
+        vk[l] = pos ? Bv[l] : A[l];
+        vp[l] = pos ? A[l] : Bv[l];
+    }
+    const T *Tp = pos ? T0 : T1;
+    V4<T> nbs[4];
+#pragma unroll
+    for (int hd = 0; hd < 4; ++hd) {
+        nbs[0].v[hd] = dpp_shl1_zero(vp[hd]);
+        nbs[2].v[hd] = dpp_shr1_zero(vp[8 + hd]);
+    }
+    nbs[1] = *reinterpret_cast<const V4<T> *>(Tp + o1 + 64);
+    nbs[3] = *reinterpret_cast<const V4<T> *>(Tp + o3 - 64);
+    if (own_cell) {
+        T tmp[16];
+        uint32_t pk[4];
+        dk_step<T, true>(tp, cf, vp, nbs, tmp, pk);
+        *reinterpret_cast<uint4 *>(pig + c * 16) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd)
+            *reinterpret_cast<V4<T> *>(Vg_out + c * 16 + 4 * qd) = V4<T>{{vk[4 * qd], vk[4 * qd + 1], vk[4 * qd + 2], vk[4 * qd + 3]}};
+    }
+}
+
 // Batched DoorKey grids with each cell's 16 states split over two threads by has_key: the first
 // HWs threads (whole waves) own (cell, has_key 0), the next HWs threads (cell, has_key 1), 8 states
 // (dir, door_open) each.  Per thread that halves the values held per register set (own, the next

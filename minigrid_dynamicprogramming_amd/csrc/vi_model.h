@@ -15,6 +15,7 @@ struct Geo {
     int quad;    // fused XYD: 4 threads per cell (one per direction) instead of one
     int pair;    // fused XYD: two-sweep step
     double tol;
+    int32_t *kexec;  // per grid: the sweep index it last computed (mgdp_vi_get_grid_sweeps); nullptr = off
 };
 
 template <typename T>

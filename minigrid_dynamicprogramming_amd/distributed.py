@@ -159,6 +159,100 @@ class Reducer:
 _Reducer = Reducer
 
 
+class LibComm:
+    """The library's own communicator (mgdp_comm_*, include/mgdp.h ABI 11): RCCL over xGMI called
+    from libmgdp, so a sharded solve is ONE C call per rank (mgdp_vi_solve_sharded) with its
+    collectives enqueued on the handle's stream -- no torch.distributed call, stream switch or
+    Python between the launches.  Bootstrapped once per process over a torch.distributed group
+    (gloo or nccl): rank 0's 128-byte ncclUniqueId is broadcast to every rank.  Ranks whose shard
+    cannot run the device protocol (empty shards, the sweep method, DP options) join the same
+    collectives host-driven (mgdp_comm_allreduce_max); see solve_sharded."""
+
+    def __init__(self, group=None, device: int | None = None):
+        import ctypes
+
+        import torch
+        import torch.distributed as dist
+
+        from . import _lib
+
+        self._lib, self._ct = _lib, ctypes
+        L = _lib.load()
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        uid = (ctypes.c_uint8 * 128)()
+        if self.rank == 0:
+            _lib.check(L.mgdp_comm_unique_id(uid), "mgdp_comm_unique_id")
+        obj = [bytes(uid) if self.rank == 0 else None]
+        src = 0 if group is None else dist.get_global_rank(group, 0)
+        dist.broadcast_object_list(obj, src=src, group=group)
+        uid = (ctypes.c_uint8 * 128).from_buffer_copy(obj[0])
+        h = ctypes.c_void_p()
+        _lib.check(L.mgdp_comm_create(uid, self.world, self.rank, self.device, ctypes.byref(h)), "mgdp_comm_create")
+        self.handle = h
+        self._words = (ctypes.c_int64 * 8)()
+        # Reducer-like counters for bench.py's collectives block (no per-collective events: the
+        # collectives run inside the C call)
+        self.device = torch.device("cuda", self.device)
+        self.timing = False
+        self.reset_counters()
+
+    def reset_counters(self):
+        self._base = self.allreduces if getattr(self, "handle", None) is not None else 0
+        self.host_reads = 0
+        self.wall_s = 0.0
+        self.device_ms = 0.0
+
+    @property
+    def calls(self) -> int:
+        return self.allreduces - self._base
+
+    def collect(self) -> float:
+        return self.device_ms
+
+    def allreduce_max(self, vals) -> list:
+        """Synchronous MAX all-reduce of up to 8 int64 host values (mgdp_comm_allreduce_max)."""
+        n = len(vals)
+        for i, v in enumerate(vals):
+            self._words[i] = int(v)
+        self._lib.check(self._lib.load().mgdp_comm_allreduce_max(self.handle, self._words, n), "mgdp_comm_allreduce_max")
+        return [int(self._words[i]) for i in range(n)]
+
+    @property
+    def allreduces(self) -> int:
+        c = self._ct.c_int64(0)
+        self._lib.check(self._lib.load().mgdp_comm_stats(self.handle, self._ct.byref(c), None, None), "mgdp_comm_stats")
+        return int(c.value)
+
+    def close(self):
+        if getattr(self, "handle", None) is not None:
+            self._lib.load().mgdp_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 -- interpreter teardown
+            pass
+
+
+def _lib_host_protocol(vi, comm):
+    """The collectives of mgdp_vi_solve_sharded driven from the host, for a rank whose shard cannot
+    run it (EmptyShard, sweep method, DP options): {k_r, own-rule dV bits} (2 words), then dV(K)
+    (1 word) only if the all-reduced dV bits are non-zero -- same words, same order as the C side."""
+    vi.reset()
+    k_loc, e_loc = _local(vi)
+    K, e_bits = comm.allreduce_max([int(k_loc), double_to_bits(e_loc)])
+    k = int(K)
+    dv = vi.run_to(k)
+    if bits_to_double(e_bits) == 0.0:
+        if dv != 0.0:
+            raise RuntimeError(f"fixed-point invariant violated: dV at sweep {k} is {dv!r}")
+    else:
+        dv = bits_to_double(comm.allreduce_max([double_to_bits(dv)])[0])
+    return k, dv
+
+
 class EmptyShard:
     """A rank that holds no grids (more ranks than grids): it joins every collective with k = 0 and
     dV = 0, so the other ranks' protocol is unchanged; it takes whichever protocol its peers take."""
@@ -272,13 +366,30 @@ def _local(vi):
     return (k, float("inf")) if lr is None else (k, float(lr()[1]))
 
 
-def solve_sharded(vi, group=None, reducer=None) -> dict:
+def solve_sharded(vi, group=None, reducer=None, comm=None) -> dict:
     """Run the protocol above on this rank's shard `vi` (a dp.ValueIteration, an EmptyShard, or any
     object with reset/run_local/run_to/sweep/finish and tol/max_sweeps, optionally local_result;
     with protocol_device and run_local_dev/run_to_dev_sync/set_result it can take the device path).
     Returns sweeps, dv, converged and the all-reduces / host reads of this solve (the one-time
     protocol agreement not counted).  Must be called by every rank of the group; build the Reducer
-    once and pass it in."""
+    once and pass it in.  comm (a LibComm, built once, passed by EVERY rank or by none): the
+    library's own collectives -- one mgdp_vi_solve_sharded call per solve on ranks whose shard can
+    run it, the same collectives host-driven on the others."""
+    if comm is not None:
+        n0 = comm.allreduces
+        if getattr(vi, "sharded_capable", False):
+            k = vi.solve_sharded(comm)
+            if hasattr(comm, "host_reads"):
+                comm.host_reads += 1
+            return {"sweeps": k, "dv": vi.dv, "converged": vi.converged, "allreduces": comm.allreduces - n0,
+                    "host_reads": 1, "protocol": "lib"}
+        k, dv = _lib_host_protocol(vi, comm)
+        while not (dv < vi.tol) and k < vi.max_sweeps:
+            dv = bits_to_double(comm.allreduce_max([double_to_bits(vi.sweep())])[0])
+            k += 1
+        vi.finish(k, dv)
+        return {"sweeps": k, "dv": dv, "converged": dv < vi.tol, "allreduces": comm.allreduces - n0,
+                "host_reads": comm.allreduces - n0, "protocol": "lib-host"}
     red = reducer or Reducer(group)
     device = _device_capable(vi, red)
     calls0, reads0 = red.calls, red.host_reads

@@ -177,8 +177,10 @@ class ValueIteration:
         d.horizon = int(horizon)
         d.flags = 1 if keep_policy_t else 0
         self.horizon = int(horizon)
+        self.method, self.lava = method, lava
         self.desc = d
         self._solve_args = None
+        self._sharded_args = None
         self._load_dev_fn = None
         h = ctypes.c_void_p()
         _lib.check(self.L.mgdp_vi_create(ctypes.byref(d), ctypes.byref(h)), "mgdp_vi_create")
@@ -201,6 +203,14 @@ class ValueIteration:
         n = self.L.mgdp_vi_kernel_name(self.h)
         if n is None:
             _lib.check(_lib.MGDP_E_INVALID, "mgdp_vi_kernel_name")
+        return n.decode()
+
+    @property
+    def variant(self) -> str:
+        """Which loop of that kernel runs (mgdp_vi_variant): e.g. serve_ew, wave2, dk_rows, dk_half."""
+        n = self.L.mgdp_vi_variant(self.h)
+        if n is None:
+            _lib.check(_lib.MGDP_E_INVALID, "mgdp_vi_variant")
         return n.decode()
 
     def load(self, grids):
@@ -262,6 +272,22 @@ class ValueIteration:
         k, dv, conv = self._out
         self.sweeps, self.dv, self.converged = k.value, dv.value, bool(conv.value)
         return self.sweeps
+
+    def solve_sharded(self, comm) -> int:
+        """One sharded solve with the library's own collectives (mgdp_vi_solve_sharded on a
+        distributed.LibComm): every rank of the communicator calls it (or joins host-driven)."""
+        if self._sharded_args is None or self._sharded_args[1] != comm.handle:
+            self._sh_out = (ctypes.c_int32(0), ctypes.c_double(0), ctypes.c_int32(0))
+            self._sharded_args = (self.h, comm.handle) + tuple(ctypes.byref(o) for o in self._sh_out)
+        _lib.check(self.L.mgdp_vi_solve_sharded(*self._sharded_args), "mgdp_vi_solve_sharded")
+        k, dv, conv = self._sh_out
+        self.sweeps, self.dv, self.converged = k.value, dv.value, bool(conv.value)
+        return self.sweeps
+
+    @property
+    def sharded_capable(self) -> bool:
+        """Whether mgdp_vi_solve_sharded runs this handle (fused method, no horizon / lava options)."""
+        return self.method == "fused" and self.horizon == 0 and self.lava == "terminal"
 
     # -- multi-device protocol pieces (see distributed.py)
     def reset(self):

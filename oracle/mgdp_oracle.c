@@ -279,6 +279,108 @@ int orc_build_table(int model, int W, int H, const uint8_t *cells, int32_t *nxt,
 DEFINE_VI(float, vi_f32)
 DEFINE_VI(double, vi_f64)
 
+/* The same Jacobi loop with per-grid FIXED-POINT COMPLETION (the GPU's rule):  */
+/* a grid whose sweep k changed nothing (max |V_k - V_{k-1}| == 0 exactly) reproduces V_k and pi_k    */
+/* at every later sweep (a Jacobi sweep is a function of V alone), so it is not swept again; the      */
+/* global rule, V, pi, the sweep count and every dv are those of the literal loop above (a fixed grid  */
+/* contributes |dV| = 0).  Timed by bench.py as the like-for-like CPU leg of the batched configs;      */
+/* grid_sweeps (NULL or B ints) receives the sweeps each grid executed.  Grids are the unit of the     */
+/* OpenMP split.                                                                                      */
+#define DEFINE_VI_FP(T, NAME)                                                                     \
+    static int NAME(int model, int B, int W, int H, const uint8_t *cells, double gamma, double tol, \
+                    double slip_p, int max_sweeps, int nthreads, T *V, int8_t *pi, int *sweeps_out, \
+                    double *dv_trace, double *dv_last, int32_t *grid_sweeps) {                    \
+        const int A = model == 0 ? 7 : 5;                                                         \
+        const int S = W * H * (model == 0 ? 4 : 16);                                              \
+        const long long BS = (long long)B * S;                                                    \
+        const int slip = slip_p >= 0.0;                                                           \
+        if (slip && model != 0) return -3;                                                        \
+        int32_t *nxt = (int32_t *)malloc(sizeof(int32_t) * BS * A);                               \
+        double *rew = (double *)malloc(sizeof(double) * BS * A);                                  \
+        uint8_t *dn = (uint8_t *)malloc(BS * A);                                                  \
+        T *Vn = (T *)malloc(sizeof(T) * BS);                                                      \
+        uint8_t *fixed = (uint8_t *)calloc((size_t)B, 1);                                         \
+        if (!nxt || !rew || !dn || !Vn || !fixed) {                                               \
+            free(nxt); free(rew); free(dn); free(Vn); free(fixed); return -2;                     \
+        }                                                                                         \
+        _Pragma("omp parallel for num_threads(nthreads) schedule(dynamic, 64)")                    \
+        for (int b = 0; b < B; ++b)                                                               \
+            orc_build_table(model, W, H, cells + (long long)b * W * H, nxt + (long long)b * S * A, \
+                            rew + (long long)b * S * A, dn + (long long)b * S * A);               \
+        const T g = (T)gamma, p = (T)slip_p, cc = (T)((1.0 - slip_p) / 6.0);                      \
+        for (long long i = 0; i < BS; ++i) V[i] = (T)0;                                           \
+        if (grid_sweeps) for (int b = 0; b < B; ++b) grid_sweeps[b] = 0;                          \
+        int k = 0;                                                                                \
+        double dv = 0.0;                                                                          \
+        while (1) {                                                                               \
+            ++k;                                                                                  \
+            double dvk = 0.0;                                                                     \
+            _Pragma("omp parallel for reduction(max : dvk) num_threads(nthreads) schedule(dynamic, 4)") \
+            for (int b = 0; b < B; ++b) {                                                         \
+                if (fixed[b]) continue;                                                           \
+                const T *Vb = V + (long long)b * S;                                               \
+                double dvb = 0.0;                                                                 \
+                for (long long i = (long long)b * S; i < (long long)(b + 1) * S; ++i) {           \
+                    const int32_t *nx = nxt + i * A;                                              \
+                    if (nx[0] < 0) { Vn[i] = (T)0; pi[i] = -1; continue; }                        \
+                    T qd[7] = {0};                                                                      \
+                    for (int a = 0; a < A; ++a) {                                                 \
+                        const T r = (T)rew[i * A + a];                                            \
+                        qd[a] = dn[i * A + a] ? r : (T)(r + g * Vb[nx[a]]);                       \
+                    }                                                                             \
+                    T best = 0;                                                                   \
+                    int arg = 0;                                                                  \
+                    if (slip) {                                                                   \
+                        T s6 = qd[0] + qd[1];                                                     \
+                        s6 = s6 + qd[2];                                                          \
+                        s6 = s6 + qd[3];                                                          \
+                        s6 = s6 + qd[4];                                                          \
+                        s6 = s6 + qd[5];                                                          \
+                        const T tail = cc * s6;                                                   \
+                        for (int a = 0; a < A; ++a) {                                             \
+                            const T q = (T)(p * qd[a]) + tail;                                    \
+                            if (a == 0 || q > best) { best = q; arg = a; }                        \
+                        }                                                                         \
+                    } else {                                                                      \
+                        for (int a = 0; a < A; ++a)                                               \
+                            if (a == 0 || qd[a] > best) { best = qd[a]; arg = a; }                \
+                    }                                                                             \
+                    Vn[i] = best;                                                                 \
+                    pi[i] = (int8_t)arg;                                                          \
+                    const T diff = best > V[i] ? best - V[i] : V[i] - best;                       \
+                    if ((double)diff > dvb) dvb = (double)diff;                                   \
+                }                                                                                 \
+                memcpy(V + (long long)b * S, Vn + (long long)b * S, sizeof(T) * S);               \
+                if (grid_sweeps) grid_sweeps[b] = k;                                              \
+                if (dvb == 0.0) fixed[b] = 1;                                                     \
+                if (dvb > dvk) dvk = dvb;                                                         \
+            }                                                                                     \
+            if (dv_trace) dv_trace[k - 1] = dvk;                                                  \
+            dv = dvk;                                                                             \
+            if (dvk < tol || k >= max_sweeps) break;                                              \
+        }                                                                                         \
+        *sweeps_out = k;                                                                          \
+        if (dv_last) *dv_last = dv;                                                               \
+        free(nxt); free(rew); free(dn); free(Vn); free(fixed);                                    \
+        return 0;                                                                                 \
+    }
+
+DEFINE_VI_FP(float, vi_fp_f32)
+DEFINE_VI_FP(double, vi_fp_f64)
+
+int orc_vi_fp(int model, int dtype, int B, int W, int H, const uint8_t *cells, double gamma, double tol,
+              double slip_p, int max_sweeps, int nthreads, void *V, int8_t *pi, int *sweeps,
+              double *dv_trace, double *dv_last, int32_t *grid_sweeps) {
+    if (model != 0 && model != 1) return -1;
+    if (B <= 0 || W < 3 || H < 3 || max_sweeps <= 0) return -1;
+    if (nthreads <= 0) nthreads = 1;
+    if (dtype == 0)
+        return vi_fp_f32(model, B, W, H, cells, gamma, tol, slip_p, max_sweeps, nthreads, (float *)V, pi,
+                         sweeps, dv_trace, dv_last, grid_sweeps);
+    return vi_fp_f64(model, B, W, H, cells, gamma, tol, slip_p, max_sweeps, nthreads, (double *)V, pi,
+                     sweeps, dv_trace, dv_last, grid_sweeps);
+}
+
 /* dtype: 0 = fp32 (V is float*), 1 = fp64 (V is double*).  slip_p < 0 -> deterministic.
  * dv_trace must hold max_sweeps doubles (or be NULL).  Returns 0 on success. */
 int orc_vi(int model, int dtype, int B, int W, int H, const uint8_t *cells, double gamma, double tol,

@@ -37,6 +37,7 @@ def lib():
         L = ctypes.CDLL(LIB_PATH)
         L.orc_build_table.argtypes = [_I, _I, _I, _P, _P, _P, _P]
         L.orc_vi.argtypes = [_I, _I, _I, _I, _I, _P, _D, _D, _D, _I, _I, _P, _P, _P, _P, _P]
+        L.orc_vi_fp.argtypes = [_I, _I, _I, _I, _I, _P, _D, _D, _D, _I, _I, _P, _P, _P, _P, _P, _P]
         L.orc_step.argtypes = [_I, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]
         L.orc_gen_obs.argtypes = [_I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]
         L.orc_vi_ex.argtypes = [_I, _I, _I, _I, _I, _P, _D, _D, _D, _I, _I, _I, _D, _I, _P, _P, _P, _P, _P]
@@ -78,8 +79,10 @@ def build_table(model: int, cells: np.ndarray):
 
 
 def value_iteration(model: int, cells: np.ndarray, gamma=0.99, tol=1e-6, slip_p=None,
-                    max_sweeps=10000, dtype="f64", nthreads=1):
-    """cells: (B, H, W) or (H, W) uint8.  Returns dict(V (B,S), pi (B,S), sweeps, dv_trace, dv)."""
+                    max_sweeps=10000, dtype="f64", nthreads=1, fixed_point=False):
+    """cells: (B, H, W) or (H, W) uint8.  Returns dict(V (B,S), pi (B,S), sweeps, dv_trace, dv).
+    fixed_point: orc_vi_fp -- a grid at an exact fixed point is not swept again (same V, pi, sweeps
+    and dv as the literal loop); the dict then also holds grid_sweeps (B,), the sweeps each grid ran."""
     cells = np.ascontiguousarray(cells, dtype=np.uint8)
     if cells.ndim == 2:
         cells = cells[None]
@@ -91,13 +94,18 @@ def value_iteration(model: int, cells: np.ndarray, gamma=0.99, tol=1e-6, slip_p=
     sweeps = ctypes.c_int(0)
     dv_last = ctypes.c_double(0)
     trace = np.zeros(max_sweeps, np.float64)
-    rc = lib().orc_vi(model, 0 if dtype == "f32" else 1, B, W, H, _ptr(cells), gamma, tol,
-                      -1.0 if slip_p is None else float(slip_p), max_sweeps, nthreads, _ptr(V),
-                      _ptr(pi), ctypes.byref(sweeps), _ptr(trace), ctypes.byref(dv_last))
+    args = (model, 0 if dtype == "f32" else 1, B, W, H, _ptr(cells), gamma, tol,
+            -1.0 if slip_p is None else float(slip_p), max_sweeps, nthreads, _ptr(V),
+            _ptr(pi), ctypes.byref(sweeps), _ptr(trace), ctypes.byref(dv_last))
+    gs = np.zeros(B, np.int32) if fixed_point else None
+    rc = lib().orc_vi_fp(*args, _ptr(gs)) if fixed_point else lib().orc_vi(*args)
     if rc != 0:
         raise ValueError(f"orc_vi failed rc={rc}")
     k = sweeps.value
-    return {"V": V, "pi": pi, "sweeps": k, "dv_trace": trace[:k].copy(), "dv": dv_last.value}
+    out = {"V": V, "pi": pi, "sweeps": k, "dv_trace": trace[:k].copy(), "dv": dv_last.value}
+    if gs is not None:
+        out["grid_sweeps"] = gs
+    return out
 
 
 def value_iteration_ex(model: int, cells: np.ndarray, gamma=0.99, tol=1e-6, slip_p=None,

@@ -135,3 +135,56 @@ def test_measure_split_events_pass(bench):
     assert m["events_in_region"] is False and m["launches"] == 4 and len(m["sweeps"]) == 4
     m = bench.measure(_args("fourrooms4096", steps=4), "f32", cells, 0, None, None, None, False)
     assert m["events_in_region"] is True
+
+
+def _full_record():
+    """A default-line record with every block at its longest (values with many digits)."""
+    import math
+
+    def cpu(v):
+        return {"value": v * math.pi, "unit": "updates/s", "cores": 16, "kind": "port",
+                "sample": "12345 full solves of 512 grid(s) of the same workload (69 sweeps in the last, f32), "
+                          "oracle/mgdp_oracle.c orc_vi (literal global loop), 2.0 s"}
+
+    def blk(v, k):
+        return {"value": v * math.e, "unit": "updates/s", "ms_per_solve": 2.4938271, "sweeps": k,
+                "executed_updates_per_s": v * 1.7182818, "executed_rank0": {"frac_of_global_rule": 0.62912345},
+                "roofline": {"valu": {"frac": 0.41234567}}, "cpu_baseline": cpu(1e9), "cpu_baseline_all_cores": cpu(1e10),
+                "cpu_baseline_fp": cpu(2e9), "cpu_baseline_fp_all_cores": cpu(2e10)}
+
+    return {"metric": "state-action Bellman updates/sec + DP sweeps-to-converge, Empty-16x16", "value": 2.5123456789e10,
+            "unit": "updates/s", "n_gpus": 8, "steps": 200, "warmup": 20, "ms_per_step": 0.00828030169941485,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: MiniGrid-Empty-16x16-v0 grids from the reference-exact generator (seed 0 replicated)",
+            "config": {"workload": "empty16", "env_id": "MiniGrid-Empty-16x16-v0", "grids_per_gpu": 1, "global_grids": 8,
+                       "states_per_grid": 1024, "actions": 7, "gamma": 0.99, "tol": 1e-6, "method": "fused",
+                       "mapping": "cell", "parallelism": "replicas only", "host_thread": "pinned (128 CPUs)"},
+            "sweeps": 29,
+            "roofline": {"bound": "hbm", "kernel": "vi_serve_kernel", "achieved": 144.46552140524724, "peak": 8000.0,
+                         "unit": "GB/s", "frac": 0.018058190175655905, "traffic": 63168.123, "launches": 1,
+                         "avg_launch_us": 288.6030077934265, "solves_per_launch": 36.0, "note": "x" * 500},
+            "cpu_baseline": cpu(1e9), "cpu_baseline_all_cores": cpu(1e10),
+            "latency": {"gpu_solve_us": 6.271, "host_and_handoff_us": 2.012},
+            "batched": {"fourrooms4096": blk(2.6e13, 37)},
+            "sharded": {"lava65536": blk(6.6e13, 49), "doorkey65536": blk(3.7e13, 69)}}
+
+
+def test_compact_line_fits_the_driver_tail(bench):
+    """The stdout line keeps every contract key and one summary per BASELINE config, in < 2000 chars
+    (the driver records the last 2000 characters of stdout)."""
+    import json
+
+    out = _full_record()
+    txt = bench.compact_dumps(bench.compact_line(out))
+    assert len(txt) < 1950, len(txt)
+    c = json.loads(txt)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in c, k
+    assert c["roofline"]["frac"] == pytest.approx(0.0181, rel=1e-3)
+    assert c["value"] == pytest.approx(out["value"], rel=1e-5)
+    assert set(c["configs"]) == {"empty16", "fourrooms4096", "lava65536", "doorkey65536"}
+    fr = c["configs"]["fourrooms4096"]
+    assert fr["v"] == pytest.approx(2.6e13 * 2.718281828, rel=1e-3)
+    assert fr["x"] == pytest.approx(2.6e13 * 1.7182818, rel=1e-3)
+    assert {"c1", "c16", "f1", "f16", "xf", "valu", "k", "ms"} <= set(fr)

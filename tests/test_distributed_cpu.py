@@ -342,3 +342,83 @@ class _BrokenFixedPointShard(_NonMonotoneDevShard):
 def test_device_protocol_refuses_broken_fixed_point():
     with pytest.raises(RuntimeError, match="fixed-point invariant"):
         solve_sharded(_BrokenFixedPointShard(), reducer=_FakeDeviceReducer())
+
+
+# -- the library's own collectives (LibComm + mgdp_vi_solve_sharded), protocol logic on gloo ---------
+class GlooLibComm:
+    """LibComm's interface (allreduce_max of int64 host words, an all-reduce counter) over gloo."""
+
+    def __init__(self):
+        self.allreduces = 0
+
+    def allreduce_max(self, vals):
+        import torch
+        import torch.distributed as dist
+
+        t = torch.tensor([int(v) for v in vals], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        self.allreduces += 1
+        return [int(x) for x in t.tolist()]
+
+
+class LibOracleShard(OracleShard):
+    """A shard on the C path: solve_sharded(comm) issues exactly mgdp_vi_solve_sharded's collectives
+    (csrc/vi.hip): {K, own-rule dV bits}; dV(K) only if the all-reduced dV bits are non-zero; one
+    word per rounding-level fallback sweep."""
+
+    sharded_capable = True
+
+    def solve_sharded(self, comm):
+        self.reset()
+        k_loc = self.run_local()
+        K, e_bits = comm.allreduce_max([k_loc, double_to_bits(self._local[1])])
+        dv = self.run_to(K)
+        if bits_to_double(e_bits) != 0.0:
+            dv = bits_to_double(comm.allreduce_max([double_to_bits(dv)])[0])
+        k = K
+        while not (dv < self.tol) and k < self.max_sweeps:
+            dv = bits_to_double(comm.allreduce_max([double_to_bits(self.sweep())])[0])
+            k += 1
+        self.finish(k, dv)
+        self.dv, self.converged = dv, dv < self.tol
+        return k
+
+
+def _lib_worker(rank, world, port, cells, slip, out, kinds):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard_range(len(cells), rank, world)
+    comm = GlooLibComm()
+    kind = kinds[rank % len(kinds)]
+    shard = EmptyShard() if hi == lo else (LibOracleShard if kind == "lib" else OracleShard)(cells[lo:hi], slip=slip)
+    res = solve_sharded(shard, comm=comm)
+    out[rank] = (res["sweeps"], res["allreduces"], getattr(shard, "V", None), getattr(shard, "pi", None), lo, hi,
+                 res["protocol"])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("slip", [None, 0.9])
+@pytest.mark.parametrize("world,kinds", [(2, ("lib",)), (2, ("lib", "host")), (4, ("host", "lib")), (8, ("lib",))])
+def test_lib_comm_protocol_matches_global_loop(world, kinds, slip):
+    """Ranks on mgdp_vi_solve_sharded's collective sequence, host-driven peers and empty shards (8
+    ranks, 6 grids) meet in the same collectives; the result is one global Jacobi loop's."""
+    g = load("grids_fourrooms.npz")
+    cells = np.stack([cells_from_enc(e) for e in g["enc"][:6 if world == 8 else 10]])
+    ref = oracle.value_iteration(0, cells, slip_p=slip, dtype="f64")
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_lib_worker, args=(world, port, cells, slip, out, kinds), nprocs=world, join=True)
+    res = dict(out)
+    for r, (k, n, V, pi, lo, hi, proto) in res.items():
+        assert k == ref["sweeps"]
+        # deterministic: one collective per solve; slip: the dV(K) word too
+        assert n == (1 if slip is None else 2) or (slip is not None and n >= 2)
+        assert proto == ("lib" if (hi > lo and kinds[r % len(kinds)] == "lib") else "lib-host")
+        if hi > lo:
+            np.testing.assert_array_equal(V, ref["V"][lo:hi])
+            np.testing.assert_array_equal(pi, ref["pi"][lo:hi])

@@ -110,6 +110,29 @@ elif mode == "sync":
             vi.set_result(k, dv)
             vi.finish(k, dv)
             assert np.array_equal(vi.values(), V_ref) and np.array_equal(vi.policy(), pi_ref)
+elif mode == "lib1":
+    # the library's own communicator (mgdp_comm_*: RCCL from libmgdp, one rank), bootstrapped over a
+    # one-rank gloo group; one mgdp_vi_solve_sharded call per solve
+    import torch.distributed as dist
+    from minigrid_dynamicprogramming_amd.distributed import LibComm
+    dist.init_process_group("gloo")
+    comm = LibComm()
+    for rep in range(3):
+        res = solve_sharded(vi, comm=comm)
+        assert res["protocol"] == "lib", res
+        if slip is None:
+            assert res["sweeps"] == k_ref and res["allreduces"] == 1, res
+        else:
+            assert res["sweeps"] == k_ref and res["allreduces"] >= 2, res
+        assert np.array_equal(vi.values(), V_ref) and np.array_equal(vi.policy(), pi_ref)
+    # a rank whose handle cannot run the C path (the sweep method) joins host-driven
+    hs = mg.ValueIteration(cells, dtype=dtype, slip_p=slip, method="sweep")
+    res = solve_sharded(hs, comm=comm)
+    assert res["protocol"] == "lib-host" and res["sweeps"] == k_ref, res
+    assert np.array_equal(hs.values(), V_ref) and np.array_equal(hs.policy(), pi_ref)
+    hs.close()
+    comm.close()
+    dist.destroy_process_group()
 else:
     import torch.distributed as dist
     dist.init_process_group("nccl", device_id=torch.device("cuda", 0))  # RCCL, one rank
@@ -131,7 +154,7 @@ print("device protocol ok")
 """
 
 
-@pytest.mark.parametrize("mode", ["steps", "sync", "rccl1"])
+@pytest.mark.parametrize("mode", ["steps", "sync", "rccl1", "lib1"])
 @pytest.mark.parametrize("env_id,B,dtype", [("MiniGrid-LavaCrossingS11N5-v0", 2048, "f32"),
                                             ("MiniGrid-FourRooms-v0", 300, "f64"),
                                             ("MiniGrid-DoorKey-16x16-v0", 700, "f32"),
@@ -140,7 +163,9 @@ def test_device_protocol(mode, env_id, B, dtype):
     """mgdp_vi_run_local_dev / run_to_dev / set_result: K and dV in a device buffer, read once.
     "steps": the entry points on a torch stream; "sync": run_local_dev + run_to_dev_sync (result via
     host-mapped words); "rccl1": distributed.solve_sharded over a one-rank
-    RCCL group (the all-reduces are real RCCL collectives ordered on the protocol stream).  Batches
+    RCCL group (the all-reduces are real RCCL collectives ordered on the protocol stream); "lib1":
+    the library's own RCCL communicator (mgdp_vi_solve_sharded, one C call per solve) plus a
+    sweep-method handle joining its collectives host-driven.  Batches
     on both sides of the in-kernel-reduce limit (512) and a lone grid; equal to a one-device solve."""
     import subprocess
     import sys
@@ -153,8 +178,9 @@ def test_device_protocol(mode, env_id, B, dtype):
     assert r.returncode == 0 and "device protocol ok" in r.stdout, r.stdout + r.stderr
 
 
+@pytest.mark.parametrize("mode", ["rccl1", "lib1"])
 @pytest.mark.parametrize("B", [300, 2048])
-def test_device_protocol_rccl1_slip(B):
+def test_device_protocol_rccl1_slip(B, mode):
     """Slip grids over a one-rank RCCL group: the own-rule dV is not an exact fixed point, so the
     protocol all-reduces dV at K too (two collectives) and still equals a one-device solve."""
     import subprocess
@@ -163,6 +189,6 @@ def test_device_protocol_rccl1_slip(B):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), RANK="0", WORLD_SIZE="1",
                LOCAL_RANK="0")
-    r = subprocess.run([sys.executable, "-c", _DEVICE_PROTO, root, "rccl1", "MiniGrid-LavaCrossingS11N5-v0", str(B),
+    r = subprocess.run([sys.executable, "-c", _DEVICE_PROTO, root, mode, "MiniGrid-LavaCrossingS11N5-v0", str(B),
                         "f32", "0.9"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "device protocol ok" in r.stdout, r.stdout + r.stderr

@@ -67,6 +67,16 @@ def test_grid_sweeps_are_each_grids_own_stopping_sweep():
     vi.solve()
     own = np.array([oracle.value_iteration(0, c, dtype="f64")["sweeps"] for c in cells])
     np.testing.assert_array_equal(vi.grid_sweeps(), own)
+    np.testing.assert_array_equal(own, oracle.value_iteration(0, cells, dtype="f64", fixed_point=True)["grid_sweeps"])
+    # the same after the protocol's run_to to the global K (the fixed-point grids only move their
+    # protocol sweep count) and after a second solve on the handle
+    vi.reset()
+    K = vi.run_local()
+    vi.run_to(K)
+    vi.finish(K, 0.0)
+    np.testing.assert_array_equal(vi.grid_sweeps(), own)
+    vi.solve()
+    np.testing.assert_array_equal(vi.grid_sweeps(), own)
     vi.close()
 
 
@@ -94,7 +104,11 @@ def test_run_to_past_k_reproduces_the_global_loop(extra):
     o = oracle.value_iteration(0, cells, dtype="f32", tol=-1.0, max_sweeps=K + extra)
     np.testing.assert_array_equal(vi.values(), o["V"])
     np.testing.assert_array_equal(vi.policy(), o["pi"])
-    assert (vi.grid_sweeps() == K + extra).all()
+    # executed sweeps do not move with run_to: each grid reports its own stopping sweep, which the
+    # fixed-point oracle (orc_vi_fp: a grid at an exact fixed point is not swept again) reproduces
+    own = oracle.value_iteration(0, cells, dtype="f32", fixed_point=True)["grid_sweeps"]
+    np.testing.assert_array_equal(vi.grid_sweeps(), own)
+    assert own.max() == K
     vi.close()
 
 

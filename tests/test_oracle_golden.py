@@ -67,6 +67,40 @@ def test_batched_vi_global_rule():
         np.testing.assert_allclose(res["V"][b], t["V"], atol=1e-12)
 
 
+@pytest.mark.parametrize("slip", [None, 0.9])
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_fixed_point_oracle_equals_literal_loop(dtype, slip):
+    """orc_vi_fp (a grid at an exact fixed point is not swept again; bench.py's like-for-like CPU
+    leg) against the literal global loop on every golden XYD table grid batched together: sweeps,
+    V, pi and the dv trace identical; each grid's executed sweeps <= the global K."""
+    names = [n for n in table_names() if int(load(f"table_{n}.npz")["model"]) == 0]
+    cells = [cells_from_enc(load(f"table_{n}.npz")["enc"]) for n in names]
+    shape = max(c.shape for c in cells)
+    cells = [c for c in cells if c.shape == shape] or cells[:1]
+    cells = np.stack(cells)
+    a = oracle.value_iteration(0, cells, dtype=dtype, slip_p=slip)
+    b = oracle.value_iteration(0, cells, dtype=dtype, slip_p=slip, fixed_point=True)
+    assert a["sweeps"] == b["sweeps"]
+    np.testing.assert_array_equal(a["V"], b["V"])
+    np.testing.assert_array_equal(a["pi"], b["pi"])
+    np.testing.assert_array_equal(a["dv_trace"], b["dv_trace"])
+    assert b["grid_sweeps"].max() <= a["sweeps"] and b["grid_sweeps"].min() >= 1
+
+
+def test_fixed_point_oracle_doorkey_golden():
+    for n in table_names():
+        t = load(f"table_{n}.npz")
+        if int(t["model"]) != 1:
+            continue
+        c = cells_from_enc(t["enc"])
+        b = oracle.value_iteration(1, np.stack([c, c]), dtype="f64", fixed_point=True)
+        assert b["sweeps"] == int(t["sweeps"])
+        np.testing.assert_array_equal(b["pi"][0], t["pi"])
+        np.testing.assert_allclose(b["V"][0], t["V"], rtol=0, atol=1e-12)
+        # deterministic: the grid's last swept sweep is the one that changed nothing (= K)
+        assert (b["grid_sweeps"] == int(t["sweeps"])).all()
+
+
 @pytest.mark.parametrize("name", traj_names())
 def test_step_trajectory_matches_reference(name):
     t = load(f"traj_{name}.npz")
