@@ -554,6 +554,10 @@ def compact_line(out: dict) -> dict:
     if cb:
         c["cpu_baseline"] = {"value": _g(cb["value"]), "unit": cb["unit"], "cores": cb["cores"], "kind": cb["kind"],
                              "sample": cb["sample"].split(" of the same workload")[0] + ", oracle C"}
+    if out.get("collectives"):
+        col = out["collectives"]
+        c["collectives"] = {k: col[k] for k in ("allreduces_per_solve", "host_reads_per_solve") if k in col}
+        c["collectives"]["path"] = "libmgdp" if "libmgdp" in col.get("path", "") else "torch"
     lat = out.get("latency") or {}
     if lat.get("gpu_solve_us") is not None:
         c["lat_us"] = {"gpu": lat["gpu_solve_us"], "host": lat.get("host_and_handoff_us")}

@@ -414,6 +414,9 @@ struct mgdp_envs {
     uint8_t *d_obs = nullptr, *d_term = nullptr, *d_trunc = nullptr;
     double *d_rew = nullptr;
     uint32_t nd_mask = 0;
+    // masked loads (auto-reset of some envs): one staging copy + envs_masked_load_kernel
+    uint8_t *d_stage = nullptr;
+    size_t stage_bytes = 0;
     double death_cost = -1.0;
     int group = 2;  // lanes per env in envs_step_kernel (MGDP_STEP_GROUP = 1, 2, 4 or 8; 2 measured fastest)
     // step-kernel timing (mgdp_envs_enable_timing): pooled event pairs handed to hipExtLaunchKernelGGL
@@ -528,7 +531,7 @@ int mgdp_envs_destroy(mgdp_envs *E) {
     DeviceGuard guard(E->device);
     if (E->stream) (void)hipStreamSynchronize(E->stream);
     void *ps[] = {E->d_cell, E->d_see, E->d_agent, E->d_carry, E->d_max, E->d_act,
-                  E->d_dir, E->d_status, E->d_obs, E->d_term, E->d_trunc, E->d_rew, E->d_cont, E->d_ccont};
+                  E->d_dir, E->d_status, E->d_obs, E->d_term, E->d_trunc, E->d_rew, E->d_cont, E->d_ccont, E->d_stage};
     for (void *p : ps) (void)hipFree(p);
     for (auto &p : E->ev) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
     for (auto &p : E->ev_pool) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
@@ -554,6 +557,37 @@ int mgdp_envs_set_stream(mgdp_envs *E, void *s) {
     if (s) E->stream = (hipStream_t)s;
     else { MGDP_HIP(hipStreamCreateWithFlags(&E->stream, hipStreamNonBlocking)); E->own_stream = true; }
     return 0;
+}
+
+// A masked reset (mgdp_envs_load with a mask): the host packs every env's prepared record into one
+// staging buffer, one copy takes it to the device, and this kernel writes the masked envs' cells,
+// agent, carry, max_steps and see_through and clears their Box contents -- O(1) runtime calls for
+// any number of envs (a per-env copy / memset loop made a 65536-env auto-reset ~300k API calls).
+// Staging layout: [mask B][see B][pad to 16][cells B*HWp][agent B*4 i32][carry B*2 i32][max B i32].
+__global__ void __launch_bounds__(64)
+envs_masked_load_kernel(int B, int HWp, const uint8_t *__restrict__ st, uint8_t *__restrict__ cell, int32_t *__restrict__ agent,
+                        int32_t *__restrict__ carry, int32_t *__restrict__ maxs, uint8_t *__restrict__ see,
+                        uint8_t *__restrict__ cont, uint8_t *__restrict__ ccont) {
+    const int b = blockIdx.x;
+    if (!st[b]) return;
+    const size_t o_cells = (size_t)((2 * B + 15) / 16 * 16);
+    const uint4 *src = reinterpret_cast<const uint4 *>(st + o_cells + (size_t)b * HWp);
+    uint4 *dst = reinterpret_cast<uint4 *>(cell + (size_t)b * HWp);
+    for (int i = threadIdx.x; i < HWp / 16; i += blockDim.x) {
+        dst[i] = src[i];
+        if (cont) reinterpret_cast<uint4 *>(cont + (size_t)b * HWp)[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (threadIdx.x == 0) {
+        const int32_t *ag = reinterpret_cast<const int32_t *>(st + o_cells + (size_t)B * HWp);
+        const int32_t *cr = ag + 4 * (size_t)B;
+        const int32_t *ms = cr + 2 * (size_t)B;
+        for (int j = 0; j < 4; ++j) agent[4 * b + j] = ag[4 * b + j];
+        carry[2 * b] = cr[2 * b];
+        carry[2 * b + 1] = cr[2 * b + 1];
+        maxs[b] = ms[b];
+        see[b] = st[B + b];
+        if (ccont) ccont[b] = 0;
+    }
 }
 
 int mgdp_envs_load(mgdp_envs *E, const uint8_t *enc, const int32_t *agent, const int32_t *max_steps,
@@ -587,17 +621,9 @@ int mgdp_envs_load(mgdp_envs *E, const uint8_t *enc, const int32_t *agent, const
     }
     std::vector<int32_t> ms(max_steps, max_steps + B);
     std::vector<uint8_t> se(see_through, see_through + B);
-    if (E->d_cont) {  // new grids hold no contents until mgdp_envs_set_contents says so
-        if (!mask) {
-            MGDP_HIP(hipMemsetAsync(E->d_cont, 0, (size_t)B * HWp, E->stream));
-            MGDP_HIP(hipMemsetAsync(E->d_ccont, 0, (size_t)B, E->stream));
-        } else {
-            for (int b = 0; b < B; ++b) {
-                if (!mask[b]) continue;
-                MGDP_HIP(hipMemsetAsync(E->d_cont + (size_t)b * HWp, 0, HWp, E->stream));
-                MGDP_HIP(hipMemsetAsync(E->d_ccont + b, 0, 1, E->stream));
-            }
-        }
+    if (E->d_cont && !mask) {  // new grids hold no contents until mgdp_envs_set_contents says so
+        MGDP_HIP(hipMemsetAsync(E->d_cont, 0, (size_t)B * HWp, E->stream));
+        MGDP_HIP(hipMemsetAsync(E->d_ccont, 0, (size_t)B, E->stream));
     }
     if (!mask) {
         MGDP_HIP(hipMemcpyAsync(E->d_cell, cl.data(), cl.size(), hipMemcpyHostToDevice, E->stream));
@@ -606,15 +632,25 @@ int mgdp_envs_load(mgdp_envs *E, const uint8_t *enc, const int32_t *agent, const
         MGDP_HIP(hipMemcpyAsync(E->d_max, ms.data(), ms.size() * 4, hipMemcpyHostToDevice, E->stream));
         MGDP_HIP(hipMemcpyAsync(E->d_see, se.data(), se.size(), hipMemcpyHostToDevice, E->stream));
     } else {
-        for (int b = 0; b < B; ++b) {
-            if (!mask[b]) continue;
-            const size_t o = (size_t)b * HWp;
-            MGDP_HIP(hipMemcpyAsync(E->d_cell + o, &cl[o], HWp, hipMemcpyHostToDevice, E->stream));
-            MGDP_HIP(hipMemcpyAsync(E->d_agent + 4 * b, &ag[4 * b], 16, hipMemcpyHostToDevice, E->stream));
-            MGDP_HIP(hipMemcpyAsync(E->d_carry + 2 * b, &cr[2 * b], 8, hipMemcpyHostToDevice, E->stream));
-            MGDP_HIP(hipMemcpyAsync(E->d_max + b, &ms[b], 4, hipMemcpyHostToDevice, E->stream));
-            MGDP_HIP(hipMemcpyAsync(E->d_see + b, &se[b], 1, hipMemcpyHostToDevice, E->stream));
+        const size_t o_cells = (size_t)((2 * B + 15) / 16 * 16);
+        const size_t need = o_cells + (size_t)B * HWp + sizeof(int32_t) * 7 * (size_t)B;
+        std::vector<uint8_t> st(need, 0);
+        std::memcpy(st.data(), mask, B);
+        std::memcpy(st.data() + B, se.data(), B);
+        std::memcpy(st.data() + o_cells, cl.data(), cl.size());
+        std::memcpy(st.data() + o_cells + (size_t)B * HWp, ag.data(), ag.size() * 4);
+        std::memcpy(st.data() + o_cells + (size_t)B * HWp + ag.size() * 4, cr.data(), cr.size() * 4);
+        std::memcpy(st.data() + o_cells + (size_t)B * HWp + ag.size() * 4 + cr.size() * 4, ms.data(), ms.size() * 4);
+        if (E->stage_bytes < need) {
+            if (E->d_stage) MGDP_HIP(hipFree(E->d_stage));
+            E->d_stage = nullptr;
+            MGDP_HIP(hipMalloc((void **)&E->d_stage, need));
+            E->stage_bytes = need;
         }
+        MGDP_HIP(hipMemcpyAsync(E->d_stage, st.data(), need, hipMemcpyHostToDevice, E->stream));
+        hipLaunchKernelGGL(envs_masked_load_kernel, dim3(B), dim3(64), 0, E->stream, B, HWp, E->d_stage, E->d_cell,
+                           E->d_agent, E->d_carry, E->d_max, E->d_see, E->d_cont, E->d_ccont);
+        MGDP_HIP(hipGetLastError());
     }
     MGDP_HIP(hipStreamSynchronize(E->stream));
     return 0;

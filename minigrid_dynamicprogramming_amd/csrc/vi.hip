@@ -30,6 +30,7 @@
 // 8 lanes per state, wave shuffle max-reduce with the lowest action index winning ties.
 #include <hip/hip_ext.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -64,6 +65,13 @@ struct mgdp_vi {
     int8_t *d_pi = nullptr;
     int32_t *d_kenv = nullptr;
     int32_t *d_kexec = nullptr;  // per grid: the sweep it last computed (fixed-point grids keep theirs)
+    // learned dispatch (Geo::order / kprio): set up from d_kexec at the first solve of cells that were
+    // already solved once (MGDP_LEARN_ORDER=0 / MGDP_LEARN_PRIO=0 turn the parts off)
+    int32_t *d_order = nullptr;
+    bool order_valid = false;
+    int solves_since_load = 0;
+    int kprio[3] = {0, 0, 0};
+    bool learn_order = true, learn_prio = true;
     double *d_dvenv = nullptr;
     unsigned long long *d_shards = nullptr;
     unsigned long long *d_red = nullptr;    // fused reduction shards [64][4]
@@ -168,6 +176,8 @@ Geo make_geo(const mgdp_vi *vi) {
     g.pair = vi->pair;
     g.tol = vi->d.tol;
     g.kexec = vi->d_kexec;
+    g.order = vi->order_valid && vi->learn_order ? vi->d_order : nullptr;
+    for (int i = 0; i < 3; ++i) g.kprio[i] = vi->order_valid && vi->learn_prio ? vi->kprio[i] : 0;
     return g;
 }
 
@@ -1040,6 +1050,8 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     if (const char *ev = std::getenv("MGDP_SWEEP_BLOCK")) vi->sweep_block = std::min(256, std::max(64, std::atoi(ev) / 64 * 64));
     if (const char *ev = std::getenv("MGDP_PERSISTENT")) vi->persistent = std::atoi(ev) != 0;
     if (const char *ev = std::getenv("MGDP_CHAIN")) vi->chain = std::atoi(ev) != 0;
+    if (const char *ev = std::getenv("MGDP_LEARN_ORDER")) vi->learn_order = std::atoi(ev) != 0;
+    if (const char *ev = std::getenv("MGDP_LEARN_PRIO")) vi->learn_prio = std::atoi(ev) != 0;
     if (const char *ev = std::getenv("MGDP_REDUCE_MULTI")) vi->reduce_multi = std::atoi(ev) != 0;
     if (const char *ev = std::getenv("MGDP_INKERNEL_MAX")) vi->inkernel_max = std::max(0, std::atoi(ev));
     // DoorKey (64-128 B of V per thread) measured slower on the register pipeline (5.38 -> 3.3 TB/s
@@ -1084,6 +1096,7 @@ int mgdp_vi_destroy(mgdp_vi *vi) {
     (void)hipFree(vi->d_pi);
     (void)hipFree(vi->d_kenv);
     (void)hipFree(vi->d_kexec);
+    (void)hipFree(vi->d_order);
     (void)hipFree(vi->d_dvenv);
     (void)hipFree(vi->d_shards);
     (void)hipFree(vi->d_red);
@@ -1134,6 +1147,8 @@ int mgdp_vi_load_cells(mgdp_vi *vi, const uint8_t *cells) {
     MGDP_HIP(hipStreamSynchronize(vi->stream));
     vi->cells_loaded = true;
     vi->k_done_valid = false;
+    vi->order_valid = false;
+    vi->solves_since_load = 0;
     return 0;
 }
 
@@ -1153,12 +1168,49 @@ int mgdp_vi_load_cells_device(mgdp_vi *vi, const uint8_t *d_cells) {
     MGDP_HIP(hipMemcpy2DAsync(vi->d_cells, vi->HWp, d_cells, vi->HW, vi->HW, vi->d.B, hipMemcpyDeviceToDevice, vi->stream));
     vi->cells_loaded = true;
     vi->k_done_valid = false;
+    vi->order_valid = false;
+    vi->solves_since_load = 0;
     return 0;
 }
+
+namespace {
+// Learned dispatch order (Geo::order / kprio): once the handle's cells have been solved, the sweeps
+// each grid executed (d_kexec) rank the grids -- longest first in dispatch order (an LPT schedule:
+// the launch's tail holds short grids, and at full residency every CU gets a stratified mix), and
+// the top 1 / 10 / 50 % raise their waves' issue priority.  Once per cells load (a D2H copy of B
+// words and a sort); V, pi and the sweep counts do not depend on it.
+constexpr int kLearnMinB = 1024;
+int learn_dispatch(mgdp_vi *vi) {
+    const int B = vi->d.B;
+    std::vector<int32_t> kx(B), idx(B);
+    MGDP_HIP(hipMemcpyAsync(kx.data(), vi->d_kexec, sizeof(int32_t) * (size_t)B, hipMemcpyDeviceToHost, vi->stream));
+    MGDP_HIP(hipStreamSynchronize(vi->stream));
+    for (int i = 0; i < B; ++i) idx[i] = i;
+    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return kx[a] > kx[b]; });
+    if (!vi->d_order) MGDP_HIP(hipMalloc((void **)&vi->d_order, sizeof(int32_t) * (size_t)B));
+    MGDP_HIP(hipMemcpyAsync(vi->d_order, idx.data(), sizeof(int32_t) * (size_t)B, hipMemcpyHostToDevice, vi->stream));
+    MGDP_HIP(hipStreamSynchronize(vi->stream));
+    const int t1 = kx[idx[B / 100]], t10 = kx[idx[B / 10]], t50 = kx[idx[B / 2]];
+    if (t50 > 0 && t1 > t50) {
+        vi->kprio[0] = t1;
+        vi->kprio[1] = std::max(t10, t50 + 1);
+        vi->kprio[2] = t50 + 1;
+    } else {
+        vi->kprio[0] = vi->kprio[1] = vi->kprio[2] = 0;  // no spread to exploit
+    }
+    vi->order_valid = true;
+    return 0;
+}
+}  // namespace
 
 int mgdp_vi_reset(mgdp_vi *vi) {
     MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
     DeviceGuard guard(vi->d.device);
+    if (!vi->order_valid && vi->solves_since_load > 0 && (vi->learn_order || vi->learn_prio) && vi->d.B >= kLearnMinB &&
+        vi->d.method == MGDP_METHOD_FUSED && !vi->opts && !serve_eligible(vi)) {
+        if (int rc = server_stop(vi)) return rc;
+        if (int rc = learn_dispatch(vi)) return rc;
+    }
     if (vi->d.method == MGDP_METHOD_SWEEP) {  // V_0 = 0 and an empty dV trace
         const size_t BS = (size_t)vi->d.B * vi->S;
         MGDP_HIP(hipMemsetAsync(vi->d_V[0], 0, BS * vi->tsize, vi->stream));
@@ -1414,6 +1466,7 @@ int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *con
         ++k;
     }
     if (int rc = mgdp_vi_finish(vi, k)) return rc;
+    ++vi->solves_since_load;
     vi->converged = vi->d.horizon > 0 ? 1 : dv < vi->d.tol;  // a finite horizon is exact after H sweeps
     if (sweeps_out) *sweeps_out = k;
     if (dv_out) *dv_out = dv;
@@ -1470,6 +1523,7 @@ int mgdp_vi_solve_sharded(mgdp_vi *vi, mgdp_comm *comm, int32_t *sweeps_out, dou
         vi->dv_red = dv;
     }
     if (int rc = mgdp_vi_finish(vi, k)) return rc;
+    ++vi->solves_since_load;
     vi->converged = dv < vi->d.tol;
     if (sweeps_out) *sweeps_out = k;
     if (dv_out) *dv_out = dv;

@@ -6,6 +6,9 @@
 
 namespace mgdp {
 constexpr int kWpDk1t = -100;  // vi_fused_kernel variant tag: batched DoorKey on one LDS tile
+// vi_fused_kernel variant tag: batched DoorKey grids of width 16 on whole-row thread maps, DPP
+// east / west fronts and two conflict-free LDS planes (fused_dk_rows; its own LDS layout, dkrow_*)
+constexpr int kWpDkRow = -800;
 // vi_fused_kernel variant tag: the direction-major one-thread-per-cell path alone.  The generic
 // variant (WP = 0) also holds the cell-major, pair and quad loops, and a kernel's VGPR budget is
 // that of its hungriest path: stripping them is what sets the batched kernels' occupancy.
@@ -40,9 +43,13 @@ __host__ __device__ constexpr bool wp_is_wave2n(int wp) { return wp <= kWpWave2n
 #ifndef MGDP_WAVE2N_MINW  // A/B builds: minimum waves per SIMD of the two-waves-per-grid kernels
 #define MGDP_WAVE2N_MINW 1
 #endif
+#ifndef MGDP_DKROW_MINW  // A/B builds: minimum waves per SIMD of fused_dk_rows (1 = the compiler's choice)
+#define MGDP_DKROW_MINW 1
+#endif
 template <typename T>
 __host__ __device__ constexpr int wave2_min_waves(int wp) {
-    return wp_is_wave2n(wp) ? MGDP_WAVE2N_MINW
+    return wp == kWpDkRow   ? MGDP_DKROW_MINW
+           : wp_is_wave2n(wp) ? MGDP_WAVE2N_MINW
            : (MGDP_WAVE2_W8 && wp_is_wave2(wp) && kWpWave2 - wp <= (sizeof(T) == 4 ? 2 : 1)) ? 8
            : (MGDP_WAVE2_P4_W6 && wp_is_wave2(wp) && sizeof(T) == 4 && kWpWave2 - wp == 4) ? 6
                                                                                             : 1;
@@ -54,9 +61,6 @@ constexpr int kWpDkHalf = -500;
 // vi_serve_kernel variant tag: the served lone deterministic XYD grid on fused_serve_xyd (east / west
 // fronts by DPP; <= 4 waves), fused_fast_xyd_soa for a grid whose wave edges do not allow it
 constexpr int kWpServeEw = -600;
-// vi_fused_kernel variant tag: batched DoorKey grids of width 16 on whole-row thread maps, DPP
-// east / west fronts and two conflict-free LDS planes (fused_dk_rows; its own LDS layout, dkrow_*)
-constexpr int kWpDkRow = -800;
 // MGDP_DK_PERM=0 (A/B builds): batched DoorKey grids keep thread t on cell t (no dk_class_perm)
 #ifndef MGDP_DK_PERM
 #define MGDP_DK_PERM 1
@@ -84,6 +88,14 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
 
     k = fresh ? 0 : kenv[e];
     dvl = fresh ? 0.0 : dvenv[e];
+    if (geo.kprio[2] > 0 && k_target < 0) {
+        // learned priority: the grids that ran longest last time get the SIMDs' issue slots first, so
+        // the launch's critical path (its longest grids) is not stretched by the short ones
+        const int kp = geo.kexec[e];
+        if (kp >= geo.kprio[0]) __builtin_amdgcn_s_setprio(3);
+        else if (kp >= geo.kprio[1]) __builtin_amdgcn_s_setprio(2);
+        else if (kp >= geo.kprio[2]) __builtin_amdgcn_s_setprio(1);
+    }
     // Fixed-point completion: a grid whose last sweep changed nothing (|dV| = 0 exactly, so
     // V_k == V_{k-1} bit for bit) reproduces V_k at every later sweep (a Jacobi sweep is a function
     // of V alone), and pi_{k'} = argmax on V_{k'-1} = pi_k: it is at sweep k_target already, with
@@ -337,7 +349,9 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
     double dvl;
     const bool lone = in_kernel_reduce && gridDim.x == 1;
     const bool work = fused_grid<T, MODEL, SLIP, MAP, false, WP>(geo, cf, cells, V, pi, kenv, dvenv, host_out, k_target,
-                                                                 fresh, lone, epoch, blockIdx.x, k, dvl, nullptr,
+                                                                 fresh, lone, epoch,
+                                                                 geo.order ? (int)geo.order[blockIdx.x] : (int)blockIdx.x,
+                                                                 k, dvl, nullptr,
                                                                  wp_is_wave2(WP) || wp_is_wave2n(WP) ? gk : nullptr);
     // a launch-wide-rule launch (wave2 with gk) reduces and publishes through its own counter tree
     const bool gk_pub = (wp_is_wave2(WP) || wp_is_wave2n(WP)) && gk != nullptr && k_target < 0 && !k_target_dev;

@@ -1649,53 +1649,59 @@ __device__ __forceinline__ void fused_dk_rows(const Geo &geo, const Coef<T> &cf,
     *reinterpret_cast<V4<T> *>(T0 + o3) = V4<T>{{A[12], A[13], A[14], A[15]}};
     __syncthreads();
     T diff = (T)0;
-    auto sweep = [&](const T *Tin, T *Tout, const T (&in)[16], T (&out)[16], const int par) -> bool {
-        if (LOCAL) {
-            if (k >= geo.max_sweeps) return false;
-            if (k > k_start) {  // the previous sweep's flags (<= 4 waves: one dword; else 16 bytes)
-                bool more;
-                if (HWs <= 256) more = *reinterpret_cast<const uint32_t *>(flags + (par ^ 1) * 16) != 0u;
-                else {
-                    const uint4 f4 = *reinterpret_cast<const uint4 *>(flags + (par ^ 1) * 16);
-                    more = (f4.x | f4.y | f4.z | f4.w) != 0u;
-                }
-                if (!more) return false;
-            }
-        } else if (k >= k_target) {
-            return false;
-        }
-        const V4<T> fS = *reinterpret_cast<const V4<T> *>(Tin + o1 + 64);  // cell c + 16, plane 1
-        const V4<T> fN = *reinterpret_cast<const V4<T> *>(Tin + o3 - 64);  // cell c - 16, plane 3
-        T fE[4], fW[4];
-#pragma unroll
-        for (int hd = 0; hd < 4; ++hd) {
-            fE[hd] = dpp_shl1_zero(in[hd]);
-            fW[hd] = dpp_shr1_zero(in[8 + hd]);
-        }
-        T d;
-        if (LOCAL || k + 1 == k_target) {
-            if (wcls == 0u) d = dk_rows_step<T, false, false, true>(tp.walk, q.f, ge, in, fE, fS, fW, fN, out);
-            else if (wcls == 1u) d = dk_rows_step<T, true, false, true>(tp.walk, q.f, ge, in, fE, fS, fW, fN, out);
-            else d = dk_rows_step<T, true, true, true>(tp.walk, q.f, ge, in, fE, fS, fW, fN, out);
-        } else {
-            if (wcls == 0u) d = dk_rows_step<T, false, false, false>(tp.walk, q.f, ge, in, fE, fS, fW, fN, out);
-            else if (wcls == 1u) d = dk_rows_step<T, true, false, false>(tp.walk, q.f, ge, in, fE, fS, fW, fN, out);
-            else d = dk_rows_step<T, true, true, false>(tp.walk, q.f, ge, in, fE, fS, fW, fN, out);
-        }
-        diff = d;
-        *reinterpret_cast<V4<T> *>(Tout + o1) = V4<T>{{out[4], out[5], out[6], out[7]}};
-        *reinterpret_cast<V4<T> *>(Tout + o3) = V4<T>{{out[12], out[13], out[14], out[15]}};
-        if (LOCAL) flag_write(d >= cf.tol, flags, par);
-        __syncthreads();
-        ++k;
-        return true;
-    };
     // at the stop: pos 0 = V_k in A, V_{k-1} in Bv and tile 1; pos 1 = V_k in Bv, V_{k-1} in A and tile 0
-    int pos;
-    while (true) {
-        if (!sweep(T0, T1, A, Bv, 0)) { pos = 0; break; }
-        if (!sweep(T1, T0, Bv, A, 1)) { pos = 1; break; }
-    }
+    int pos = 0;
+    // One sweep loop per wave form (the class is wave-uniform and fixed for the launch): the loop
+    // body is straight-line code, so the two register sets keep their registers across sweeps (a
+    // class switch inside the loop made the compiler merge the forms' outputs with copies).  Every
+    // loop takes the same barriers and the same (block-uniform) stop decisions.
+    auto run = [&](auto goal_c, auto kd_c) {
+        constexpr bool GOAL = decltype(goal_c)::value, KD = decltype(kd_c)::value;
+        auto sweep = [&](const T *Tin, T *Tout, const T (&in)[16], T (&out)[16], const int par) -> bool {
+            if (LOCAL) {
+                if (k >= geo.max_sweeps) return false;
+                if (k > k_start) {  // the previous sweep's flags (<= 4 waves: one dword; else 16 bytes)
+                    bool more;
+                    if (HWs <= 256) more = *reinterpret_cast<const uint32_t *>(flags + (par ^ 1) * 16) != 0u;
+                    else {
+                        const uint4 f4 = *reinterpret_cast<const uint4 *>(flags + (par ^ 1) * 16);
+                        more = (f4.x | f4.y | f4.z | f4.w) != 0u;
+                    }
+                    if (!more) return false;
+                }
+            } else if (k >= k_target) {
+                return false;
+            }
+            const V4<T> fS = *reinterpret_cast<const V4<T> *>(Tin + o1 + 64);  // cell c + 16, plane 1
+            const V4<T> fN = *reinterpret_cast<const V4<T> *>(Tin + o3 - 64);  // cell c - 16, plane 3
+            T fE[4], fW[4];
+#pragma unroll
+            for (int hd = 0; hd < 4; ++hd) {
+                fE[hd] = dpp_shl1_zero(in[hd]);
+                fW[hd] = dpp_shr1_zero(in[8 + hd]);
+            }
+            T d;
+            if (LOCAL) d = dk_rows_step<T, GOAL, KD, true>(tp.walk, q.f, ge, in, fE, fS, fW, fN, out);
+            else if (k + 1 == k_target) d = dk_rows_step<T, GOAL, KD, true>(tp.walk, q.f, ge, in, fE, fS, fW, fN, out);
+            else d = dk_rows_step<T, GOAL, KD, false>(tp.walk, q.f, ge, in, fE, fS, fW, fN, out);
+            diff = d;
+            *reinterpret_cast<V4<T> *>(Tout + o1) = V4<T>{{out[4], out[5], out[6], out[7]}};
+            *reinterpret_cast<V4<T> *>(Tout + o3) = V4<T>{{out[12], out[13], out[14], out[15]}};
+            if (LOCAL) flag_write(d >= cf.tol, flags, par);
+            __syncthreads();
+            ++k;
+            return true;
+        };
+        while (true) {
+            if (!sweep(T0, T1, A, Bv, 0)) { pos = 0; break; }
+            if (!sweep(T1, T0, Bv, A, 1)) { pos = 1; break; }
+        }
+    };
+    using Yes = std::integral_constant<bool, true>;
+    using No = std::integral_constant<bool, false>;
+    if (wcls == 0u) run(No{}, No{});
+    else if (wcls == 1u) run(Yes{}, No{});
+    else run(Yes{}, Yes{});
     dvl = (double)block_max(diff, slots, 0);
     done(k, dvl);
     T vk[16], vp[16];

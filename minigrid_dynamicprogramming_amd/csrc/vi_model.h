@@ -16,6 +16,12 @@ struct Geo {
     int pair;    // fused XYD: two-sweep step
     double tol;
     int32_t *kexec;  // per grid: the sweep index it last computed (mgdp_vi_get_grid_sweeps); nullptr = off
+    // Learned dispatch (round 5): when the same grids are solved again, workgroup b takes grid
+    // order[b] (longest previous solve first) and a grid whose previous solve ran >= kprio[i]
+    // sweeps raises its waves' issue priority to 3 - i (nullptr / 0: off).  Results do not depend
+    // on either: grids are independent.
+    const int32_t *order;
+    int kprio[3];
 };
 
 template <typename T>

@@ -159,3 +159,40 @@ def test_contents_are_validated():
     venv.L.mgdp_envs_set_state(venv.h, None, carry.ctypes.data, None, None)  # a new carry holds nothing
     assert not venv.get_contents()[1].any()
     venv.close()
+
+
+def test_masked_load_replaces_only_masked_envs():
+    """mgdp_envs_load with a mask (auto-reset of some envs; one staging copy + a scatter kernel):
+    the masked envs get the new grids, agents, max_steps, see_through, a cleared carry and no Box
+    contents; every other env keeps its state and contents byte for byte."""
+    B, W = 4096 + 5, 8
+    enc0, agent0, held0 = random_box_rooms(B, W, seed=11)
+    enc1, agent1, _ = random_box_rooms(B, W, seed=12)
+    venv = MiniGridVecEnv("MiniGrid-Empty-8x8-v0", B)
+    ms0 = np.full(B, 77, np.int32)
+    venv.load(enc0, agent0, max_steps=ms0, see_through=[False] * B, held=held0)
+    rng = np.random.default_rng(5)
+    for _ in range(7):  # move agents / carry things, so the kept envs' state is not the loaded one
+        venv.step(rng.integers(0, 7, B).astype(np.int32))
+    before = venv.get_state()
+    mask = (rng.random(B) < 0.3).astype(np.uint8)
+    ms1 = np.full(B, 55, np.int32)
+    venv.load(enc1, agent1, max_steps=ms1, see_through=[True] * B, mask=mask)
+    after = venv.get_state()
+    m = mask.astype(bool)
+    np.testing.assert_array_equal(after["enc"][m], enc1[m])
+    np.testing.assert_array_equal(after["agent"][m], agent1[m])
+    assert (after["carry"][m] == 0).all() and (after["step_count"][m] == 0).all()
+    assert (after["held"][m] == 0).all() and (after["carry_held"][m] == 0).all()
+    for k in ("enc", "agent", "carry", "step_count", "held", "carry_held"):
+        np.testing.assert_array_equal(after[k][~m], before[k][~m], err_msg=k)
+    # the masked envs step with their new max_steps / see_through: compare with a fresh handle
+    ref = MiniGridVecEnv("MiniGrid-Empty-8x8-v0", int(m.sum()))
+    ref.load(enc1[m], agent1[m], max_steps=ms1[m], see_through=[True] * int(m.sum()))
+    a = rng.integers(0, 7, B).astype(np.int32)
+    obs, rew, term, trunc, _ = venv.step(a)
+    robs, rrew, rterm, rtrunc, _ = ref.step(a[m])
+    np.testing.assert_array_equal(obs["image"][m], robs["image"])
+    np.testing.assert_array_equal(rew[m], rrew)
+    ref.close()
+    venv.close()
