@@ -66,12 +66,14 @@ struct mgdp_vi {
     int32_t *d_kenv = nullptr;
     int32_t *d_kexec = nullptr;  // per grid: the sweep it last computed (fixed-point grids keep theirs)
     // learned dispatch (Geo::order / kprio): set up from d_kexec at the first solve of cells that were
-    // already solved once (MGDP_LEARN_ORDER=0 / MGDP_LEARN_PRIO=0 turn the parts off)
+    // already solved once (MGDP_LEARN_ORDER=0 turns the order off, MGDP_LEARN_PRIO=1 the priority on)
     int32_t *d_order = nullptr;
     bool order_valid = false;
     int solves_since_load = 0;
     int kprio[3] = {0, 0, 0};
-    bool learn_order = true, learn_prio = true;
+    // measured (profiles/r05_ab2/): the order alone +3-6 % (LavaS11N5 x 8192 / x 65536, FourRooms x
+    // 4096, DoorKey-16 x 65536); the priority on top of it nothing or worse -- off by default
+    bool learn_order = true, learn_prio = false;
     double *d_dvenv = nullptr;
     unsigned long long *d_shards = nullptr;
     unsigned long long *d_red = nullptr;    // fused reduction shards [64][4]
@@ -115,6 +117,7 @@ struct mgdp_vi {
     int pair2 = 1;                // batched plain XYD with cpt 2: adjacent-cell pairs (MGDP_PAIR2=0: fused_fast_xyd_soa_xn)
     int wave2 = 0;                // batched plain XYD on one wave per grid: cells per lane P (fused_wave2_xyd; 0 = off)
     int wave2n = 0;               // ... on two waves per grid instead: blocks per wave PW (fused_wave2n_xyd; 0 = off)
+    int band = 0;                 // ... on column bands of this many rows instead (fused_band_xyd; MGDP_BAND)
     int sweep_block = 256;
     int sweep_m = 1;              // grids staged per workgroup iteration (measured: m>1 no faster)
     int sweep_pipe = 2;           // register-pipelined sweep kernel: grids fetched ahead (0 = staged kernel)
@@ -321,6 +324,21 @@ F pick_wave2(int P, F dflt) {
     }
     return dflt;
 }
+// The column-band instantiation for HB rows per band (1..8); `dflt` if out of range.
+template <template <typename, int, bool, int, int> class K, typename T, int MODEL, bool SLIP, int MAP, typename F>
+F pick_band(int HB, F dflt) {
+    switch (HB) {
+    case 1: return K<T, MODEL, SLIP, MAP, kWpBand - 1>::fn;
+    case 2: return K<T, MODEL, SLIP, MAP, kWpBand - 2>::fn;
+    case 3: return K<T, MODEL, SLIP, MAP, kWpBand - 3>::fn;
+    case 4: return K<T, MODEL, SLIP, MAP, kWpBand - 4>::fn;
+    case 5: return K<T, MODEL, SLIP, MAP, kWpBand - 5>::fn;
+    case 6: return K<T, MODEL, SLIP, MAP, kWpBand - 6>::fn;
+    case 7: return K<T, MODEL, SLIP, MAP, kWpBand - 7>::fn;
+    case 8: return K<T, MODEL, SLIP, MAP, kWpBand - 8>::fn;
+    default: return dflt;
+    }
+}
 // The two-waves-per-grid instantiation for PW blocks per wave (2..4); `dflt` if out of range.
 template <template <typename, int, bool, int, int> class K, typename T, int MODEL, bool SLIP, int MAP, typename F>
 F pick_wave2n(int PW, F dflt) {
@@ -396,6 +414,9 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
         if (vi->wave2n) {
             kern = pick_wave2n<FusedK, T, MODEL, SLIP, MAP>(vi->wave2n, kern);
             smem = wave2n_smem_bytes(vi->HWp, vi->d.W, 2 * vi->wave2n, (int)sizeof(T));
+        } else if (vi->band) {
+            kern = pick_band<FusedK, T, MODEL, SLIP, MAP>(vi->band, kern);
+            smem = 256 + (vi->HWp + 15) / 16 * 16;
         } else if (vi->wave2) {
             kern = pick_wave2<FusedK, T, MODEL, SLIP, MAP>(vi->wave2, kern);
             smem = wave2_smem_bytes(vi->HWp, vi->d.W, vi->wave2, (int)sizeof(T));
@@ -439,6 +460,7 @@ int launch_serve_t(mgdp_vi *vi, unsigned int served) {
         if (vi->cpt == 2) kern = ServeK<T, MODEL, SLIP, MAP, -2>::fn;
         if constexpr (!SLIP) {
             if (vi->serve_ew) kern = ServeK<T, MODEL, SLIP, MAP, kWpServeEw>::fn;
+            if (vi->band) kern = pick_band<ServeK, T, MODEL, SLIP, MAP>(vi->band, kern);
         }
     }
     if constexpr (MODEL == MGDP_MODEL_DOORKEY && MAP == MGDP_MAP_CELL && !SLIP) {
@@ -626,7 +648,7 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
 // Persistent solver hand-off (lone grid on the one-thread-per-cell fused path).
 bool serve_eligible(const mgdp_vi *vi) {
     return vi->persistent && !vi->opts && vi->d.method == MGDP_METHOD_FUSED && vi->d.B == 1 && vi->d.mapping == MGDP_MAP_CELL &&
-           (vi->HW <= vi->cpt * vi->fused_block || vi->wave_p) && !vi->pair && !vi->quad;
+           (vi->HW <= vi->cpt * vi->fused_block || vi->wave_p || vi->band) && !vi->pair && !vi->quad;
 }
 // Ask a resident server to leave and drain the stream.  Every entry point that enqueues other
 // work on the stream, or reads results, calls this first.  A grid handed over for the next request
@@ -926,13 +948,25 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
                 vi->wave2n = (vi->wave2 + 1) / 2;
                 vi->fused_block = 128;
             }
+            // Column bands instead of row-major blocks (fused_band_xyd: north / south fronts in
+            // registers, no LDS tile): MGDP_BAND=1 (A/B; off by default until measured per size)
+            int band_on = 0;
+            if (const char *ev = std::getenv("MGDP_BAND")) band_on = std::atoi(ev);
+            const int hb = band_rows(d.W, d.H);
+            if (band_on && !vi->wave2n && hb >= 1 && hb <= 8) vi->band = hb;
             // the in-launch reduction (GkCtx) when the batch is resident at once
             int gk_on = 1;
             if (const char *ev = std::getenv("MGDP_GK")) gk_on = std::atoi(ev);
             const bool f32 = d.dtype == MGDP_F32;
             const void *k2 = nullptr;
             int smem2 = 0;
-            if (vi->wave2n) {
+            if (vi->band) {
+                smem2 = 256 + (vi->HWp + 15) / 16 * 16;
+                k2 = f32 ? (const void *)pick_band<FusedK, float, MGDP_MODEL_XYD, false, MGDP_MAP_CELL>(
+                               vi->band, FusedK<float, MGDP_MODEL_XYD, false, MGDP_MAP_CELL, 0>::fn)
+                         : (const void *)pick_band<FusedK, double, MGDP_MODEL_XYD, false, MGDP_MAP_CELL>(
+                               vi->band, FusedK<double, MGDP_MODEL_XYD, false, MGDP_MAP_CELL, 0>::fn);
+            } else if (vi->wave2n) {
                 smem2 = wave2n_smem_bytes(vi->HWp, d.W, 2 * vi->wave2n, vi->tsize);
                 k2 = f32 ? (const void *)pick_wave2n<FusedK, float, MGDP_MODEL_XYD, false, MGDP_MAP_CELL>(
                                vi->wave2n, FusedK<float, MGDP_MODEL_XYD, false, MGDP_MAP_CELL, 0>::fn)
@@ -958,6 +992,19 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
         vi->serve_ew = serve_ew && d.B == 1 && d.model == MGDP_MODEL_XYD && d.method == MGDP_METHOD_FUSED &&
                        d.slip_p < 0.0 && !vi->pair && !vi->quad && !vi->opts && !vi->wave_p && vi->cpt == 1 &&
                        vi->fused_block <= 256 && vi->HWs >= vi->fused_block && 2 * vi->HWs >= 3 * padw;
+        // The served lone deterministic XYD grid on ONE wave in column bands (fused_band_xyd: no
+        // barrier, no LDS tile; MGDP_SERVE_BAND=1, A/B)
+        int serve_band = 0;
+        if (const char *ev = std::getenv("MGDP_SERVE_BAND")) serve_band = std::atoi(ev);
+        const int hb1 = band_rows(d.W, d.H);
+        if (serve_band && d.B == 1 && d.model == MGDP_MODEL_XYD && d.method == MGDP_METHOD_FUSED && d.slip_p < 0.0 &&
+            !vi->pair && !vi->quad && !vi->opts && hb1 >= 1 && hb1 <= 8) {
+            vi->band = hb1;
+            vi->serve_ew = 0;
+            vi->wave_p = 0;
+            vi->cpt = 1;
+            vi->fused_block = 64;
+        }
         int dk1t = 0;
         if (const char *ev = std::getenv("MGDP_DK_1T")) dk1t = std::atoi(ev) != 0;
         if (dk1t && d.B > 1 && d.model == MGDP_MODEL_DOORKEY && d.dtype == MGDP_F32 && d.method == MGDP_METHOD_FUSED &&
@@ -1615,12 +1662,14 @@ const char *mgdp_vi_variant(const mgdp_vi *vi) {
     if (vi->d.mapping == MGDP_MAP_SA) return "sa";
     if (serve_eligible(vi)) {
         if (vi->dkhalf) return "serve_dk_half";
+        if (vi->band) return "serve_band";
         if (vi->serve_ew) return "serve_ew";
         return vi->wave_p ? "serve_wave" : "serve";
     }
     if (vi->dkrow) return "dk_rows";
     if (vi->dkhalf) return "dk_half";
     if (vi->dk1t) return "dk_1t";
+    if (vi->band) return "band";
     if (vi->wave2n) return "wave2n";
     if (vi->wave2) return "wave2";
     if (vi->wave_p) return "wave";

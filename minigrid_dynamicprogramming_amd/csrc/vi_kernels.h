@@ -21,6 +21,10 @@ __host__ __device__ constexpr bool wp_is_pair(int wp) { return wp <= kWpPair - 1
 // (fused_wave2_xyd, its own compact LDS layout; vi_fused_kernel only).
 constexpr int kWpWave2 = -400;
 __host__ __device__ constexpr bool wp_is_wave2(int wp) { return wp <= kWpWave2 - 1 && wp >= kWpWave2 - 8; }
+// Tags -901 .. -908: batched deterministic XYD, one wave per grid in column bands of HB = -tag - 900
+// rows (fused_band_xyd; no LDS tile, vi_fused_kernel only).
+constexpr int kWpBand = -900;
+__host__ __device__ constexpr bool wp_is_band(int wp) { return wp <= kWpBand - 1 && wp >= kWpBand - 8; }
 // Tags -702 .. -704: batched deterministic XYD, TWO waves per grid, PW = -tag - 700 blocks of 64
 // cells per wave (fused_wave2n_xyd; 128-thread workgroups, vi_fused_kernel only).
 constexpr int kWpWave2n = -700;
@@ -125,6 +129,34 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
                                           GkCtx{gk, epoch, e, geo.B, host_out});
         else
             fused_wave2n_xyd<T, false, PW>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
+        if (threadIdx.x == 0) {
+            kenv[e] = k;
+            if (geo.kexec) geo.kexec[e] = k;
+            dvenv[e] = dvl;
+        }
+        return true;
+    }
+    if constexpr (wp_is_band(WP)) {  // LDS: slots, then the cells (no tile); served: the server's staged cells
+        static_assert(MODEL == MGDP_MODEL_XYD && !SLIP && MAP == MGDP_MAP_CELL, "band: plain XYD");
+        constexpr int HB = kWpBand - WP;
+        uint8_t *cl2 = SERVED ? reinterpret_cast<uint8_t *>(smem + L.cells_off()) : smem + 256;
+        if (!SERVED) {
+            copy16(cl2, cells + (long long)e * geo.HWp, geo.HWp);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its LDS writes are ordered
+        }
+        auto done2 = [&](int kk, double dv) {
+            if (SERVED) {
+                if (threadIdx.x == 0) publish_tagged(host_out, kk, dv, epoch);
+            } else if (lone && threadIdx.x == 0) {
+                publish(host_out, (unsigned long long)kk, (unsigned long long)__double_as_longlong(dv),
+                        (unsigned long long)kk, epoch);
+            }
+        };
+        if (k_target < 0)
+            fused_band_xyd<T, true, HB>(geo, cf, cl2, V + vb, V + vb, pi + vb, k, k_target, dvl, done2,
+                                        GkCtx{gk, epoch, e, geo.B, host_out});
+        else
+            fused_band_xyd<T, false, HB>(geo, cf, cl2, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
         if (threadIdx.x == 0) {
             kenv[e] = k;
             if (geo.kexec) geo.kexec[e] = k;
@@ -323,7 +355,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
 // WP > 0: the one-wave lone-grid variant (fused_wave_xyd), 64 threads, so its WP cells per lane
 // may use the whole register file.
 template <typename T, int MODEL, bool SLIP, int MAP, int WP = 0>
-__global__ void __launch_bounds__(WP > 0 || wp_is_wave2(WP) ? 64 : (wp_is_wave2n(WP) ? 128 : 1024), wave2_min_waves<T>(WP))
+__global__ void __launch_bounds__(WP > 0 || wp_is_wave2(WP) || wp_is_band(WP) ? 64 : (wp_is_wave2n(WP) ? 128 : 1024), wave2_min_waves<T>(WP))
 vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
@@ -332,7 +364,7 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
                 unsigned long long *__restrict__ host_mirror, unsigned long long *__restrict__ gk) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
-    T *slots = reinterpret_cast<T *>(smem + (wp_is_wave2(WP) || wp_is_wave2n(WP) || WP == kWpDkRow ? 0 : L.slots_off()));
+    T *slots = reinterpret_cast<T *>(smem + (wp_is_wave2(WP) || wp_is_wave2n(WP) || wp_is_band(WP) || WP == kWpDkRow ? 0 : L.slots_off()));
     // multi-GPU protocol (mgdp_vi_run_to_dev): the target sweep is the all-reduced K in device
     // memory, written by a collective ordered before this launch on the stream
     if (k_target_dev) {
@@ -352,9 +384,9 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
                                                                  fresh, lone, epoch,
                                                                  geo.order ? (int)geo.order[blockIdx.x] : (int)blockIdx.x,
                                                                  k, dvl, nullptr,
-                                                                 wp_is_wave2(WP) || wp_is_wave2n(WP) ? gk : nullptr);
+                                                                 wp_is_wave2(WP) || wp_is_wave2n(WP) || wp_is_band(WP) ? gk : nullptr);
     // a launch-wide-rule launch (wave2 with gk) reduces and publishes through its own counter tree
-    const bool gk_pub = (wp_is_wave2(WP) || wp_is_wave2n(WP)) && gk != nullptr && k_target < 0 && !k_target_dev;
+    const bool gk_pub = (wp_is_wave2(WP) || wp_is_wave2n(WP) || wp_is_band(WP)) && gk != nullptr && k_target < 0 && !k_target_dev;
     if (in_kernel_reduce && !gk_pub)
         fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16), epoch, work);
 }

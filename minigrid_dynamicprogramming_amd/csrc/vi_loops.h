@@ -1049,6 +1049,165 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
     }
 }
 
+// Batched deterministic XYD grids, one wave per grid, COLUMN BANDS (round 5): lane l = b*W + x owns
+// the HB cells (b*HB + j, x), j < HB, of column x in band b (nb = 64 / W bands of HB = ceil(H / nb)
+// rows).  A cell's north / south fronts are then the lane's own registers (the next / previous
+// slot) except across band edges, and its east / west fronts the neighbouring lanes (DPP wave
+// shifts; x = 0 and x = W - 1 are border walls, whose fronts do not matter), so a sweep moves two
+// values between lanes (ds_bpermute: the band-edge fronts) and touches no LDS tile at all --
+// fused_wave2_xyd's row-major blocks read 2P and write 2P LDS words per sweep, a round trip on
+// every sweep's critical path that left FourRooms x 4096 (4 waves per SIMD) stalled half the time.
+// Same one-multiply backup, geometric fronts (invalid states hold +0), goal reward, ballot stop
+// rule, uncommitted last sweep and per-action pi pass as fused_wave2_xyd: bit-identical V, pi and
+// sweep counts.  Grids with W <= 64 and ceil(H / (64 / W)) <= 8.
+template <typename T>
+__device__ __forceinline__ T lane_shfl(T v, int src) {  // lane src's v (ds_bpermute, no LDS memory)
+    if constexpr (sizeof(T) == 4) {
+        return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
+    } else {
+        const long long b = __double_as_longlong(v);
+        const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)b), hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b >> 32));
+        return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+    }
+}
+__host__ __device__ inline int band_rows(int W, int H) { return W > 64 ? 0 : (H + 64 / W - 1) / (64 / W); }
+
+template <typename T, bool LOCAL, int HB, typename Done>
+__device__ __forceinline__ void fused_band_xyd(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, const T *Vg,
+                                               T *Vg_out, int8_t *pig, int &k, int k_target, double &dvl,
+                                               const Done &done, const GkCtx gk = GkCtx{}) {
+    static_assert(HB >= 1 && HB <= 8, "goal bits: 4 per cell, 32 per lane");
+    const int lane = (int)threadIdx.x;
+    const int W = geo.W, nb = 64 / W;
+    const int band = lane / W, x = lane - band * W;
+    const bool lane_on = band < nb;
+    const int up = lane >= W ? lane - W : lane, dn = lane + W < 64 ? lane + W : lane;  // band-edge partners
+    T ge[HB];
+    uint32_t goal = 0;
+    int cix[HB];
+    T own[HB][4];
+#pragma unroll
+    for (int j = 0; j < HB; ++j) {
+        const int row = band * HB + j;
+        const bool on = lane_on && row < geo.H;
+        const int c = on ? row * W + x : -1;
+        cix[j] = c;
+        const int cc = on ? c : 0;  // idle slots shadow cell 0 (a wall) and never write HBM
+        const bool valid = xyd_free(cl[cc]);
+        ge[j] = valid ? cf.g : (T)0;
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+            goal |= (uint32_t)(valid && cl[valid ? cc + geo.off[d] : cc] == T_GOAL) << (4 * j + d);
+        const V4<T> v = (k == 0 || !on) ? V4<T>{{(T)0, (T)0, (T)0, (T)0}} : *reinterpret_cast<const V4<T> *>(Vg + cc * 4);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) own[j][d] = v.v[d];
+    }
+    uint32_t goal_slots = 0;  // per slot j: does any lane's cell have a goal ahead (a uniform branch)
+#pragma unroll
+    for (int j = 0; j < HB; ++j)
+        goal_slots |= (__builtin_amdgcn_ballot_w64(((goal >> (4 * j)) & 15u) != 0u) != 0ull ? 1u : 0u) << j;
+    const int k_start = k;
+    bool more = true;
+    T diff = (T)0;
+    // the four geometric fronts of every slot from a register set
+    auto fronts = [&](const T (&in)[HB][4], T (&FE)[HB], T (&FS)[HB], T (&FW)[HB], T (&FN)[HB]) {
+        const T s_edge = lane_shfl(in[0][1], dn);       // south of slot HB-1: next band's slot 0, plane 1
+        const T n_edge = lane_shfl(in[HB - 1][3], up);  // north of slot 0: previous band's slot HB-1, plane 3
+#pragma unroll
+        for (int j = 0; j < HB; ++j) {
+            FE[j] = dpp_shl1_zero(in[j][0]);
+            FW[j] = dpp_shr1_zero(in[j][2]);
+            FS[j] = j + 1 < HB ? in[j + 1][1] : s_edge;
+            FN[j] = j > 0 ? in[j - 1][3] : n_edge;
+        }
+    };
+    auto sweep = [&](const T (&in)[HB][4], T (&out)[HB][4]) -> bool {  // `out` written only on commit
+        if (LOCAL) {
+            if (k >= geo.max_sweeps || (k > k_start && !more)) return false;
+        } else if (k >= k_target) {
+            return false;
+        }
+        T FE[HB], FS[HB], FW[HB], FN[HB];
+        fronts(in, FE, FS, FW, FN);
+        T o[HB][4];
+#pragma unroll
+        for (int j = 0; j < HB; ++j) {
+            const T m02 = vmax(in[j][0], in[j][2]), m13 = vmax(in[j][1], in[j][3]);
+            const T m[4] = {vmax(vmax(in[j][0], m13), FE[j]), vmax(vmax(in[j][1], m02), FS[j]),
+                            vmax(vmax(in[j][2], m13), FW[j]), vmax(vmax(in[j][3], m02), FN[j])};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[j][q] = ge[j] * m[q];
+        }
+#pragma unroll
+        for (int j = 0; j < HB; ++j) {
+            if ((goal_slots >> j) & 1u) {  // max(fl(g * m), 1): the goal's reward
+#pragma unroll
+                for (int q = 0; q < 4; ++q) o[j][q] = ((goal >> (4 * j + q)) & 1u) ? vmax(o[j][q], (T)1) : o[j][q];
+            }
+        }
+        T dm = (T)0;
+        if (LOCAL || MGDP_RUNTO_DV_ALL || k + 1 == k_target) {  // a k_target loop: |dV| of its last sweep only
+#pragma unroll
+            for (int j = 0; j < HB; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) dm = vmax(dm, vabs(o[j][q] - in[j][q]));
+        }
+        diff = dm;
+        if (LOCAL) more = __ballot(dm >= cf.tol) != 0ull;
+#pragma unroll
+        for (int j = 0; j < HB; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) out[j][q] = o[j][q];
+        ++k;
+        return true;
+    };
+    T alt[HB][4], prev[HB][4];
+    while (true) {
+        if (!sweep(own, alt)) {
+#pragma unroll
+            for (int j = 0; j < HB; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) prev[j][q] = alt[j][q];
+            break;
+        }
+        if (!sweep(alt, own)) {
+#pragma unroll
+            for (int j = 0; j < HB; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    prev[j][q] = own[j][q];
+                    own[j][q] = alt[j][q];
+                }
+            break;
+        }
+    }
+    dvl = (double)wave_max(diff);
+    if (LOCAL && gk.buf != nullptr) gk_exit(gk, k, dvl);  // this launch's reduction and its publication
+    done(k, dvl);
+    // pi of the last sweep = argmax on V_{k-1} (`prev`), per action with the usual topology
+    T FE[HB], FS[HB], FW[HB], FN[HB];
+    fronts(prev, FE, FS, FW, FN);
+#pragma unroll
+    for (int j = 0; j < HB; ++j) {
+        const int c = cix[j];
+        if (c >= 0) {
+            const XydTopo<T> tp = xyd_topo<T>(cl, geo, c);
+            const T front[4] = {FE[j], FS[j], FW[j], FN[j]};
+            V4<T> op, tmp;
+            T nbv[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                op.v[d] = prev[j][d];
+                nbv[d] = (tp.nbi[d] >> 2) != c ? front[d] : prev[j][d];  // blocked / terminal: own state
+            }
+            uint32_t pk;
+            xyd_step<T, false, true>(tp, cf, op, nbv, tmp, pk);
+            *reinterpret_cast<uint32_t *>(pig + c * 4) = pk;
+            *reinterpret_cast<V4<T> *>(Vg_out + c * 4) = V4<T>{{own[j][0], own[j][1], own[j][2], own[j][3]}};
+        }
+    }
+}
+
 // Batched deterministic XYD grids on TWO waves per grid (fused_wave2n_xyd): wave w owns blocks
 // w*PW .. w*PW + PW - 1 of the P = 2*PW 64-cell blocks, so a grid's sweep is two chains of PW
 // blocks instead of one of P -- for batches too small to fill the GPU with one wave per grid

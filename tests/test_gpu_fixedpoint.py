@@ -191,10 +191,11 @@ def test_capacity_batches_next_to_a_resident_server(delta):
 
 @pytest.mark.parametrize("env_id,B", [("MiniGrid-LavaCrossingS11N5-v0", 4096), ("MiniGrid-FourRooms-v0", 2048),
                                       ("MiniGrid-DoorKey-16x16-v0", 1024)])
-@pytest.mark.parametrize("learn", [{}, {"MGDP_LEARN_PRIO": "0"}, {"MGDP_LEARN_ORDER": "0"}])
+@pytest.mark.parametrize("learn", [{}, {"MGDP_LEARN_PRIO": "1"}, {"MGDP_LEARN_ORDER": "0", "MGDP_LEARN_PRIO": "1"}])
 def test_learned_dispatch_order_is_exact(env_id, B, learn):
     """From the second solve of the same cells on, workgroups take the grids longest-first (the
-    previous solve's executed sweeps) and the longest raise their issue priority: every solve, and a
+    previous solve's executed sweeps), optionally the longest raise their issue priority
+    (MGDP_LEARN_PRIO=1): every solve, and a
     solve after new cells (order dropped), equals the oracle's global loop; executed sweeps too."""
     cells = gen.generate(env_id, 0, B, enc=False, cells=True, agent=False)["cells"]
     model = 1 if "DoorKey" in env_id else 0
