@@ -851,8 +851,11 @@ def host_info():
         nproc = int(subprocess.run(["nproc"], capture_output=True, text=True, timeout=10).stdout.strip())
     except Exception:
         pass
+    from minigrid_dynamicprogramming_amd import _lib
+
     return {"nproc": nproc, "affinity_cpus": aff, "cores_used": cores, "cpu_model": model,
-            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "hip_runtime": _lib.hip_runtime()}  # which libamdhip64 serves libmgdp (torch's when imported first)
 
 
 def numpy_baseline(cells, model, gamma, tol, dtype, budget_s):

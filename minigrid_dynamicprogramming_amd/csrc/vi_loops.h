@@ -1707,11 +1707,18 @@ __host__ __device__ inline int dkrow_smem_bytes(int HWp, int HWs, int tsize) {
 
 // Value sweep of one DoorKey cell from geometric fronts (fE / fW: the east / west neighbours' plane
 // 0 / 2 values, fS / fN: the south / north neighbours' plane 1 / 3 groups).  Candidates per state as
-// dk_step_fast (left, right, self, forward; KD: pickup / toggle targets), one multiply by ge.
+// dk_step_fast (left, right, self, forward; KD: pickup / toggle targets), one multiply.  KD waves:
+//  * pickup (key ahead, has_key 0) and unlocking (a closed door ahead, has_key 1, door_open 0) only
+//    apply where the geometric front is an invalid, +0 state (the key cell without the key, the door
+//    cell shut), so their target REPLACES the front value (one select, no extra max); only closing
+//    an open door (door_open 1: the open door ahead is walkable) is an extra candidate;
+//  * the cell's own invalid states (the key / door cells themselves) take ge4[hd] = 0 instead of g,
+//    so they yield +0 without a select -- except in waves that also add a goal reward (GOAL && KD),
+//    where max(0, 1) must be masked.
 template <typename T, bool GOAL, bool KD, bool DV>
-__device__ __forceinline__ T dk_rows_step(uint32_t walk, const uint32_t (&f)[4], T ge, const T (&in)[16],
-                                          const T (&fE)[4], const V4<T> &fS, const T (&fW)[4], const V4<T> &fN,
-                                          T (&out)[16]) {
+__device__ __forceinline__ T dk_rows_step(uint32_t walk, const uint32_t (&f)[4], T ge, const T (&ge4)[4],
+                                          const T (&in)[16], const T (&fE)[4], const V4<T> &fS, const T (&fW)[4],
+                                          const V4<T> &fN, T (&out)[16]) {
     T df[16];
 #pragma unroll
     for (int hd = 0; hd < 4; ++hd) {
@@ -1719,21 +1726,19 @@ __device__ __forceinline__ T dk_rows_step(uint32_t walk, const uint32_t (&f)[4],
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
             const int l = d * 4 + hd;
-            const T F = d == 0 ? fE[hd] : (d == 1 ? fS.v[hd] : (d == 2 ? fW[hd] : fN.v[hd]));
+            T F = d == 0 ? fE[hd] : (d == 1 ? fS.v[hd] : (d == 2 ? fW[hd] : fN.v[hd]));
             const T xS = in[l];
-            T M = vmax(vmax((d & 1) ? m02 : m13, xS), F);
+            const bool key = f[d] & 64u, door = f[d] & 128u;
             if (KD) {
-                const bool key = f[d] & 64u, door = f[d] & 128u;
-                const int hk = hd >> 1, dop = hd & 1;
-                T cand = (T)0;
-                if (!hk) cand = key ? in[d * 4 + 2 + dop] : cand;
-                if (dop) cand = door ? in[d * 4 + hk * 2] : cand;
-                else if (hk) cand = door ? in[d * 4 + 3] : cand;
-                M = vmax(M, cand);
+                if (hd == 0) F = key ? in[d * 4 + 2] : F;   // (hk 0, dop 0): pickup -> (hk 1, dop 0)
+                if (hd == 1) F = key ? in[d * 4 + 3] : F;   // (hk 0, dop 1): pickup -> (hk 1, dop 1)
+                if (hd == 2) F = door ? in[d * 4 + 3] : F;  // (hk 1, dop 0): unlock -> (hk 1, dop 1)
             }
-            T best = ge * M;
+            T M = vmax(vmax((d & 1) ? m02 : m13, xS), F);
+            if (KD && (hd & 1)) M = vmax(M, door ? in[d * 4 + (hd >> 1) * 2] : (T)0);  // close -> (hk, 0)
+            T best = (KD ? ge4[hd] : ge) * M;
             if (GOAL) best = vmax(best, (f[d] & 16u) ? (T)1 : (T)0);
-            if (KD) best = ((walk >> hd) & 1u) ? best : (T)0;
+            if (KD && GOAL) best = ((walk >> hd) & 1u) ? best : (T)0;
             out[l] = best;
             if (DV) df[l] = vabs(best - xS);
         }
@@ -1794,6 +1799,9 @@ __device__ __forceinline__ void fused_dk_rows(const Geo &geo, const Coef<T> &cf,
     const uint32_t cls = dk_fast_class(q);
     const uint32_t wcls = (__builtin_amdgcn_ballot_w64(cls & 1u) ? 1u : 0u) | (__builtin_amdgcn_ballot_w64(cls & 2u) ? 2u : 0u);
     const T ge = tp.walk != 0u ? cf.g : (T)0;
+    T ge4[4];  // per (has_key, door_open): g where the agent may stand, else 0
+#pragma unroll
+    for (int hd = 0; hd < 4; ++hd) ge4[hd] = ((tp.walk >> hd) & 1u) ? cf.g : (T)0;
     const int k_start = k;
     T *const T0 = tiles, *const T1 = tiles + 2 * PL * 4;
     const int o1 = (16 + c) * 4, o3 = (PL + 16 + c) * 4;  // own entries of planes 1 / 3 (T units)
@@ -1840,9 +1848,9 @@ __device__ __forceinline__ void fused_dk_rows(const Geo &geo, const Coef<T> &cf,
                 fW[hd] = dpp_shr1_zero(in[8 + hd]);
             }
             T d;
-            if (LOCAL) d = dk_rows_step<T, GOAL, KD, true>(tp.walk, q.f, ge, in, fE, fS, fW, fN, out);
-            else if (k + 1 == k_target) d = dk_rows_step<T, GOAL, KD, true>(tp.walk, q.f, ge, in, fE, fS, fW, fN, out);
-            else d = dk_rows_step<T, GOAL, KD, false>(tp.walk, q.f, ge, in, fE, fS, fW, fN, out);
+            if (LOCAL) d = dk_rows_step<T, GOAL, KD, true>(tp.walk, q.f, ge, ge4, in, fE, fS, fW, fN, out);
+            else if (k + 1 == k_target) d = dk_rows_step<T, GOAL, KD, true>(tp.walk, q.f, ge, ge4, in, fE, fS, fW, fN, out);
+            else d = dk_rows_step<T, GOAL, KD, false>(tp.walk, q.f, ge, ge4, in, fE, fS, fW, fN, out);
             diff = d;
             *reinterpret_cast<V4<T> *>(Tout + o1) = V4<T>{{out[4], out[5], out[6], out[7]}};
             *reinterpret_cast<V4<T> *>(Tout + o3) = V4<T>{{out[12], out[13], out[14], out[15]}};
