@@ -187,7 +187,7 @@ int mgdp_vi_resume(mgdp_vi *vi, const void *V, int32_t k, double dv, int32_t *sw
  *   -> [only if dv_own != 0: p[5] <- dv, all-reduce(MAX) p[5], host read]
  *   -> mgdp_vi_set_result(K, dv) -> (rare fallback: mgdp_vi_sweep + host all-reduces) -> finish.
  * A launch writes d_pub[0..3] = {max sweeps over the shard's grids, max|dV| as IEEE-754 bits
- * (non-negative doubles order like their bits), min sweeps, launch epoch}; run_local_dev only
+ * (non-negative doubles order like their bits), min sweeps, 0} (a device buffer carries no epoch); run_local_dev only
  * enqueues. */
 int mgdp_vi_run_local_dev(mgdp_vi *vi, int64_t *d_pub);
 /* Every grid to exactly the sweep *d_k (read on the device when the launch starts); enqueue only. */

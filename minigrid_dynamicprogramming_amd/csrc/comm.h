@@ -7,7 +7,7 @@
 namespace mgdp {
 // MAX all-reduce of n int64 words of device memory, in place, enqueued on `stream`.
 int comm_allreduce_max_dev(mgdp_comm *c, int64_t *d, size_t n, hipStream_t stream);
-// The communicator's device protocol buffer: int64[8] of device memory ({K, dV bits, kmin, epoch},
+// The communicator's device protocol buffer: int64[8] of device memory ({K, dV bits, kmin, 0},
 // [5] = dV(K) bits), and a pinned host word for the one-word collectives.
 int64_t *comm_proto(mgdp_comm *c);
 int64_t *comm_host_word(mgdp_comm *c);

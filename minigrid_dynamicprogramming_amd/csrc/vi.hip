@@ -77,13 +77,14 @@ struct mgdp_vi {
     double *d_dvenv = nullptr;
     unsigned long long *d_shards = nullptr;
     unsigned long long *d_red = nullptr;    // fused reduction shards [64][4]
-    unsigned long long *d_pub1 = nullptr;   // device copy of a run_local launch's {kmax, dV, kmin, epoch} (chained solve)
+    unsigned long long *d_pub1 = nullptr;   // device copy of a run_local launch's {kmax, dV, kmin, 0} (chained solve)
     bool chain = true;                      // batched fused solve: run_local -> run_to(K from device memory), one host wait (MGDP_CHAIN=0: two)
     int inkernel_max = kInKernelReduceMaxB; // batches up to this fold {k, dV} in the fused launch itself (MGDP_INKERNEL_MAX)
     unsigned int *d_ticket = nullptr;       // arrival ticket of the fused reduction
     bool reduce_multi = true;               // B > inkernel_max: vi_reduce_multi_kernel (MGDP_REDUCE_MULTI)
-    // host-mapped words (kHoutWords): [0..3] {kmax, dV bits, kmin, epoch} of a launch, [5..7] the
-    // server's tagged result, [8..9] trace stamps, [11] server exit word, [13] run_to mirror,
+    // host-mapped words (kHoutWords): [0..3] {kmax, dV hi, dV lo, kmin} of a launch (each tagged with
+    // its epoch), [5..7] the server's tagged result, [8..9] trace stamps, [11] server exit word,
+    // [12..13] the run_to mirror (tagged),
     // [16] request word and [17] its source word (their own 128-B line: the server polls the pair)
     unsigned long long *h_out = nullptr;
     unsigned long long *d_hout = nullptr;   // device alias of h_out
@@ -104,7 +105,7 @@ struct mgdp_vi {
     int fused_block = 256;
     int sweep_grid = 2048;
     int fresh = 1;          // next fused launch starts from V_0 = 0
-    unsigned int epoch = 0; // tag of the last fused launch; its result lands in h_out[3]
+    unsigned int epoch = 0; // tag of the last fused launch; its result lands in h_out[0..3]
     int nbuf = 2;                 // fused LDS V buffers (3 = two-sweep XYD step)
     int quad = 0;                 // fused XYD: 4 threads per cell
     int pair = 0;                 // fused XYD: two-sweep step
@@ -117,6 +118,11 @@ struct mgdp_vi {
     int pair2 = 1;                // batched plain XYD with cpt 2: adjacent-cell pairs (MGDP_PAIR2=0: fused_fast_xyd_soa_xn)
     int wave2 = 0;                // batched plain XYD on one wave per grid: cells per lane P (fused_wave2_xyd; 0 = off)
     int wave2n = 0;               // ... on two waves per grid instead: blocks per wave PW (fused_wave2n_xyd; 0 = off)
+    // ... mixed: two waves for the learned order's long grids, one for the rest (kWpMix; MGDP_MIX=1,
+    // fp32, P = wave2 in 2..6); nmix = the long grids (kexec >= mix_frac x the longest), set with the order
+    bool mix = false;
+    int nmix = 0;
+    double mix_frac = 0.75;
     int band = 0;                 // ... on column bands of this many rows instead (fused_band_xyd; MGDP_BAND)
     int sweep_block = 256;
     int sweep_m = 1;              // grids staged per workgroup iteration (measured: m>1 no faster)
@@ -150,10 +156,10 @@ struct mgdp_vi {
     unsigned long long clk_tag = 0;  // the last server launch whose clock words were added
     double clk_cycles = 0.0, clk_ticks = 0.0, clk_busy = 0.0, clk_solves = 0.0;
     long long clk_launches = 0;
-    // launch-wide global rule (GkCtx, fused_wave2_xyd): one launch per batched solve when every grid
-    // wave of the batch can be resident at once (MGDP_GK=0 turns it off)
+    // the in-launch reduction (GkCtx, the wave2 family): one launch per batched deterministic solve
+    // (MGDP_GK=0 turns it off)
     bool gk = false;
-    int gk_capacity = 0;          // resident workgroups of the wave2 kernel on this device
+    int gk_capacity = 0;          // resident workgroups of the wave2 kernel on this device (MGDP_GK=2)
     unsigned long long *d_gk = nullptr;
 };
 
@@ -181,6 +187,7 @@ Geo make_geo(const mgdp_vi *vi) {
     g.kexec = vi->d_kexec;
     g.order = vi->order_valid && vi->learn_order ? vi->d_order : nullptr;
     for (int i = 0; i < 3; ++i) g.kprio[i] = vi->order_valid && vi->learn_prio ? vi->kprio[i] : 0;
+    g.nmix = g.order && vi->mix ? vi->nmix : 0;
     return g;
 }
 
@@ -238,13 +245,20 @@ int timed_collect(mgdp_vi *vi) {
 
 // {kmax, dV, kmin} of a launch too large to reduce in itself: kRedShards workgroups on the
 // fused reduction's idle shards (MGDP_REDUCE_MULTI=0: the one-workgroup kernel)
+// The epoch of a launch whose result goes to the host-mapped words (never 0: publish() writes a
+// device buffer's raw words for epoch 0)
+inline unsigned int next_host_epoch(mgdp_vi *vi) {
+    if (++vi->epoch == 0u) ++vi->epoch;
+    return vi->epoch;
+}
+
 inline void launch_reduce(mgdp_vi *vi, unsigned long long *pub) {
     if (vi->reduce_multi)
         hipLaunchKernelGGL(vi_reduce_multi_kernel, dim3(kRedShards), dim3(256), 0, vi->stream, vi->d_kenv, vi->d_dvenv,
-                           vi->d.B, vi->d_red, vi->d_ticket, pub, vi->epoch);
+                           vi->d.B, vi->d_red, vi->d_ticket, pub, pub == vi->d_hout ? vi->epoch : 0u);
     else
         hipLaunchKernelGGL(vi_reduce_kernel, dim3(1), dim3(1024), 0, vi->stream, vi->d_kenv, vi->d_dvenv, vi->d.B,
-                           pub, vi->epoch);
+                           pub, pub == vi->d_hout ? vi->epoch : 0u);
 }
 
 template <typename T, int MODEL, bool SLIP, bool ND, int HMODE>
@@ -258,7 +272,7 @@ int launch_opts_t(mgdp_vi *vi, int k_target) {
     hipExtLaunchKernelGGL(kern, dim3(vi->d.B), dim3(vi->fused_block), L.total(), vi->stream, tp.a, tp.b, 0, g,
                           make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv, vi->d_dvenv,
                           vi->d_red, vi->d_ticket, vi->d_hout, k_target, vi->fresh,
-                          vi->d.B <= vi->inkernel_max ? 1 : 0, ++vi->epoch, (const T *)vi->d_rgoal, vi->d_pi_t);
+                          vi->d.B <= vi->inkernel_max ? 1 : 0, next_host_epoch(vi), (const T *)vi->d_rgoal, vi->d_pi_t);
     MGDP_HIP(hipGetLastError());
     vi->fresh = 0;
     if (vi->d.B > vi->inkernel_max) {
@@ -339,6 +353,21 @@ F pick_band(int HB, F dflt) {
     default: return dflt;
     }
 }
+// The mixed-wave-count instantiation for P blocks of 64 cells (2..6, fp32); `dflt` otherwise.
+template <template <typename, int, bool, int, int> class K, typename T, int MODEL, bool SLIP, int MAP, typename F>
+F pick_mix(int P, F dflt) {
+    if constexpr (std::is_same<T, float>::value) {
+        switch (P) {
+        case 2: return K<T, MODEL, SLIP, MAP, kWpMix - 2>::fn;
+        case 3: return K<T, MODEL, SLIP, MAP, kWpMix - 3>::fn;
+        case 4: return K<T, MODEL, SLIP, MAP, kWpMix - 4>::fn;
+        case 5: return K<T, MODEL, SLIP, MAP, kWpMix - 5>::fn;
+        case 6: return K<T, MODEL, SLIP, MAP, kWpMix - 6>::fn;
+        default: break;
+        }
+    }
+    return dflt;
+}
 // The two-waves-per-grid instantiation for PW blocks per wave (2..4); `dflt` if out of range.
 template <template <typename, int, bool, int, int> class K, typename T, int MODEL, bool SLIP, int MAP, typename F>
 F pick_wave2n(int PW, F dflt) {
@@ -367,8 +396,8 @@ F pick_dkhalf(int n, F dflt) {
     }
 }
 
-// pub: where the launch's {kmax, dV bits, kmin, epoch} go (default: the host-mapped words the host
-// polls; the multi-GPU device protocol passes a device buffer it all-reduces); k_dev: the target
+// pub: where the launch's {kmax, dV bits, kmin} go (default: the host-mapped words the host polls,
+// epoch-tagged; the multi-GPU device protocol passes a device buffer it all-reduces, raw); k_dev: the target
 // sweep read from device memory instead of k_target (mgdp_vi_run_to_dev).
 template <typename T, int MODEL, bool SLIP, int MAP>
 int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr, const long long *k_dev = nullptr,
@@ -411,7 +440,10 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
         if (vi->dkrow && !vi->dk1t && !vi->dkhalf) smem = dkrow_smem_bytes(vi->HWp, vi->HWs, (int)sizeof(T));
     }
     if constexpr (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL && !SLIP) {
-        if (vi->wave2n) {
+        if (vi->mix) {
+            kern = pick_mix<FusedK, T, MODEL, SLIP, MAP>(vi->wave2, kern);
+            smem = mix_smem_bytes(vi->HWp, vi->d.W, vi->wave2, (int)sizeof(T));
+        } else if (vi->wave2n) {
             kern = pick_wave2n<FusedK, T, MODEL, SLIP, MAP>(vi->wave2n, kern);
             smem = wave2n_smem_bytes(vi->HWp, vi->d.W, 2 * vi->wave2n, (int)sizeof(T));
         } else if (vi->band) {
@@ -438,7 +470,7 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
     hipExtLaunchKernelGGL(kern, dim3(vi->d.B), dim3(vi->fused_block), smem, vi->stream, tp.a, tp.b, 0, g,
                        make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv,
                        vi->d_dvenv, vi->d_red, vi->d_ticket, pub, k_target, vi->fresh,
-                       vi->d.B <= vi->inkernel_max ? 1 : 0, ++vi->epoch, k_dev, mirror, gk);
+                       vi->d.B <= vi->inkernel_max ? 1 : 0, pub == vi->d_hout ? next_host_epoch(vi) : 0u, k_dev, mirror, gk);
     MGDP_HIP(hipGetLastError());
     vi->fresh = 0;
     if (vi->d.B > vi->inkernel_max && !gk) {  // a launch-wide-rule launch publishes its own reduction
@@ -567,8 +599,8 @@ struct SweepF {
 
 // Read the reduction the last fused launch published to host-mapped memory: max k, max dV, min k.
 int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
-    // The last workgroup (or the reduce kernel) publishes {kmax, dV, kmin, epoch} to host-mapped
-    // memory; the persistent server publishes three epoch-tagged words instead.  Poll them rather
+    // The last workgroup (or the reduce kernel) publishes {kmax, dV hi, dV lo, kmin} to host-mapped
+    // memory as four epoch-tagged words; the persistent server publishes three (words 5..7).  Poll them rather
     // than synchronise the stream (lower completion latency); everything else stays stream-ordered.
     // Poll the stream now and then to surface faults -- and, in serving mode, to relaunch a server
     // that left before it saw the request.
@@ -576,7 +608,7 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
     const unsigned long long ep = (unsigned long long)vi->epoch;
     const bool tagged = vi->serving;
     auto ready = [&]() -> bool {
-        if (!tagged) return h[3] == ep;
+        if (!tagged) return (h[0] >> 32) == ep && (h[1] >> 32) == ep && (h[2] >> 32) == ep && (h[3] >> 32) == ep;
         return (h[5] >> 32) == ep && (h[6] >> 32) == ep && (h[7] >> 32) == ep;
     };
     int relaunches = 0;
@@ -632,9 +664,9 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
         km = kmin = h[5] & 0xffffffffull;
         dvb = ((h[6] & 0xffffffffull) << 32) | (h[7] & 0xffffffffull);
     } else {
-        km = h[0];
-        dvb = h[1];
-        kmin = h[2];
+        km = h[0] & 0xffffffffull;
+        dvb = ((h[1] & 0xffffffffull) << 32) | (h[2] & 0xffffffffull);
+        kmin = h[3] & 0xffffffffull;
     }
     std::memcpy(&vi->dv_red, (const void *)&dvb, sizeof(double));  // non-negative doubles order like their bits
     vi->k_min = (int)kmin;
@@ -948,13 +980,20 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
                 vi->wave2n = (vi->wave2 + 1) / 2;
                 vi->fused_block = 128;
             }
+            if (const char *ev = std::getenv("MGDP_MIX"))
+                vi->mix = std::atoi(ev) != 0 && !vi->wave2n && d.dtype == MGDP_F32 && vi->wave2 >= 2 && vi->wave2 <= 6;
+            if (const char *ev = std::getenv("MGDP_MIX_FRAC")) vi->mix_frac = std::atof(ev);
+            if (vi->mix) vi->fused_block = 128;
             // Column bands instead of row-major blocks (fused_band_xyd: north / south fronts in
             // registers, no LDS tile): MGDP_BAND=1 (A/B; off by default until measured per size)
             int band_on = 0;
             if (const char *ev = std::getenv("MGDP_BAND")) band_on = std::atoi(ev);
             const int hb = band_rows(d.W, d.H);
-            if (band_on && !vi->wave2n && hb >= 1 && hb <= 8) vi->band = hb;
-            // the in-launch reduction (GkCtx) when the batch is resident at once
+            if (band_on && !vi->wave2n && !vi->mix && hb >= 1 && hb <= 8) vi->band = hb;
+            // The in-launch reduction (GkCtx) -- round 5: for any batch size.  Since fixed-point
+            // completion no grid waits for another, so the counter tree needs no residency and a
+            // batch past it saves the reduce kernel (MGDP_GK=2: round 4's rule, resident batches only;
+            // MGDP_GK=0: never)
             int gk_on = 1;
             if (const char *ev = std::getenv("MGDP_GK")) gk_on = std::atoi(ev);
             const bool f32 = d.dtype == MGDP_F32;
@@ -966,6 +1005,10 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
                                vi->band, FusedK<float, MGDP_MODEL_XYD, false, MGDP_MAP_CELL, 0>::fn)
                          : (const void *)pick_band<FusedK, double, MGDP_MODEL_XYD, false, MGDP_MAP_CELL>(
                                vi->band, FusedK<double, MGDP_MODEL_XYD, false, MGDP_MAP_CELL, 0>::fn);
+            } else if (vi->mix) {
+                smem2 = mix_smem_bytes(vi->HWp, d.W, vi->wave2, vi->tsize);
+                k2 = (const void *)pick_mix<FusedK, float, MGDP_MODEL_XYD, false, MGDP_MAP_CELL>(
+                    vi->wave2, FusedK<float, MGDP_MODEL_XYD, false, MGDP_MAP_CELL, 0>::fn);
             } else if (vi->wave2n) {
                 smem2 = wave2n_smem_bytes(vi->HWp, d.W, 2 * vi->wave2n, vi->tsize);
                 k2 = f32 ? (const void *)pick_wave2n<FusedK, float, MGDP_MODEL_XYD, false, MGDP_MAP_CELL>(
@@ -982,7 +1025,7 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
             int per_cu = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k2, vi->fused_block, smem2) == hipSuccess)
                 vi->gk_capacity = per_cu * cus;
-            vi->gk = gk_on != 0 && d.B <= vi->gk_capacity;
+            vi->gk = gk_on == 1 || (gk_on == 2 && d.B <= vi->gk_capacity);
         }
         // The served lone deterministic XYD grid: east / west fronts by DPP, <= 4 waves (one dword
         // of stop flags); the two-plane padded tiles must fit the usual V buffers.
@@ -1245,6 +1288,13 @@ int learn_dispatch(mgdp_vi *vi) {
     } else {
         vi->kprio[0] = vi->kprio[1] = vi->kprio[2] = 0;  // no spread to exploit
     }
+    // mixed wave counts: the grids that ran >= mix_frac x the longest sweep on two waves (they are the
+    // first workgroups of the order just set)
+    vi->nmix = 0;
+    if (vi->mix && kx[idx[0]] > 0) {
+        const int thr = std::max(1, (int)std::ceil(vi->mix_frac * kx[idx[0]]));
+        while (vi->nmix < B && kx[idx[vi->nmix]] >= thr) ++vi->nmix;
+    }
     vi->order_valid = true;
     return 0;
 }
@@ -1374,22 +1424,34 @@ int mgdp_vi_run_to_dev_sync(mgdp_vi *vi, const int64_t *d_kdv, int32_t *k_out, d
     // The gate (one wave): with E = d_kdv[1] == 0 every grid of every rank stopped its own rule at an
     // exact fixed point, so every grid is at K already (fixed-point completion) and the gate
     // publishes the result {K, dV 0}; else it publishes "more" and run_to(K) follows.  Either way
-    // E goes to h_out[13] and the host waits on host-mapped words only.
+    // E goes to h_out[12..13] and the host waits on host-mapped words only.
     hipLaunchKernelGGL(vi_gate_kernel, dim3(1), dim3(64), 0, vi->stream, reinterpret_cast<const long long *>(d_kdv),
-                       vi->d_hout, ++vi->epoch);
+                       vi->d_hout, next_host_epoch(vi));
     MGDP_HIP(hipGetLastError());
     if (int rc = reduce_env(vi, &km, &dv)) return rc;
     if (vi->k_min != km) {
-        // result -> host-mapped words (reduce_env polls them), d_kdv[1] -> h_out[13] by the launch
+        // result -> host-mapped words (reduce_env polls them), d_kdv[1] -> h_out[12..13] by the launch
         if (int rc = dispatch<FusedF>(vi, 0, (unsigned long long *)nullptr, reinterpret_cast<const long long *>(d_kdv),
-                                      vi->d_hout + 13))
+                                      vi->d_hout + 12))
             return rc;
         if (int rc = reduce_env(vi, &km, &dv)) return rc;
     }
     MGDP_CHECK(vi->k_min == km, MGDP_E_INVALID, "run_to_dev_sync: grids ended at sweeps %d..%d, not at one common K",
                vi->k_min, km);
     vi->k_done = km;
-    const unsigned long long rb = vi->h_out[13];
+    // the mirror's two tagged words were stored with the result's (no order between them)
+    const volatile unsigned long long *h = vi->h_out;
+    const unsigned long long ep = (unsigned long long)vi->epoch;
+    for (uint64_t spin = 1; (h[12] >> 32) != ep || (h[13] >> 32) != ep; ++spin) {
+        if ((spin & 1023u) == 0u) {
+            const hipError_t q = hipStreamQuery(vi->stream);
+            if (q == hipSuccess && ((h[12] >> 32) != ep || (h[13] >> 32) != ep))
+                MGDP_CHECK(false, MGDP_E_HIP, "run_to_dev_sync: the launch finished without its E words (epoch %u)", vi->epoch);
+            if (q != hipSuccess && q != hipErrorNotReady) return hip_fail(q, "run_to_dev_sync", __FILE__, __LINE__);
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    const unsigned long long rb = ((h[12] & 0xffffffffull) << 32) | (h[13] & 0xffffffffull);
     double rule;
     std::memcpy(&rule, &rb, sizeof(double));
     if (k_out) *k_out = km;
@@ -1523,7 +1585,7 @@ int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *con
 
 // The sharded solve with the library's own collectives (include/mgdp.h, ABI 11): the device
 // protocol of distributed.py with RCCL called from here on the handle's stream instead of through
-// torch.distributed -- run_local_dev publishes {K_r, E_r bits, kmin, epoch} into the communicator's
+// torch.distributed -- run_local_dev publishes {K_r, E_r bits, kmin, 0} into the communicator's
 // device words, ncclAllReduce(MAX) of the first two is enqueued right behind it, the gate (or
 // run_to(K)) reads them on the device, and the host waits once on host-mapped words.  Only when
 // some grid anywhere stopped its own rule with dV > 0 (E != 0: slip, rounding, a cap) is dV(K)
@@ -1551,7 +1613,7 @@ int mgdp_vi_solve_sharded(mgdp_vi *vi, mgdp_comm *comm, int32_t *sweeps_out, dou
     DeviceGuard guard(vi->d.device);
     if (int rc = mgdp_vi_reset(vi)) return rc;
     int64_t *p = comm_proto(comm);
-    if (int rc = mgdp_vi_run_local_dev(vi, p)) return rc;                  // {K_r, E_r bits, kmin, epoch}
+    if (int rc = mgdp_vi_run_local_dev(vi, p)) return rc;                  // {K_r, E_r bits, kmin, 0}
     if (int rc = comm_allreduce_max_dev(comm, p, 2, vi->stream)) return rc;  // {K, E} over every rank
     int32_t k = 0;
     double dv = 0.0, rule = 0.0;
@@ -1670,6 +1732,7 @@ const char *mgdp_vi_variant(const mgdp_vi *vi) {
     if (vi->dkhalf) return "dk_half";
     if (vi->dk1t) return "dk_1t";
     if (vi->band) return "band";
+    if (vi->mix) return "mix";
     if (vi->wave2n) return "wave2n";
     if (vi->wave2) return "wave2";
     if (vi->wave_p) return "wave";

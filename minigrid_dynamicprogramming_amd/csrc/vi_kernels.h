@@ -29,6 +29,14 @@ __host__ __device__ constexpr bool wp_is_band(int wp) { return wp <= kWpBand - 1
 // cells per wave (fused_wave2n_xyd; 128-thread workgroups, vi_fused_kernel only).
 constexpr int kWpWave2n = -700;
 __host__ __device__ constexpr bool wp_is_wave2n(int wp) { return wp <= kWpWave2n - 2 && wp >= kWpWave2n - 4; }
+// Tags -1002 .. -1006 (fp32): batched deterministic XYD, P = -tag - 1000 blocks of 64 cells, 128-thread
+// workgroups with MIXED wave counts: the first Geo::nmix workgroups of the learned dispatch order
+// (the grids whose previous solve ran longest) sweep on two waves (fused_wave2n_xyd, PW = ceil(P / 2)
+// blocks each), every other grid on one (fused_wave2_xyd; its second wave leaves at once).  For
+// batches whose launch is set by a long tail of slow grids (an 8-way LavaS11N5 shard: median 24
+// sweeps, max 47): splitting a long grid's sweep chain over two waves shortens the tail.
+constexpr int kWpMix = -1000;
+__host__ __device__ constexpr bool wp_is_mix(int wp) { return wp <= kWpMix - 2 && wp >= kWpMix - 6; }
 // Minimum waves per SIMD the one-wave kernels are compiled for.  Left alone, the fp32 P <= 2
 // variants (LavaS11N5: 121 cells) take 57 VGPRs but 106 SGPRs, and the SGPRs cap them at 7 waves
 // per SIMD (28 workgroups / CU, 7168 grids resident): 8 makes the compiler fit 8 waves' SGPRs too
@@ -54,6 +62,7 @@ template <typename T>
 __host__ __device__ constexpr int wave2_min_waves(int wp) {
     return wp == kWpDkRow   ? MGDP_DKROW_MINW
            : wp_is_wave2n(wp) ? MGDP_WAVE2N_MINW
+           : (MGDP_WAVE2_W8 && wp_is_mix(wp) && kWpMix - wp <= 2) ? 8
            : (MGDP_WAVE2_W8 && wp_is_wave2(wp) && kWpWave2 - wp <= (sizeof(T) == 4 ? 2 : 1)) ? 8
            : (MGDP_WAVE2_P4_W6 && wp_is_wave2(wp) && sizeof(T) == 4 && kWpWave2 - wp == 4) ? 6
                                                                                             : 1;
@@ -112,6 +121,39 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     const bool work = k_target < 0 ? (!(k > 0 && dvl < geo.tol) && k < geo.max_sweeps) : (k < k_target);
     if (!work) return false;
     const long long vb = (long long)e * geo.S;
+    if constexpr (wp_is_mix(WP)) {  // two waves for the first nmix workgroups, one for the rest
+        static_assert(MODEL == MGDP_MODEL_XYD && !SLIP && MAP == MGDP_MAP_CELL && !SERVED, "mix: batched plain XYD");
+        constexpr int P = kWpMix - WP, PW = (P + 1) / 2;
+        uint8_t *cl2 = smem + 256;
+        copy16(cl2, cells + (long long)e * geo.HWp, geo.HWp);
+        T *tile = reinterpret_cast<T *>(smem + wave2_tile_off(geo.HWp));
+        auto done2 = [&](int kk, double dv) {
+            if (lone && threadIdx.x == 0)
+                publish(host_out, (unsigned long long)kk, (unsigned long long)__double_as_longlong(dv),
+                        (unsigned long long)kk, epoch);
+        };
+        if ((int)blockIdx.x < geo.nmix) {  // workgroup-uniform: both waves are here
+            __syncthreads();
+            if (k_target < 0)
+                fused_wave2n_xyd<T, true, PW>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2,
+                                              GkCtx{gk, epoch, e, geo.B, host_out});
+            else
+                fused_wave2n_xyd<T, false, PW>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
+        } else {  // wave 0 alone (vi_fused_kernel let wave 1 go)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (k_target < 0)
+                fused_wave2_xyd<T, true, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2,
+                                            GkCtx{gk, epoch, e, geo.B, host_out});
+            else
+                fused_wave2_xyd<T, false, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
+        }
+        if (threadIdx.x == 0) {
+            kenv[e] = k;
+            if (geo.kexec) geo.kexec[e] = k;
+            dvenv[e] = dvl;
+        }
+        return true;
+    }
     if constexpr (wp_is_wave2n(WP)) {  // two waves per grid: cells, then two N/S tiles (wave2n_*)
         static_assert(MODEL == MGDP_MODEL_XYD && !SLIP && MAP == MGDP_MAP_CELL && !SERVED, "wave2n: batched plain XYD");
         constexpr int PW = kWpWave2n - WP;
@@ -355,7 +397,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
 // WP > 0: the one-wave lone-grid variant (fused_wave_xyd), 64 threads, so its WP cells per lane
 // may use the whole register file.
 template <typename T, int MODEL, bool SLIP, int MAP, int WP = 0>
-__global__ void __launch_bounds__(WP > 0 || wp_is_wave2(WP) || wp_is_band(WP) ? 64 : (wp_is_wave2n(WP) ? 128 : 1024), wave2_min_waves<T>(WP))
+__global__ void __launch_bounds__(WP > 0 || wp_is_wave2(WP) || wp_is_band(WP) ? 64 : (wp_is_wave2n(WP) || wp_is_mix(WP) ? 128 : 1024), wave2_min_waves<T>(WP))
 vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ red, unsigned int *__restrict__ ticket,
@@ -364,18 +406,20 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
                 unsigned long long *__restrict__ host_mirror, unsigned long long *__restrict__ gk) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
-    T *slots = reinterpret_cast<T *>(smem + (wp_is_wave2(WP) || wp_is_wave2n(WP) || wp_is_band(WP) || WP == kWpDkRow ? 0 : L.slots_off()));
+    constexpr bool kOwnLds = wp_is_wave2(WP) || wp_is_wave2n(WP) || wp_is_band(WP) || wp_is_mix(WP);  // wave2-family layouts, gk
+    T *slots = reinterpret_cast<T *>(smem + (kOwnLds || WP == kWpDkRow ? 0 : L.slots_off()));
+    // a one-wave grid of a mixed launch: its second wave leaves before touching anything
+    if constexpr (wp_is_mix(WP))
+        if (threadIdx.x >= 64 && (int)blockIdx.x >= geo.nmix) return;
     // multi-GPU protocol (mgdp_vi_run_to_dev): the target sweep is the all-reduced K in device
     // memory, written by a collective ordered before this launch on the stream
     if (k_target_dev) {
         k_target = (int)k_target_dev[0];
         // mgdp_vi_run_to_dev_sync: the all-reduced word after K (the own-rule dV) goes to the host
-        // with this launch's result.  Stored before the block's reduction ticket (fused_reduce
-        // drains it first) or, past the in-kernel limit, before the reduce kernel runs: it is
-        // visible before the epoch word the host polls.
+        // with this launch's result, as two words tagged with this launch's epoch (the host waits
+        // for them as for the result's)
         if (host_mirror && blockIdx.x == 0 && threadIdx.x == 0)
-            __hip_atomic_store(host_mirror, (unsigned long long)k_target_dev[1], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
+            publish_word2(host_mirror, (unsigned long long)k_target_dev[1], epoch);
     }
     int k;
     double dvl;
@@ -384,9 +428,9 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
                                                                  fresh, lone, epoch,
                                                                  geo.order ? (int)geo.order[blockIdx.x] : (int)blockIdx.x,
                                                                  k, dvl, nullptr,
-                                                                 wp_is_wave2(WP) || wp_is_wave2n(WP) || wp_is_band(WP) ? gk : nullptr);
+                                                                 kOwnLds ? gk : nullptr);
     // a launch-wide-rule launch (wave2 with gk) reduces and publishes through its own counter tree
-    const bool gk_pub = (wp_is_wave2(WP) || wp_is_wave2n(WP) || wp_is_band(WP)) && gk != nullptr && k_target < 0 && !k_target_dev;
+    const bool gk_pub = kOwnLds && gk != nullptr && k_target < 0 && !k_target_dev;
     if (in_kernel_reduce && !gk_pub)
         fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16), epoch, work);
 }
@@ -660,7 +704,7 @@ __global__ void __launch_bounds__(64) vi_gate_kernel(const long long *__restrict
                                                      unsigned long long *__restrict__ host_out, unsigned int epoch) {
     if (threadIdx.x == 0) {
         const unsigned long long K = (unsigned long long)kdv[0], E = (unsigned long long)kdv[1];
-        __hip_atomic_store(host_out + 13, E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        publish_word2(host_out + 12, E, epoch);  // six tagged words, no drain between them
         publish(host_out, K, 0ull, E == 0 ? K : kGateMore, epoch);
     }
 }

@@ -183,14 +183,32 @@ constexpr int kInKernelReduceMaxB = 512;  // above this, a separate one-workgrou
 // publishes {kmax, dV bits, kmin} to host-mapped memory.
 __device__ __forceinline__ void publish(unsigned long long *host_out, unsigned long long km,
                                         unsigned long long dv, unsigned long long kn, unsigned int epoch) {
-    // The host polls host_out[3]; the three values are acknowledged (vmcnt drained) before the
-    // epoch word is stored, so the host sees them first.  No L2 write-back (release) is needed:
-    // V and pi are consumed only by later stream-ordered operations.
-    __hip_atomic_store(host_out + 0, km, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(host_out + 1, dv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(host_out + 2, kn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(host_out + 3, (unsigned long long)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (epoch == 0) {
+        // a device buffer (the multi-GPU protocol's / the chained solve's): raw {kmax, dV bits, kmin,
+        // 0}, read by stream-ordered launches and collectives only
+        __hip_atomic_store(host_out + 0, km, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(host_out + 1, dv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(host_out + 2, kn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(host_out + 3, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    // The host-mapped words: four 8-byte words, each tagged with the launch epoch in its high half
+    // ({kmax}, {dV bits 63..32}, {dV bits 31..0}, {kmin}), so they may land in any order and need
+    // no drain between them -- one PCIe write latency to the host instead of two (round 4 stored
+    // the values, drained them, then the epoch word).  The host waits until all four carry its
+    // epoch.  No L2 write-back (release) is needed: V and pi are consumed only by later
+    // stream-ordered operations.
+    const unsigned long long tag = (unsigned long long)epoch << 32;
+    __hip_atomic_store(host_out + 0, tag | (km & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host_out + 1, tag | (dv >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host_out + 2, tag | (dv & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host_out + 3, tag | (kn & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// A 64-bit value for the host as two epoch-tagged words (the run_to mirror of the protocol's E)
+__device__ __forceinline__ void publish_word2(unsigned long long *w, unsigned long long v, unsigned int epoch) {
+    const unsigned long long tag = (unsigned long long)epoch << 32;
+    __hip_atomic_store(w + 0, tag | (v >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(w + 1, tag | (v & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Persistent-server result: three 8-byte words, each tagged with the request epoch in its high half
@@ -788,7 +806,7 @@ __host__ __device__ inline int wave2_smem_bytes(int HWp, int W, int P, int tsize
 // 256 shard counters (by e % 256, each counter on its own 128-B line, so at most B / 256 arrivals
 // contend per line); a shard's last arrival folds its grids' slots into the shard's slots and draws
 // a ticket of the top counter, whose last arrival folds the shards and publishes {kmax, dV bits,
-// kmin, epoch}.  Slots are stored and loaded agent-scope (sc1) and every store is drained before
+// kmin}.  Slots are stored and loaded agent-scope (sc1) and every store is drained before
 // the ticket that announces it (MI355X_MICROARCH.md: inter-workgroup hand-off).  No grid waits for
 // another: a grid whose own rule stopped at an EXACT fixed point (|dV| = 0) is complete for every
 // later sweep index (fixed-point completion, see fused_grid), so the global rule needs no K here.
@@ -797,7 +815,7 @@ struct GkCtx {
     unsigned int epoch;
     int e;                    // grid (workgroup) index
     int B;                    // grids in the launch
-    unsigned long long *pub;  // where the launch's {kmax, dV bits, kmin, epoch} go (host-mapped or device)
+    unsigned long long *pub;  // where the launch's {kmax, dV bits, kmin} go (host-mapped: epoch-tagged; device: raw)
 };
 constexpr int kGkShards = 256;
 constexpr int kGkLine = 16;                                    // u64 words per 128-B line
@@ -1223,6 +1241,11 @@ __host__ __device__ inline int wave2n_smem_bytes(int HWp, int W, int P, int tsiz
     return wave2_tile_off(HWp) + 2 * wave2n_tile_elems(W, P) * tsize + 64;
 }
 template <int B> struct WaveBuf { static constexpr int value = B; };
+// A mixed launch (kWpMix): P blocks on one wave or 2 * ceil(P / 2) on two, the larger layout
+__host__ __device__ inline int mix_smem_bytes(int HWp, int W, int P, int tsize) {
+    const int a = wave2_smem_bytes(HWp, W, P, tsize), b = wave2n_smem_bytes(HWp, W, 2 * ((P + 1) / 2), tsize);
+    return a > b ? a : b;
+}
 
 template <typename T, bool LOCAL, int PW, typename Done>
 __device__ __forceinline__ void fused_wave2n_xyd(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *tile,

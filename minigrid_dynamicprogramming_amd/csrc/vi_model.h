@@ -22,6 +22,9 @@ struct Geo {
     // on either: grids are independent.
     const int32_t *order;
     int kprio[3];
+    // Mixed wave counts (round 5, fused_mix tags): the first nmix workgroups of the learned order
+    // (the grids whose previous solve ran longest) take two waves per grid, the rest one.
+    int nmix;
 };
 
 template <typename T>

@@ -22,7 +22,7 @@ second all-reduce is skipped, and a deterministic batch (the shortest-path value
 needs ONE collective per solve.
 
 Device protocol (RCCL, fused method): K and E never visit the host before run_to.  The shard's
-run_local launch publishes {k max, dV bits, k min, epoch} into an int64 buffer on the GPU, the
+run_local launch publishes {k max, dV bits, k min, 0} into an int64 buffer on the GPU, the
 all-reduce of its first two words runs on the same stream (ProcessGroupNCCL orders its stream after
 the current one and the current one after the collective), run_to reads K on the device and its
 result comes back through host-mapped memory with E (mgdp_vi_run_to_dev_sync): one host wait per
@@ -309,7 +309,7 @@ def _device_capable(vi, red) -> bool:
 def _device_protocol(vi, red):
     p = red.proto
     vi.reset()
-    vi.run_local_dev(red.p_local)         # {k max, own-rule dV bits, k min, epoch}
+    vi.run_local_dev(red.p_local)         # {k max, own-rule dV bits, k min, 0}
     red.max_(red.p_kd)                    # K = the slowest grid anywhere, E = the largest own-rule dV
     t = time.perf_counter()
     k, dv, rule = vi.run_to_dev_sync(red.p_kd)  # the gate (or run_to K); the solve's one host wait

@@ -338,7 +338,7 @@ class ValueIteration:
             self._bound_stream = int(stream_ptr)
 
     def run_local_dev(self, pub):
-        """pub: int64 CUDA tensor (or pointer) of 4 words <- {k max, dV bits, k min, epoch}."""
+        """pub: int64 CUDA tensor (or pointer) of 4 words <- {k max, dV bits, k min, 0}."""
         if getattr(self, "_rld_fn", None) is None:
             self._rld_fn = _lib.raw_fn("mgdp_vi_run_local_dev")
         rc = self._rld_fn(self.h, _lib.ptr(pub))
