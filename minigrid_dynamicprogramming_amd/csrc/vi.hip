@@ -990,11 +990,13 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
             if (const char *ev = std::getenv("MGDP_BAND")) band_on = std::atoi(ev);
             const int hb = band_rows(d.W, d.H);
             if (band_on && !vi->wave2n && !vi->mix && hb >= 1 && hb <= 8) vi->band = hb;
-            // The in-launch reduction (GkCtx) -- round 5: for any batch size.  Since fixed-point
-            // completion no grid waits for another, so the counter tree needs no residency and a
-            // batch past it saves the reduce kernel (MGDP_GK=2: round 4's rule, resident batches only;
-            // MGDP_GK=0: never)
-            int gk_on = 1;
+            // The in-launch reduction (GkCtx) while the batch is resident at once (MGDP_GK=2, the
+            // default).  Since fixed-point completion no grid waits for another, so the counter tree
+            // would work for any B (MGDP_GK=1), but past the resident capacity every grid's exit
+            // waits for its counter's atomic while the next grid could start: LavaS11N5 x 65536
+            // 153 vs 144-145 us per launch, Empty-16 x 65536 314-319 vs 309-312
+            // (profiles/r05_mix/) -- the reduce kernel is cheaper there.  MGDP_GK=0: never.
+            int gk_on = 2;
             if (const char *ev = std::getenv("MGDP_GK")) gk_on = std::atoi(ev);
             const bool f32 = d.dtype == MGDP_F32;
             const void *k2 = nullptr;

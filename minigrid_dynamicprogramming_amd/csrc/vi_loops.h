@@ -909,6 +909,7 @@ __device__ __forceinline__ void gk_exit(const GkCtx &g, int k_rep, double dv) {
     }
 }
 
+template <int B> struct WaveBuf { static constexpr int value = B; };
 template <typename T, bool LOCAL, int P, typename Done>
 __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *tile,
                                                 const T *Vg, T *Vg_out, int8_t *pig, int &k, int k_target,
@@ -947,20 +948,16 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
 #pragma unroll
     for (int j = 0; j < P; ++j)
         goal_blocks |= (__builtin_amdgcn_ballot_w64(((goal >> (4 * j)) & 15u) != 0u) != 0ull ? 1u : 0u) << j;
-    const int k_start = k;
-    bool more = true;
     T diff = (T)0;
-    auto sweep = [&](const T (&in)[P][4], T (&out)[P][4]) -> bool {  // `out` written only on commit
+    // One sweep in -> out; returns whether another follows (the caller ran at least one: fused_grid
+    // only calls with work to do).  The stop test ends the sweep that decides it, so at an exit the
+    // sweep's own operands are V_{k-1} (in) and V_k (out) -- no loop-carried copy of V_{k-1}.
+    auto sweep = [&](const T (&in)[P][4], T (&out)[P][4]) -> bool {
         T FS[P], FN[P];
 #pragma unroll
         for (int j = 0; j < P; ++j) {
             FS[j] = S1[j * 64 + lane + W];
             FN[j] = N3[j * 64 + lane - W];
-        }
-        if (LOCAL) {
-            if (k >= geo.max_sweeps || (k > k_start && !more)) return false;
-        } else if (k >= k_target) {
-            return false;
         }
         T R[P], L[P];
 #pragma unroll
@@ -1001,68 +998,64 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
                 for (int q = 0; q < 4; ++q) dm = vmax(dm, vabs(o[j][q] - in[j][q]));
         }
         diff = dm;
-        if (LOCAL) more = __ballot(dm >= cf.tol) != 0ull;
 #pragma unroll
         for (int j = 0; j < P; ++j)
 #pragma unroll
             for (int q = 0; q < 4; ++q) out[j][q] = o[j][q];
         ++k;
-        return true;
+        if (LOCAL) return k < geo.max_sweeps && __ballot(dm >= cf.tol) != 0ull;
+        return k < k_target;
     };
-    T alt[P][4], prev[P][4];
+    // Exit work (reduction, publication, pi pass, V store) on cur = V_k, prv = V_{k-1}.
+    auto finish = [&](const T (&cur)[P][4], const T (&prv)[P][4]) {
+        dvl = (double)wave_max(diff);
+        if (LOCAL && gk.buf != nullptr) gk_exit(gk, k, dvl);  // this launch's reduction and its publication
+        done(k, dvl);
+        // pi of the last sweep = argmax on V_{k-1} (`prv`), per action with the usual topology
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            S1[j * 64 + lane] = prv[j][1];
+            N3[j * 64 + lane] = prv[j][3];
+        }
+        asm volatile("" ::: "memory");
+        T R[P], L[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            R[j] = dpp_mov<0x134>(prv[j][0]);
+            L[j] = dpp_mov<0x13C>(prv[j][2]);
+        }
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int c = j * 64 + lane;
+            const T front[4] = {(j + 1 < P && lane == 63) ? R[j + 1] : R[j], S1[c + W],
+                                (j > 0 && lane == 0) ? L[j - 1] : L[j], N3[c - W]};
+            if (c < geo.HW) {
+                const XydTopo<T> tp = xyd_topo<T>(cl, geo, c);
+                V4<T> op, tmp;
+                T nbv[4];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    op.v[d] = prv[j][d];
+                    nbv[d] = (tp.nbi[d] >> 2) != c ? front[d] : prv[j][d];  // blocked / terminal: own state
+                }
+                uint32_t pk;
+                xyd_step<T, false, true>(tp, cf, op, nbv, tmp, pk);
+                *reinterpret_cast<uint32_t *>(pig + c * 4) = pk;
+                *reinterpret_cast<V4<T> *>(Vg_out + c * 4) = V4<T>{{cur[j][0], cur[j][1], cur[j][2], cur[j][3]}};
+            }
+        }
+    };
+    // Two sweeps per iteration with fixed roles (own -> alt -> own); each exit runs the exit work
+    // on its own roles.
+    T alt[P][4];
     while (true) {
         if (!sweep(own, alt)) {
-#pragma unroll
-            for (int j = 0; j < P; ++j)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) prev[j][q] = alt[j][q];
-            break;
+            finish(alt, own);
+            return;
         }
         if (!sweep(alt, own)) {
-#pragma unroll
-            for (int j = 0; j < P; ++j)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    prev[j][q] = own[j][q];
-                    own[j][q] = alt[j][q];
-                }
-            break;
-        }
-    }
-    dvl = (double)wave_max(diff);
-    if (LOCAL && gk.buf != nullptr) gk_exit(gk, k, dvl);  // this launch's reduction and its publication
-    done(k, dvl);
-    // pi of the last sweep = argmax on V_{k-1} (`prev`), per action with the usual topology
-#pragma unroll
-    for (int j = 0; j < P; ++j) {
-        S1[j * 64 + lane] = prev[j][1];
-        N3[j * 64 + lane] = prev[j][3];
-    }
-    asm volatile("" ::: "memory");
-    T R[P], L[P];
-#pragma unroll
-    for (int j = 0; j < P; ++j) {
-        R[j] = dpp_mov<0x134>(prev[j][0]);
-        L[j] = dpp_mov<0x13C>(prev[j][2]);
-    }
-#pragma unroll
-    for (int j = 0; j < P; ++j) {
-        const int c = j * 64 + lane;
-        const T front[4] = {(j + 1 < P && lane == 63) ? R[j + 1] : R[j], S1[c + W],
-                            (j > 0 && lane == 0) ? L[j - 1] : L[j], N3[c - W]};
-        if (c < geo.HW) {
-            const XydTopo<T> tp = xyd_topo<T>(cl, geo, c);
-            V4<T> op, tmp;
-            T nbv[4];
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                op.v[d] = prev[j][d];
-                nbv[d] = (tp.nbi[d] >> 2) != c ? front[d] : prev[j][d];  // blocked / terminal: own state
-            }
-            uint32_t pk;
-            xyd_step<T, false, true>(tp, cf, op, nbv, tmp, pk);
-            *reinterpret_cast<uint32_t *>(pig + c * 4) = pk;
-            *reinterpret_cast<V4<T> *>(Vg_out + c * 4) = V4<T>{{own[j][0], own[j][1], own[j][2], own[j][3]}};
+            finish(own, alt);
+            return;
         }
     }
 }
@@ -1240,7 +1233,6 @@ __host__ __device__ inline int wave2n_tile_elems(int W, int P) { return 2 * 64 *
 __host__ __device__ inline int wave2n_smem_bytes(int HWp, int W, int P, int tsize) {
     return wave2_tile_off(HWp) + 2 * wave2n_tile_elems(W, P) * tsize + 64;
 }
-template <int B> struct WaveBuf { static constexpr int value = B; };
 // A mixed launch (kWpMix): P blocks on one wave or 2 * ceil(P / 2) on two, the larger layout
 __host__ __device__ inline int mix_smem_bytes(int HWp, int W, int P, int tsize) {
     const int a = wave2_smem_bytes(HWp, W, P, tsize), b = wave2n_smem_bytes(HWp, W, 2 * ((P + 1) / 2), tsize);
@@ -1825,7 +1817,6 @@ __device__ __forceinline__ void fused_dk_rows(const Geo &geo, const Coef<T> &cf,
     T ge4[4];  // per (has_key, door_open): g where the agent may stand, else 0
 #pragma unroll
     for (int hd = 0; hd < 4; ++hd) ge4[hd] = ((tp.walk >> hd) & 1u) ? cf.g : (T)0;
-    const int k_start = k;
     T *const T0 = tiles, *const T1 = tiles + 2 * PL * 4;
     const int o1 = (16 + c) * 4, o3 = (PL + 16 + c) * 4;  // own entries of planes 1 / 3 (T units)
     T A[16], Bv[16];
@@ -1847,21 +1838,11 @@ __device__ __forceinline__ void fused_dk_rows(const Geo &geo, const Coef<T> &cf,
     // loop takes the same barriers and the same (block-uniform) stop decisions.
     auto run = [&](auto goal_c, auto kd_c) {
         constexpr bool GOAL = decltype(goal_c)::value, KD = decltype(kd_c)::value;
+        // One sweep in -> out; returns whether another follows (fused_grid calls with work to do, so
+        // the first always runs).  The stop test ends the sweep that decides it, right after its
+        // barrier: the exits then find V_{k-1} in the sweep's own input set (no copy of it carried
+        // through the loop -- round 4's test at the next sweep's start cost 12-24 VGPR moves per sweep).
         auto sweep = [&](const T *Tin, T *Tout, const T (&in)[16], T (&out)[16], const int par) -> bool {
-            if (LOCAL) {
-                if (k >= geo.max_sweeps) return false;
-                if (k > k_start) {  // the previous sweep's flags (<= 4 waves: one dword; else 16 bytes)
-                    bool more;
-                    if (HWs <= 256) more = *reinterpret_cast<const uint32_t *>(flags + (par ^ 1) * 16) != 0u;
-                    else {
-                        const uint4 f4 = *reinterpret_cast<const uint4 *>(flags + (par ^ 1) * 16);
-                        more = (f4.x | f4.y | f4.z | f4.w) != 0u;
-                    }
-                    if (!more) return false;
-                }
-            } else if (k >= k_target) {
-                return false;
-            }
             const V4<T> fS = *reinterpret_cast<const V4<T> *>(Tin + o1 + 64);  // cell c + 16, plane 1
             const V4<T> fN = *reinterpret_cast<const V4<T> *>(Tin + o3 - 64);  // cell c - 16, plane 3
             T fE[4], fW[4];
@@ -1880,11 +1861,18 @@ __device__ __forceinline__ void fused_dk_rows(const Geo &geo, const Coef<T> &cf,
             if (LOCAL) flag_write(d >= cf.tol, flags, par);
             __syncthreads();
             ++k;
-            return true;
+            if (LOCAL) {
+                if (k >= geo.max_sweeps) return false;
+                // this sweep's flags (<= 4 waves: one dword; else 16 bytes)
+                if (HWs <= 256) return *reinterpret_cast<const uint32_t *>(flags + par * 16) != 0u;
+                const uint4 f4 = *reinterpret_cast<const uint4 *>(flags + par * 16);
+                return (f4.x | f4.y | f4.z | f4.w) != 0u;
+            }
+            return k < k_target;
         };
         while (true) {
-            if (!sweep(T0, T1, A, Bv, 0)) { pos = 0; break; }
-            if (!sweep(T1, T0, Bv, A, 1)) { pos = 1; break; }
+            if (!sweep(T0, T1, A, Bv, 0)) { pos = 1; break; }
+            if (!sweep(T1, T0, Bv, A, 1)) { pos = 0; break; }
         }
     };
     using Yes = std::integral_constant<bool, true>;

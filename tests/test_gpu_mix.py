@@ -3,7 +3,7 @@ dispatch order puts the grids that ran longest first and the first nmix workgrou
 waves (fused_wave2n_xyd) while the rest stay on one (fused_wave2_xyd) -- against the oracle's
 literal global loop: sweeps, V, pi and per-grid executed sweeps bit for bit over repeated solves,
 every P = 2..6 class, every split fraction (0: all grids on two waves), run_to caps, and batches past
-the resident capacity (the in-launch reduction for any B)."""
+the resident capacity (the in-launch reduction for any B, MGDP_GK=1)."""
 import numpy as np
 import pytest
 
@@ -90,7 +90,8 @@ def test_mixed_waves_caps_and_protocol(ms, monkeypatch):
 @pytest.mark.parametrize("gk", ["1", "2", "0"])
 def test_inlaunch_reduction_past_capacity(gk, monkeypatch):
     """LavaS11N5 x 20000 (past the one-wave kernel's 8192 resident grids): the in-launch reduction for
-    any B (default), round 4's resident-only rule (MGDP_GK=2) and the reduce kernel (0) agree."""
+    any B (MGDP_GK=1), the resident-only rule (2, the default: the reduce kernel here) and the reduce
+    kernel (0) agree."""
     monkeypatch.setenv("MGDP_GK", gk)
     cells = gen.generate("MiniGrid-LavaCrossingS11N5-v0", 5, 20000, enc=False, cells=True, agent=False)["cells"]
     o = oracle.value_iteration(0, cells, dtype="f32", nthreads=16, fixed_point=True)
