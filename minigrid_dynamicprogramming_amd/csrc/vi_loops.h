@@ -909,6 +909,33 @@ __device__ __forceinline__ void gk_exit(const GkCtx &g, int k_rep, double dv) {
     }
 }
 
+#ifndef MGDP_WAVE2_PREFETCH  // A/B builds: 1 = fused_wave2_xyd reads the next sweep's fronts early
+#define MGDP_WAVE2_PREFETCH 0   // measured neutral (profiles/r05_pf/) and +9 VGPRs at P = 4
+#endif
+#ifndef MGDP_WAVE2_DVTREE  // A/B builds: 0 = fused_wave2_xyd folds |dV| in one running max
+#define MGDP_WAVE2_DVTREE 1
+#endif
+// max of |x_i| over N values as a tree of v_max3 (depth log3 N instead of a running max's N / 2:
+// max is exact and order-free, so the result is the same bits)
+template <int N, typename T>
+__device__ __forceinline__ T tree_max3(const T *x) {
+    if constexpr (N == 1) {
+        return x[0];
+    } else if constexpr (N == 2) {
+        return vmax(x[0], x[1]);
+    } else if constexpr (N == 3) {
+        return vmax(vmax(x[0], x[1]), x[2]);
+    } else {
+        constexpr int M = (N + 2) / 3;
+        T y[M];
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+            const int a = 3 * i;
+            y[i] = a + 2 < N ? vmax(vmax(x[a], x[a + 1]), x[a + 2]) : (a + 1 < N ? vmax(x[a], x[a + 1]) : x[a]);
+        }
+        return tree_max3<M, T>(y);
+    }
+}
 template <int B> struct WaveBuf { static constexpr int value = B; };
 template <typename T, bool LOCAL, int P, typename Done>
 __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *tile,
@@ -949,16 +976,24 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
     for (int j = 0; j < P; ++j)
         goal_blocks |= (__builtin_amdgcn_ballot_w64(((goal >> (4 * j)) & 15u) != 0u) != 0ull ? 1u : 0u) << j;
     T diff = (T)0;
-    // One sweep in -> out; returns whether another follows (the caller ran at least one: fused_grid
-    // only calls with work to do).  The stop test ends the sweep that decides it, so at an exit the
-    // sweep's own operands are V_{k-1} (in) and V_k (out) -- no loop-carried copy of V_{k-1}.
-    auto sweep = [&](const T (&in)[P][4], T (&out)[P][4]) -> bool {
-        T FS[P], FN[P];
+    // The north / south fronts of the sweep about to run.  With MGDP_WAVE2_PREFETCH a sweep reads the
+    // next sweep's right after storing its own planes, so the LDS round trip overlaps its |dV|
+    // reduction, stop ballot and branch instead of opening the next sweep (the reads of a sweep
+    // that turns out to be the last are simply unused).
+    T FS[P], FN[P];
+    auto read_fronts = [&]() {
 #pragma unroll
         for (int j = 0; j < P; ++j) {
             FS[j] = S1[j * 64 + lane + W];
             FN[j] = N3[j * 64 + lane - W];
         }
+    };
+    if (MGDP_WAVE2_PREFETCH) read_fronts();
+    // One sweep in -> out; returns whether another follows (the caller ran at least one: fused_grid
+    // only calls with work to do).  The stop test ends the sweep that decides it, so at an exit the
+    // sweep's own operands are V_{k-1} (in) and V_k (out) -- no loop-carried copy of V_{k-1}.
+    auto sweep = [&](const T (&in)[P][4], T (&out)[P][4]) -> bool {
+        if (!MGDP_WAVE2_PREFETCH) read_fronts();
         T R[P], L[P];
 #pragma unroll
         for (int j = 0; j < P; ++j) {
@@ -990,12 +1025,22 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
             N3[j * 64 + lane] = o[j][3];
         }
         asm volatile("" ::: "memory");
+        if (MGDP_WAVE2_PREFETCH) read_fronts();  // LDS is in order per wave: after this sweep's stores
         // a k_target loop reports |dV| of its last sweep only (a uniform branch)
         if (LOCAL || MGDP_RUNTO_DV_ALL || k + 1 == k_target) {
+            if (MGDP_WAVE2_DVTREE) {
+                T ad[4 * P];
 #pragma unroll
-            for (int j = 0; j < P; ++j)
+                for (int j = 0; j < P; ++j)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) dm = vmax(dm, vabs(o[j][q] - in[j][q]));
+                    for (int q = 0; q < 4; ++q) ad[4 * j + q] = vabs(o[j][q] - in[j][q]);
+                dm = tree_max3<4 * P, T>(ad);
+            } else {
+#pragma unroll
+                for (int j = 0; j < P; ++j)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) dm = vmax(dm, vabs(o[j][q] - in[j][q]));
+            }
         }
         diff = dm;
 #pragma unroll
