@@ -19,8 +19,11 @@ ARCH = os.environ.get("MGDP_ARCH", "gfx950")
 # multiplies and differences into v_pk_mul_f32 / v_pk_add_f32, which measured 5-23 % slower on
 # MI355X than the scalar form (FourRooms x 4096 1.33 -> 1.64e13 updates/s unpacked;
 # profiles/r03_slp_gk/).
+# --offload-compress: the gfx950 code objects go into the fatbin compressed (5.4 -> ~2 MB; the HIP
+# runtime inflates them once at load), so the library every GPU run pushes stays small.
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Xarch_device", "-fno-honor-nans",
-         "-Xarch_device", "-fno-slp-vectorize", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result"]
+         "-Xarch_device", "-fno-slp-vectorize", f"--offload-arch={ARCH}", "--offload-compress", "-Wall",
+         "-Wno-unused-result"]
 LIBS = ["-ldl"]
 
 

@@ -912,8 +912,8 @@ __device__ __forceinline__ void gk_exit(const GkCtx &g, int k_rep, double dv) {
 #ifndef MGDP_WAVE2_PREFETCH  // A/B builds: 1 = fused_wave2_xyd reads the next sweep's fronts early
 #define MGDP_WAVE2_PREFETCH 0   // measured neutral (profiles/r05_pf/) and +9 VGPRs at P = 4
 #endif
-#ifndef MGDP_WAVE2_DVTREE  // A/B builds: 0 = fused_wave2_xyd folds |dV| in one running max
-#define MGDP_WAVE2_DVTREE 1
+#ifndef MGDP_WAVE2_DVTREE  // A/B builds: 1 = fused_wave2_xyd folds |dV| as a v_max3 tree
+#define MGDP_WAVE2_DVTREE 0   // measured neutral (profiles/r05_tree/) and +9 VGPRs at P = 2, 4 (81 -> 90: 6 -> 5 waves)
 #endif
 // max of |x_i| over N values as a tree of v_max3 (depth log3 N instead of a running max's N / 2:
 // max is exact and order-free, so the result is the same bits)
