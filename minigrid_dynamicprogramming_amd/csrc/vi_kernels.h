@@ -55,12 +55,15 @@ __host__ __device__ constexpr bool wp_is_mix(int wp) { return wp <= kWpMix - 2 &
 #ifndef MGDP_WAVE2N_MINW  // A/B builds: minimum waves per SIMD of the two-waves-per-grid kernels
 #define MGDP_WAVE2N_MINW 1
 #endif
-#ifndef MGDP_DKROW_MINW  // A/B builds: minimum waves per SIMD of fused_dk_rows (1 = the compiler's choice)
-#define MGDP_DKROW_MINW 1
+// Minimum waves per SIMD of fp32 fused_dk_rows: 6 (80 VGPRs and 80 B of scratch, 6 grids per CU) measured
+// 1950-1960 vs 1992-1996 us per DoorKey-16 x 65536 solve at the compiler's 5 (100 VGPRs), neutral at
+// 8192 grids (profiles/r05_dkw6/).  A/B builds: 1 = the compiler's choice.
+#ifndef MGDP_DKROW_MINW
+#define MGDP_DKROW_MINW 6
 #endif
 template <typename T>
 __host__ __device__ constexpr int wave2_min_waves(int wp) {
-    return wp == kWpDkRow   ? MGDP_DKROW_MINW
+    return wp == kWpDkRow   ? (sizeof(T) == 4 ? MGDP_DKROW_MINW : 1)  // fp64 at 6 waves spills 492 B
            : wp_is_wave2n(wp) ? MGDP_WAVE2N_MINW
            : (MGDP_WAVE2_W8 && wp_is_mix(wp) && kWpMix - wp <= 2) ? 8
            : (MGDP_WAVE2_W8 && wp_is_wave2(wp) && kWpWave2 - wp <= (sizeof(T) == 4 ? 2 : 1)) ? 8
