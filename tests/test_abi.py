@@ -38,9 +38,55 @@ def test_abi_version_and_error_string():
     assert "null" in _lib.last_error()
 
 
-def test_code_object_targets_gfx950():
-    data = open(_lib.lib_path(), "rb").read()
-    assert b"gfx950" in data
+def _elf_section(path, name):
+    """Bytes of one section of a 64-bit little-endian ELF file."""
+    import struct
+
+    b = open(path, "rb").read()
+    shoff, = struct.unpack_from("<Q", b, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+    sh = [struct.unpack_from("<IIQQQQIIQQ", b, shoff + i * shentsize) for i in range(shnum)]
+    strtab = sh[shstrndx]
+    for s in sh:
+        nm = b[strtab[4] + s[0]:b.index(b"\0", strtab[4] + s[0])].decode()
+        if nm == name:
+            return b[s[4]:s[4] + s[5]]
+    raise KeyError(name)
+
+
+def test_code_object_targets_gfx950(tmp_path):
+    """Every offload bundle in the library's fatbin carries a gfx950 code object.  The bundles are
+    compressed (build.py: --offload-compress), so the target is read back by clang-offload-bundler."""
+    import shutil
+    import struct
+    import subprocess
+
+    fat = _elf_section(_lib.lib_path(), ".hip_fatbin")
+    starts, i = [], 0
+    while True:
+        hits = [x for x in (fat.find(b"CCOB", i), fat.find(b"__CLANG_OFFLOAD_BUNDLE__", i)) if x >= 0]
+        if not hits:
+            break
+        starts.append(min(hits))
+        i = min(hits) + 4
+    assert len(starts) >= 3  # vi, envs, gen (lib.cpp / comm.cpp carry no device code)
+    bundler = shutil.which("clang-offload-bundler") or "/opt/rocm/lib/llvm/bin/clang-offload-bundler"
+    for n, s in enumerate(starts):
+        if fat[s:s + 4] == b"CCOB":
+            ver = struct.unpack_from("<H", fat, s + 4)[0]
+            size = struct.unpack_from("<Q" if ver >= 3 else "<I", fat, s + 8)[0]
+        else:
+            size = (starts[n + 1] if n + 1 < len(starts) else len(fat)) - s
+        chunk = tmp_path / f"b{n}.bin"
+        chunk.write_bytes(fat[s:s + size])
+        if not os.path.exists(bundler):
+            if fat[s:s + 4] == b"CCOB":
+                pytest.skip("clang-offload-bundler not found: compressed bundles cannot be listed")
+            assert b"gfx950" in fat[s:s + size]
+            continue
+        out = subprocess.run([bundler, "--list", "--type=o", f"--input={chunk}"], capture_output=True, text=True,
+                             check=True).stdout
+        assert "hipv4-amdgcn-amd-amdhsa--gfx950" in out, out
 
 
 def test_desc_struct_layout_matches_header():
