@@ -1331,9 +1331,10 @@ __device__ __forceinline__ void fused_wave2n_xyd(const Geo &geo, const Coef<T> &
     for (int j = 0; j < PW; ++j)
         goal_blocks |= (__builtin_amdgcn_ballot_w64(((goal >> (4 * j)) & 15u) != 0u) != 0ull ? 1u : 0u) << j;
     __syncthreads();
-    const int k_start = k;
     T diff = (T)0;
-    // sweep k_start + i reads tile i & 1 and writes the other (b: compile-time in the unrolled pair)
+    // sweep k_start + i reads tile i & 1 and writes the other (b: compile-time in the unrolled pair).
+    // As fused_wave2_xyd: the stop test ends the sweep that decides it (both waves' flags, read
+    // right after its barrier), so at an exit V_{k-1} is the sweep's own input set.
     auto sweep = [&](auto bc, const T (&in)[PW][4], T (&out)[PW][4]) -> bool {
         constexpr int b = decltype(bc)::value;
         const T *const N3r = tile + b * TS + padw, *const S1r = N3r + 64 * P;
@@ -1346,12 +1347,6 @@ __device__ __forceinline__ void fused_wave2n_xyd(const Geo &geo, const Coef<T> &
             FN[j] = N3r[c - W];
         }
         const T eE = edge[2 * b], eW = edge[2 * b + 1];
-        const uint32_t fl = flag[2 * b] | flag[2 * b + 1];
-        if (LOCAL) {
-            if (k >= geo.max_sweeps || (k > k_start && fl == 0u)) return false;
-        } else if (k >= k_target) {
-            return false;
-        }
         T R[PW], L[PW];
 #pragma unroll
         for (int j = 0; j < PW; ++j) {
@@ -1402,73 +1397,68 @@ __device__ __forceinline__ void fused_wave2n_xyd(const Geo &geo, const Coef<T> &
 #pragma unroll
             for (int q = 0; q < 4; ++q) out[j][q] = o[j][q];
         ++k;
-        __syncthreads();  // this sweep's tile, edges and flags before the next sweep reads them
-        return true;
+        __syncthreads();  // this sweep's tile, edges and flags before anyone reads them
+        if (LOCAL) return k < geo.max_sweeps && (flag[2 * (b ^ 1)] | flag[2 * (b ^ 1) + 1]) != 0u;
+        return k < k_target;
     };
-    T alt[PW][4], prev[PW][4];
+    // the exit work on cur = V_k, prv = V_{k-1} (each exit with its own roles)
+    auto finish = [&](const T (&cur)[PW][4], const T (&prv)[PW][4]) {
+        {
+            const T dw = wave_max(diff);
+            if (lane == 0) dvx[w] = dw;
+        }
+        __syncthreads();  // both waves' |dV|; past this no sweep reads a tile
+        dvl = (double)vmax(dvx[0], dvx[1]);
+        if (LOCAL && gk.buf != nullptr && w == 0) gk_exit(gk, k, dvl);  // the launch's reduction (one wave per grid)
+        done(k, dvl);
+        // pi of the last sweep = argmax on V_{k-1} (`prv`), per action with the usual topology
+        T *const N3 = tile + padw, *const S1 = tile + padw + 64 * P;
+#pragma unroll
+        for (int j = 0; j < PW; ++j) {
+            const int c = (w * PW + j) * 64 + lane;
+            S1[c] = prv[j][1];
+            N3[c] = prv[j][3];
+        }
+        if (w == 1 && lane == 0) edge[0] = prv[0][0];
+        if (w == 0 && lane == 63) edge[1] = prv[PW - 1][2];
+        __syncthreads();
+        const T eE = edge[0], eW = edge[1];
+        T R[PW], L[PW];
+#pragma unroll
+        for (int j = 0; j < PW; ++j) {
+            R[j] = dpp_mov<0x134>(prv[j][0]);
+            L[j] = dpp_mov<0x13C>(prv[j][2]);
+        }
+#pragma unroll
+        for (int j = 0; j < PW; ++j) {
+            const int c = (w * PW + j) * 64 + lane;
+            const T front[4] = {lane == 63 ? (j + 1 < PW ? R[j + 1] : (w == 0 ? eE : R[j])) : R[j], S1[c + W],
+                                lane == 0 ? (j > 0 ? L[j - 1] : (w == 1 ? eW : L[j])) : L[j], N3[c - W]};
+            if (c < geo.HW) {
+                const XydTopo<T> tp = xyd_topo<T>(cl, geo, c);
+                V4<T> op, tmp;
+                T nbv[4];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    op.v[d] = prv[j][d];
+                    nbv[d] = (tp.nbi[d] >> 2) != c ? front[d] : prv[j][d];  // blocked / terminal: own state
+                }
+                uint32_t pk;
+                xyd_step<T, false, true>(tp, cf, op, nbv, tmp, pk);
+                *reinterpret_cast<uint32_t *>(pig + c * 4) = pk;
+                *reinterpret_cast<V4<T> *>(Vg_out + c * 4) = V4<T>{{cur[j][0], cur[j][1], cur[j][2], cur[j][3]}};
+            }
+        }
+    };
+    T alt[PW][4];
     while (true) {
         if (!sweep(WaveBuf<0>{}, own, alt)) {
-#pragma unroll
-            for (int j = 0; j < PW; ++j)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) prev[j][q] = alt[j][q];
-            break;
+            finish(alt, own);
+            return;
         }
         if (!sweep(WaveBuf<1>{}, alt, own)) {
-#pragma unroll
-            for (int j = 0; j < PW; ++j)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    prev[j][q] = own[j][q];
-                    own[j][q] = alt[j][q];
-                }
-            break;
-        }
-    }
-    {
-        const T dw = wave_max(diff);
-        if (lane == 0) dvx[w] = dw;
-    }
-    __syncthreads();  // both waves' |dV|; past this no sweep reads a tile
-    dvl = (double)vmax(dvx[0], dvx[1]);
-    if (LOCAL && gk.buf != nullptr && w == 0) gk_exit(gk, k, dvl);  // the launch's reduction (one wave per grid)
-    done(k, dvl);
-    // pi of the last sweep = argmax on V_{k-1} (`prev`), per action with the usual topology
-    T *const N3 = tile + padw, *const S1 = tile + padw + 64 * P;
-#pragma unroll
-    for (int j = 0; j < PW; ++j) {
-        const int c = (w * PW + j) * 64 + lane;
-        S1[c] = prev[j][1];
-        N3[c] = prev[j][3];
-    }
-    if (w == 1 && lane == 0) edge[0] = prev[0][0];
-    if (w == 0 && lane == 63) edge[1] = prev[PW - 1][2];
-    __syncthreads();
-    const T eE = edge[0], eW = edge[1];
-    T R[PW], L[PW];
-#pragma unroll
-    for (int j = 0; j < PW; ++j) {
-        R[j] = dpp_mov<0x134>(prev[j][0]);
-        L[j] = dpp_mov<0x13C>(prev[j][2]);
-    }
-#pragma unroll
-    for (int j = 0; j < PW; ++j) {
-        const int c = (w * PW + j) * 64 + lane;
-        const T front[4] = {lane == 63 ? (j + 1 < PW ? R[j + 1] : (w == 0 ? eE : R[j])) : R[j], S1[c + W],
-                            lane == 0 ? (j > 0 ? L[j - 1] : (w == 1 ? eW : L[j])) : L[j], N3[c - W]};
-        if (c < geo.HW) {
-            const XydTopo<T> tp = xyd_topo<T>(cl, geo, c);
-            V4<T> op, tmp;
-            T nbv[4];
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                op.v[d] = prev[j][d];
-                nbv[d] = (tp.nbi[d] >> 2) != c ? front[d] : prev[j][d];  // blocked / terminal: own state
-            }
-            uint32_t pk;
-            xyd_step<T, false, true>(tp, cf, op, nbv, tmp, pk);
-            *reinterpret_cast<uint32_t *>(pig + c * 4) = pk;
-            *reinterpret_cast<V4<T> *>(Vg_out + c * 4) = V4<T>{{own[j][0], own[j][1], own[j][2], own[j][3]}};
+            finish(own, alt);
+            return;
         }
     }
 }
