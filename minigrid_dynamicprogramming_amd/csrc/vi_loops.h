@@ -1763,8 +1763,11 @@ __host__ __device__ inline int dkrow_smem_bytes(int HWp, int HWs, int tsize) {
 //    cell shut), so their target REPLACES the front value (one select, no extra max); only closing
 //    an open door (door_open 1: the open door ahead is walkable) is an extra candidate;
 //  * the cell's own invalid states (the key / door cells themselves) take ge4[hd] = 0 instead of g,
-//    so they yield +0 without a select -- except in waves that also add a goal reward (GOAL && KD),
-//    where max(0, 1) must be masked.
+//    so they yield +0 without a select.
+// GOAL waves: a state whose forward move enters the goal is worth exactly 1 where the agent can be
+// (the oracle's max(fl(g * M), 1) with fl(g * M) <= g < 1, every value being <= 1) and +0 where it
+// cannot, so one select replaces the reward's max (and, in KD waves, the walkability mask the max
+// needed): `one` = 1 / 0 per (has_key, door_open) in KD waves, 1 otherwise.
 template <typename T, bool GOAL, bool KD, bool DV>
 __device__ __forceinline__ T dk_rows_step(uint32_t walk, const uint32_t (&f)[4], T ge, const T (&ge4)[4],
                                           const T (&in)[16], const T (&fE)[4], const V4<T> &fS, const T (&fW)[4],
@@ -1787,8 +1790,7 @@ __device__ __forceinline__ T dk_rows_step(uint32_t walk, const uint32_t (&f)[4],
             T M = vmax(vmax((d & 1) ? m02 : m13, xS), F);
             if (KD && (hd & 1)) M = vmax(M, door ? in[d * 4 + (hd >> 1) * 2] : (T)0);  // close -> (hk, 0)
             T best = (KD ? ge4[hd] : ge) * M;
-            if (GOAL) best = vmax(best, (f[d] & 16u) ? (T)1 : (T)0);
-            if (KD && GOAL) best = ((walk >> hd) & 1u) ? best : (T)0;
+            if (GOAL) best = (f[d] & 16u) ? (KD ? (((walk >> hd) & 1u) ? (T)1 : (T)0) : (T)1) : best;
             out[l] = best;
             if (DV) df[l] = vabs(best - xS);
         }
