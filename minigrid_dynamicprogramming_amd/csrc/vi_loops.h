@@ -706,11 +706,13 @@ __device__ __forceinline__ void fused_pair_xyd(const Geo &geo, const Coef<T> &cf
 #pragma unroll
             for (int q = 0; q < 4; ++q) o[j][q] = ge[j] * m[q];
         }
-        if (goal_wave) {  // max(fl(g * m), 1): the goal's reward (uniform branch: few waves have one)
+        // the goal's reward max(fl(g * m), 1) is exactly 1 (values are <= 1): a select (uniform
+        // branch: few waves have one)
+        if (goal_wave) {
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) o[j][q] = ((goal >> (4 * j + q)) & 1u) ? vmax(o[j][q], (T)1) : o[j][q];
+                for (int q = 0; q < 4; ++q) o[j][q] = ((goal >> (4 * j + q)) & 1u) ? (T)1 : o[j][q];
         }
 #pragma unroll
         for (int j = 0; j < 2; ++j)
@@ -1014,9 +1016,9 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
         }
 #pragma unroll
         for (int j = 0; j < P; ++j) {
-            if ((goal_blocks >> j) & 1u) {  // max(fl(g * m), 1): the goal's reward
+            if ((goal_blocks >> j) & 1u) {  // the goal's reward max(fl(g * m), 1) is exactly 1 (values are <= 1): a select
 #pragma unroll
-                for (int q = 0; q < 4; ++q) o[j][q] = ((goal >> (4 * j + q)) & 1u) ? vmax(o[j][q], (T)1) : o[j][q];
+                for (int q = 0; q < 4; ++q) o[j][q] = ((goal >> (4 * j + q)) & 1u) ? (T)1 : o[j][q];
             }
         }
 #pragma unroll
@@ -1196,9 +1198,9 @@ __device__ __forceinline__ void fused_band_xyd(const Geo &geo, const Coef<T> &cf
         }
 #pragma unroll
         for (int j = 0; j < HB; ++j) {
-            if ((goal_slots >> j) & 1u) {  // max(fl(g * m), 1): the goal's reward
+            if ((goal_slots >> j) & 1u) {  // the goal's reward max(fl(g * m), 1) is exactly 1 (values are <= 1): a select
 #pragma unroll
-                for (int q = 0; q < 4; ++q) o[j][q] = ((goal >> (4 * j + q)) & 1u) ? vmax(o[j][q], (T)1) : o[j][q];
+                for (int q = 0; q < 4; ++q) o[j][q] = ((goal >> (4 * j + q)) & 1u) ? (T)1 : o[j][q];
             }
         }
         T dm = (T)0;
@@ -1368,9 +1370,9 @@ __device__ __forceinline__ void fused_wave2n_xyd(const Geo &geo, const Coef<T> &
         }
 #pragma unroll
         for (int j = 0; j < PW; ++j) {
-            if ((goal_blocks >> j) & 1u) {  // max(fl(g * m), 1): the goal's reward
+            if ((goal_blocks >> j) & 1u) {  // the goal's reward max(fl(g * m), 1) is exactly 1 (values are <= 1): a select
 #pragma unroll
-                for (int q = 0; q < 4; ++q) o[j][q] = ((goal >> (4 * j + q)) & 1u) ? vmax(o[j][q], (T)1) : o[j][q];
+                for (int q = 0; q < 4; ++q) o[j][q] = ((goal >> (4 * j + q)) & 1u) ? (T)1 : o[j][q];
             }
         }
 #pragma unroll
