@@ -1771,9 +1771,9 @@ __host__ __device__ inline int dkrow_smem_bytes(int HWp, int HWs, int tsize) {
 // cannot, so one select replaces the reward's max (and, in KD waves, the walkability mask the max
 // needed): `one` = 1 / 0 per (has_key, door_open) in KD waves, 1 otherwise.
 template <typename T, bool GOAL, bool KD, bool DV>
-__device__ __forceinline__ T dk_rows_step(uint32_t walk, const uint32_t (&f)[4], T ge, const T (&ge4)[4],
-                                          const T (&in)[16], const T (&fE)[4], const V4<T> &fS, const T (&fW)[4],
-                                          const V4<T> &fN, T (&out)[16]) {
+__device__ __forceinline__ T dk_rows_step(uint32_t walk, const uint32_t (&f)[4], uint32_t gdirs, T ge,
+                                          const T (&ge4)[4], const T (&in)[16], const T (&fE)[4], const V4<T> &fS,
+                                          const T (&fW)[4], const V4<T> &fN, T (&out)[16]) {
     T df[16];
 #pragma unroll
     for (int hd = 0; hd < 4; ++hd) {
@@ -1791,13 +1791,22 @@ __device__ __forceinline__ T dk_rows_step(uint32_t walk, const uint32_t (&f)[4],
             }
             T M = vmax(vmax((d & 1) ? m02 : m13, xS), F);
             if (KD && (hd & 1)) M = vmax(M, door ? in[d * 4 + (hd >> 1) * 2] : (T)0);  // close -> (hk, 0)
-            T best = (KD ? ge4[hd] : ge) * M;
-            if (GOAL) best = (f[d] & 16u) ? (KD ? (((walk >> hd) & 1u) ? (T)1 : (T)0) : (T)1) : best;
-            out[l] = best;
-            if (DV) df[l] = vabs(best - xS);
+            out[l] = (KD ? ge4[hd] : ge) * M;
+        }
+    }
+    if (GOAL) {  // per direction, a wave-uniform branch (a wave holds one to three of the goal's neighbours)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            if ((gdirs >> d) & 1u) {
+#pragma unroll
+                for (int hd = 0; hd < 4; ++hd)
+                    out[d * 4 + hd] = (f[d] & 16u) ? (KD ? (((walk >> hd) & 1u) ? (T)1 : (T)0) : (T)1) : out[d * 4 + hd];
+            }
         }
     }
     if constexpr (!DV) return (T)0;
+#pragma unroll
+    for (int l = 0; l < 16; ++l) df[l] = vabs(out[l] - in[l]);
     const T a = vmax(vmax(df[0], df[1]), df[2]), b = vmax(vmax(df[3], df[4]), df[5]);
     const T c = vmax(vmax(df[6], df[7]), df[8]), e = vmax(vmax(df[9], df[10]), df[11]);
     const T h = vmax(vmax(df[12], df[13]), df[14]);
@@ -1850,6 +1859,10 @@ __device__ __forceinline__ void fused_dk_rows(const Geo &geo, const Coef<T> &cf,
     const int cc = own_cell ? c : 0;  // idle threads shadow cell 0 (a border wall): they compute +0
     const DkTopo tp = dk_topo(cl, geo, cc);
     const DkFast q = dk_fast_topo(tp, 0);
+    // the directions in which some cell of this wave has the goal ahead (wave-uniform)
+    uint32_t gdirs = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) gdirs |= (__builtin_amdgcn_ballot_w64((q.f[d] & 16u) != 0u) != 0ull ? 1u : 0u) << d;
     const uint32_t cls = dk_fast_class(q);
     const uint32_t wcls = (__builtin_amdgcn_ballot_w64(cls & 1u) ? 1u : 0u) | (__builtin_amdgcn_ballot_w64(cls & 2u) ? 2u : 0u);
     const T ge = tp.walk != 0u ? cf.g : (T)0;
@@ -1891,9 +1904,9 @@ __device__ __forceinline__ void fused_dk_rows(const Geo &geo, const Coef<T> &cf,
                 fW[hd] = dpp_shr1_zero(in[8 + hd]);
             }
             T d;
-            if (LOCAL) d = dk_rows_step<T, GOAL, KD, true>(tp.walk, q.f, ge, ge4, in, fE, fS, fW, fN, out);
-            else if (k + 1 == k_target) d = dk_rows_step<T, GOAL, KD, true>(tp.walk, q.f, ge, ge4, in, fE, fS, fW, fN, out);
-            else d = dk_rows_step<T, GOAL, KD, false>(tp.walk, q.f, ge, ge4, in, fE, fS, fW, fN, out);
+            if (LOCAL) d = dk_rows_step<T, GOAL, KD, true>(tp.walk, q.f, gdirs, ge, ge4, in, fE, fS, fW, fN, out);
+            else if (k + 1 == k_target) d = dk_rows_step<T, GOAL, KD, true>(tp.walk, q.f, gdirs, ge, ge4, in, fE, fS, fW, fN, out);
+            else d = dk_rows_step<T, GOAL, KD, false>(tp.walk, q.f, gdirs, ge, ge4, in, fE, fS, fW, fN, out);
             diff = d;
             *reinterpret_cast<V4<T> *>(Tout + o1) = V4<T>{{out[4], out[5], out[6], out[7]}};
             *reinterpret_cast<V4<T> *>(Tout + o3) = V4<T>{{out[12], out[13], out[14], out[15]}};
