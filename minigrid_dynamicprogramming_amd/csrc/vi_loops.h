@@ -946,6 +946,9 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
     static_assert(P >= 1 && P <= 8, "goal bits: 4 per cell, 32 per lane");
     const int lane = (int)threadIdx.x;
     const int W = geo.W, padw = wave2_padw(W);
+    // k came from a per-grid word in memory (a VGPR); it is wave-uniform, so count sweeps in an SGPR
+    // (the loop's k < max_sweeps test and increment are then scalar instructions, not VALU)
+    k = __builtin_amdgcn_readfirstlane(k);
     T *const N3 = tile + padw;           // plane 3 (V of direction 3) of cell c at N3[c]
     T *const S1 = tile + padw + 64 * P;  // plane 1 of cell c at S1[c]
     T ge[P];
@@ -1136,6 +1139,7 @@ __device__ __forceinline__ void fused_band_xyd(const Geo &geo, const Coef<T> &cf
                                                const Done &done, const GkCtx gk = GkCtx{}) {
     static_assert(HB >= 1 && HB <= 8, "goal bits: 4 per cell, 32 per lane");
     const int lane = (int)threadIdx.x;
+    k = __builtin_amdgcn_readfirstlane(k);  // uniform: the sweep count in an SGPR
     const int W = geo.W, nb = 64 / W;
     const int band = lane / W, x = lane - band * W;
     const bool lane_on = band < nb;
@@ -1293,6 +1297,7 @@ __device__ __forceinline__ void fused_wave2n_xyd(const Geo &geo, const Coef<T> &
     static_assert(PW >= 1 && PW <= 8, "goal bits: 4 per cell, 32 per lane");
     constexpr int P = 2 * PW;
     const int w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+    k = __builtin_amdgcn_readfirstlane(k);  // uniform: the sweep count in an SGPR
     const int W = geo.W, padw = wave2_padw(W);
     const int TS = wave2n_tile_elems(W, P);
     T *const edge = tile + 2 * TS;  // [tile][0: plane 0 of cell 64 PW, 1: plane 2 of cell 64 PW - 1]
@@ -1819,6 +1824,7 @@ __device__ __forceinline__ void fused_dk_rows(const Geo &geo, const Coef<T> &cf,
                                               int8_t *pig, int &k, int k_target, double &dvl, const Done &done) {
     const int t = (int)threadIdx.x, lane = t & 63;
     const int HW = geo.HW, HWs = (int)blockDim.x, PL = dkrow_plane(HWs);
+    k = __builtin_amdgcn_readfirstlane(k);  // uniform: the sweep count in an SGPR (as fused_wave2_xyd)
     const int nrow = HWs >> 4;  // row slots (rows past H are idle; <= 64: HWs <= 1024)
     // 1. Row classes from the identity map (thread t on cell t): bit 1 KD, bit 0 GOAL, bit 2 walkable.
     {
