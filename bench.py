@@ -773,10 +773,12 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded, split_ev
                            "host_reads_per_solve": reads / args.steps,
                            "allreduce_us_per_solve_rank0": dev_ms * 1000.0 / args.steps,
                            "protocol_host_us_per_solve_rank0": wall_s * 1e6 / args.steps,
-                           "path": "torch.distributed ProcessGroupNCCL (distributed.Reducer)",
-                           "note": "device time of the RCCL all-reduces (events on the protocol stream, includes "
+                           "path": f"torch.distributed {dist.get_backend() if dist is not None else '-'} "
+                                   "process group (distributed.Reducer)",
+                           "note": "device time of the all-reduces (events on the protocol stream, includes "
                                    "waiting for the slowest rank; from the events pass when the region runs "
-                                   "without events) and host time of the one read per solve"}
+                                   "without events; 0 on a CPU-side gloo group) and host time of the one read "
+                                   "per solve"}
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         u = torch.tensor([upd_rank], dtype=torch.float64, device=red_dev)
