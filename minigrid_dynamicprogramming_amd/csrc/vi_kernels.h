@@ -221,10 +221,11 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
                 publish(host_out, (unsigned long long)kk, (unsigned long long)__double_as_longlong(dv),
                         (unsigned long long)kk, epoch);
         };
-        if (k_target < 0) {
-            // the in-launch reduction when the host passed its buffer (buf == nullptr: off)
-            fused_wave2_xyd<T, true, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2,
-                                        GkCtx{gk, epoch, e, geo.B, host_out});
+        if (k_target < 0 && gk != nullptr) {  // resident: the in-launch reduction, write-through exit stores
+            fused_wave2_xyd<T, true, P, true>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2,
+                                              GkCtx{gk, epoch, e, geo.B, host_out});
+        } else if (k_target < 0) {
+            fused_wave2_xyd<T, true, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
         } else {
             fused_wave2_xyd<T, false, P>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2);
         }

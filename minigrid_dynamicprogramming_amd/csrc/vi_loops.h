@@ -222,6 +222,45 @@ __device__ __forceinline__ void publish_tagged(unsigned long long *host_out, int
     __hip_atomic_store(host_out + 7, tag | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// A grid's exit stores (its V row and pi words), `wt`: written through the XCD L2 (agent-scope
+// relaxed stores: sc1).  Plain stores leave the batch's V / pi dirty in the L2s, and the launch's
+// end-of-kernel release writes them back after its last wave (MI355X_MICROARCH.md, boundary row:
+// + bytes / 6 TB/s); written through, they reach memory while the other grids still sweep.  Measured
+// (profiles/r05_wt/): a resident batch's kernel 1-2 % shorter (FourRooms x 4096 45.0 -> 44.0 us,
+// LavaS11N5 x 8192 27.5 -> 27.1), a batch past residency 6 % longer (the waves queued behind the
+// write-through stores): fused_wave2_xyd writes through in the launches with the in-launch reduction
+// (resident batches), its own instantiation.  MGDP_WT_EXIT=0 (A/B builds): never.
+#ifndef MGDP_WT_EXIT
+#define MGDP_WT_EXIT 1
+#endif
+template <typename T>
+__device__ __forceinline__ void store_v4_exit(T *p, const V4<T> &v, bool wt) {
+    if (MGDP_WT_EXIT && wt) {
+        unsigned long long *q = reinterpret_cast<unsigned long long *>(p);
+        if constexpr (sizeof(T) == 4) {
+            // one 16-B store, as the plain form (two 8-B atomic stores re-paired the loop's registers:
+            // +5 VALU per two sweeps at P = 2); its vmcnt is not tracked by the compiler, which only
+            // makes a later wait of its own more conservative (vector memory returns in order)
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            const f4v x = {v.v[0], v.v[1], v.v[2], v.v[3]};
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
+        } else {
+#pragma unroll
+            for (int d = 0; d < 4; ++d)
+                __hip_atomic_store(q + d, (unsigned long long)__double_as_longlong(v.v[d]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } else {
+        *reinterpret_cast<V4<T> *>(p) = v;
+    }
+}
+__device__ __forceinline__ void store_pi_exit(int8_t *p, uint32_t pk, bool wt) {
+    if (MGDP_WT_EXIT && wt)
+        __hip_atomic_store(reinterpret_cast<uint32_t *>(p), pk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *reinterpret_cast<uint32_t *>(p) = pk;
+}
+
 __device__ __forceinline__ void fused_reduce(unsigned long long *red, unsigned int *ticket,
                                              unsigned long long *host_out, int k, double dvl,
                                              unsigned int *lds_flag, unsigned int epoch, bool published) {
@@ -939,7 +978,9 @@ __device__ __forceinline__ T tree_max3(const T *x) {
     }
 }
 template <int B> struct WaveBuf { static constexpr int value = B; };
-template <typename T, bool LOCAL, int P, typename Done>
+// WT: write the exit stores through the L2 (store_v4_exit; the caller instantiates it for the launches
+// with the in-launch reduction, i.e. resident batches)
+template <typename T, bool LOCAL, int P, bool WT = false, typename Done>
 __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *tile,
                                                 const T *Vg, T *Vg_out, int8_t *pig, int &k, int k_target,
                                                 double &dvl, const Done &done, const GkCtx gk = GkCtx{}) {
@@ -1090,8 +1131,8 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
                 }
                 uint32_t pk;
                 xyd_step<T, false, true>(tp, cf, op, nbv, tmp, pk);
-                *reinterpret_cast<uint32_t *>(pig + c * 4) = pk;
-                *reinterpret_cast<V4<T> *>(Vg_out + c * 4) = V4<T>{{cur[j][0], cur[j][1], cur[j][2], cur[j][3]}};
+                store_pi_exit(pig + c * 4, pk, WT);
+                store_v4_exit(Vg_out + c * 4, V4<T>{{cur[j][0], cur[j][1], cur[j][2], cur[j][3]}}, WT);
             }
         }
     };
