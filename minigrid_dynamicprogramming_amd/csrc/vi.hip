@@ -188,6 +188,7 @@ Geo make_geo(const mgdp_vi *vi) {
     g.order = vi->order_valid && vi->learn_order ? vi->d_order : nullptr;
     for (int i = 0; i < 3; ++i) g.kprio[i] = vi->order_valid && vi->learn_prio ? vi->kprio[i] : 0;
     g.nmix = g.order && vi->mix ? vi->nmix : 0;
+    g.wt = vi->gk_capacity > 0 && vi->d.B <= vi->gk_capacity;
     return g;
 }
 

@@ -221,7 +221,8 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
                 publish(host_out, (unsigned long long)kk, (unsigned long long)__double_as_longlong(dv),
                         (unsigned long long)kk, epoch);
         };
-        if (k_target < 0 && gk != nullptr) {  // resident: the in-launch reduction, write-through exit stores
+        if (k_target < 0 && (gk != nullptr || geo.wt)) {  // resident: write-through exit stores (and the
+                                                          // in-launch reduction unless a protocol launch)
             fused_wave2_xyd<T, true, P, true>(geo, cf, cl2, tile, V + vb, V + vb, pi + vb, k, k_target, dvl, done2,
                                               GkCtx{gk, epoch, e, geo.B, host_out});
         } else if (k_target < 0) {

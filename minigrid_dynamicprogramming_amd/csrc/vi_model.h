@@ -25,6 +25,9 @@ struct Geo {
     // Mixed wave counts (round 5, fused_mix tags): the first nmix workgroups of the learned order
     // (the grids whose previous solve ran longest) take two waves per grid, the rest one.
     int nmix;
+    // The batch fits the one-wave kernel's resident capacity: its own-rule launches write their exit
+    // V / pi through the L2 (fused_wave2_xyd WT, store_v4_exit)
+    int wt;
 };
 
 template <typename T>
