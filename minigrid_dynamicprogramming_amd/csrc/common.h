@@ -38,19 +38,31 @@ inline int hip_fail(hipError_t e, const char *what, const char *file, int line) 
         if (!(cond)) { ::mgdp::set_error(__VA_ARGS__); return (code); }      \
     } while (0)
 
-// Sets the device for the calling thread and restores the previous one on scope exit (no runtime
-// call beyond hipGetDevice when the thread is already on `dev`: the lone-grid solve path crosses
-// several guarded entry points per solve).
+// Sets the device for the calling thread and restores the previous one on scope exit.  A guard
+// nested inside another guard of the same device on the same thread makes no runtime call at all
+// (`active`): a batched solve crosses five guarded entry points (solve, reset, run_local, run_to,
+// finish), and each hipGetDevice is a runtime call on the host's critical path of the solve loop.
 struct DeviceGuard {
+    static inline thread_local int active = -1;  // the device an enclosing guard holds current
     int prev = -1;
+    int outer = -1;
     bool ok = false;
     explicit DeviceGuard(int dev) {
+        outer = active;
+        if (outer == dev) { ok = true; return; }
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev == dev) { prev = -1; ok = true; return; }
-        ok = hipSetDevice(dev) == hipSuccess;
+        if (prev == dev) {
+            prev = -1;
+            ok = true;
+        } else {
+            ok = hipSetDevice(dev) == hipSuccess;
+        }
+        if (ok) active = dev;
     }
     ~DeviceGuard() {
+        if (outer == active) return;  // nested: nothing was changed
         if (prev >= 0) (void)hipSetDevice(prev);
+        active = outer;
     }
 };
 

@@ -456,7 +456,8 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
         }
     }
     if (smem > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
-    if (std::getenv("MGDP_DEBUG_OCC")) {  // diagnostics: resident workgroups per CU of this launch
+    static const bool debug_occ = std::getenv("MGDP_DEBUG_OCC") != nullptr;  // read once, not per launch
+    if (debug_occ) {  // diagnostics: resident workgroups per CU of this launch
         int per_cu = 0;
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)kern, vi->fused_block, smem);
         std::fprintf(stderr, "mgdp occupancy: %d workgroups/CU (block %d, LDS %d B)\n", per_cu, vi->fused_block, smem);
@@ -1548,6 +1549,7 @@ int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *con
             return 0;
         }
     }
+    DeviceGuard guard(vi->d.device);  // the entry points below nest inside it (no runtime call each)
     if (int rc = mgdp_vi_reset(vi)) return rc;
     int32_t k = 0;
     double dv = 0.0;
