@@ -37,6 +37,7 @@ def main():
             ms, n = vi.kernel_time()
             gs = vi.grid_sweeps()
             row["caps"][str(cap)] = {"k": int(k), "kernel_us": round(ms * 1e3 / max(n, 1), 2),
+                                     "kernel_us_per_solve": round(ms * 1e3 / args.solves, 2), "launches": n,
                                      "mean_grid_sweeps": round(float(np.mean(gs)), 2), "kernel": vi.kernel_name}
             vi.close()
         print(json.dumps(row), flush=True)
