@@ -392,7 +392,24 @@ def main():
         if not reducer_box and backend == "nccl" and os.environ.get("MGDP_BENCH_LIB_COMM", "1") != "0":
             from minigrid_dynamicprogramming_amd.distributed import LibComm
 
-            reducer_box.append(LibComm(device=local))
+            # every rank takes the library's communicator or none does: a rank whose mgdp_comm_create
+            # failed (an error code, not a hang) sends the whole job to the torch.distributed protocol
+            comm, err = None, ""
+            try:
+                if os.environ.get("MGDP_BENCH_LIB_COMM_FAIL") == str(rank):  # rehearsal of the fallback
+                    raise RuntimeError("MGDP_BENCH_LIB_COMM_FAIL")
+                comm = LibComm(device=local)
+            except Exception as ex:  # noqa: BLE001 -- reported, then the torch path
+                err = f"{type(ex).__name__}: {ex}"
+            ok = torch.tensor([0 if comm is None else 1], dtype=torch.int32, device=red_dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok.item()) == 1:
+                reducer_box.append(comm)
+            else:
+                if comm is not None:
+                    comm.close()
+                log(f"[rank {rank}] library communicator unavailable ({err or 'failed on another rank'}); "
+                    "torch.distributed protocol instead")
         if not reducer_box:
             from minigrid_dynamicprogramming_amd.distributed import Reducer
 
