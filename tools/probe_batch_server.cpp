@@ -7,7 +7,8 @@
 //              forwards it to a device word that every workgroup polls (s_sleep between polls).
 // Every wait is bounded (s_memrealtime idle limits), so the grid always drains.
 // Build: hipcc -O2 --offload-arch=gfx950 -o tools/probe_batch_server tools/probe_batch_server.cpp
-// Run:   tools/probe_batch_server [B] [work] [requests] [sleep]
+// Run:   tools/probe_batch_server [B] [work] [requests] [sleep: 2 / 10 / 40, 0 = lane 0 polls without
+//        s_sleep, -1 = every lane polls without s_sleep]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -106,7 +107,17 @@ __global__ void __launch_bounds__(64) server(int B, int work, u64 *tree, const u
             }
         }
         u64 f = 0;
-        if (lane == 0) {
+        if (sleep < 0) {  // variant: every lane polls (no divergent loop), no s_sleep
+            while (true) {
+                f = __hip_atomic_load(dflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                f = __builtin_amdgcn_readfirstlane((unsigned)(f >> 32)) == (unsigned)(f >> 32) ? f : f;
+                if (f >= want) break;
+                if (__builtin_amdgcn_s_memrealtime() - t_last > 2 * idle) {
+                    f = kQuit;
+                    break;
+                }
+            }
+        } else if (lane == 0) {
             while (true) {
                 f = __hip_atomic_load(dflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (f >= want) break;
@@ -116,7 +127,7 @@ __global__ void __launch_bounds__(64) server(int B, int work, u64 *tree, const u
                 }
                 if (sleep >= 40) __builtin_amdgcn_s_sleep(40);
                 else if (sleep >= 10) __builtin_amdgcn_s_sleep(10);
-                else __builtin_amdgcn_s_sleep(2);
+                else if (sleep >= 1) __builtin_amdgcn_s_sleep(2);
             }
         }
         f = __shfl(f, 0);
