@@ -430,7 +430,10 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
     if constexpr (MODEL == MGDP_MODEL_DOORKEY && MAP == MGDP_MAP_CELL && !SLIP) {
         if (vi->dk1t) kern = FusedK<T, MODEL, SLIP, MAP, kWpDk1t>::fn;
         else if (vi->dkhalf) kern = pick_dkhalf<FusedK, T, MODEL, SLIP, MAP>(vi->HWs / 64, kern);
-        else if (vi->dkrow) kern = FusedK<T, MODEL, SLIP, MAP, kWpDkRow>::fn;
+        else if (vi->dkrow)  // fp32 16x16 own-rule launches: the compile-time 256-thread variant
+            kern = (sizeof(T) == 4 && vi->HWs == 256 && vi->fused_block == 256 && k_target < 0 && !k_dev)
+                       ? FusedK<T, MODEL, SLIP, MAP, kWpDkRow16>::fn
+                       : FusedK<T, MODEL, SLIP, MAP, kWpDkRow>::fn;
     }
     if constexpr (MAP == MGDP_MAP_CELL) {  // one cell per thread, direction-major: the stripped variant
         if (kern == FusedK<T, MODEL, SLIP, MAP, 0>::fn && !vi->pair && !vi->quad && vi->HW <= vi->fused_block)

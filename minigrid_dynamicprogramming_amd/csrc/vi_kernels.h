@@ -9,6 +9,12 @@ constexpr int kWpDk1t = -100;  // vi_fused_kernel variant tag: batched DoorKey o
 // vi_fused_kernel variant tag: batched DoorKey grids of width 16 on whole-row thread maps, DPP
 // east / west fronts and two conflict-free LDS planes (fused_dk_rows; its own LDS layout, dkrow_*)
 constexpr int kWpDkRow = -800;
+// ... the same for exactly 16x16 cells (DoorKey-16x16: 256 threads, plane stride known at compile time,
+// so one LDS base register serves every tile access) and own-rule launches only (one copy of the sweep
+// loops: the run_to copy kept values live across both).  Both are what let the fp32 loop fit 80 VGPRs
+// -- 6 waves per SIMD -- with no scratch (round 5's 6-wave build spilled 76 B per thread).
+constexpr int kWpDkRow16 = -801;
+__host__ __device__ constexpr bool wp_is_dkrow(int wp) { return wp == kWpDkRow || wp == kWpDkRow16; }
 // vi_fused_kernel variant tag: the direction-major one-thread-per-cell path alone.  The generic
 // variant (WP = 0) also holds the cell-major, pair and quad loops, and a kernel's VGPR budget is
 // that of its hungriest path: stripping them is what sets the batched kernels' occupancy.
@@ -55,15 +61,21 @@ __host__ __device__ constexpr bool wp_is_mix(int wp) { return wp <= kWpMix - 2 &
 #ifndef MGDP_WAVE2N_MINW  // A/B builds: minimum waves per SIMD of the two-waves-per-grid kernels
 #define MGDP_WAVE2N_MINW 1
 #endif
-// Minimum waves per SIMD of fp32 fused_dk_rows: 6 (80 VGPRs and 80 B of scratch, 6 grids per CU) measured
-// 1950-1960 vs 1992-1996 us per DoorKey-16 x 65536 solve at the compiler's 5 (100 VGPRs), neutral at
-// 8192 grids (profiles/r05_dkw6/).  A/B builds: 1 = the compiler's choice.
+// Minimum waves per SIMD of fp32 fused_dk_rows: round 5's 6 (80 VGPRs and 76-80 B of scratch, 6 grids per
+// CU) measured 1950-1960 vs 1992-1996 us per DoorKey-16 x 65536 solve at 5, neutral at 8192 grids
+// (profiles/r05_dkw6/), but its spill stores doubled the launch's HBM writes.  Now: the 16x16 own-rule
+// variant (kWpDkRow16) at 6 waves, 80 VGPRs, no scratch; the general one at 5 (96 VGPRs, no scratch).
+// A/B builds: MGDP_DKROW16_MINW / MGDP_DKROW_MINW (1 = the compiler's choice).
 #ifndef MGDP_DKROW_MINW
-#define MGDP_DKROW_MINW 6
+#define MGDP_DKROW_MINW 5
+#endif
+#ifndef MGDP_DKROW16_MINW
+#define MGDP_DKROW16_MINW 6
 #endif
 template <typename T>
 __host__ __device__ constexpr int wave2_min_waves(int wp) {
-    return wp == kWpDkRow   ? (sizeof(T) == 4 ? MGDP_DKROW_MINW : 1)  // fp64 at 6 waves spills 492 B
+    return wp == kWpDkRow     ? (sizeof(T) == 4 ? MGDP_DKROW_MINW : 1)  // fp64 at 6 waves spills 492 B
+           : wp == kWpDkRow16 ? (sizeof(T) == 4 ? MGDP_DKROW16_MINW : 1)
            : wp_is_wave2n(wp) ? MGDP_WAVE2N_MINW
            : (MGDP_WAVE2_W8 && wp_is_mix(wp) && kWpMix - wp <= 2) ? 8
            : (MGDP_WAVE2_W8 && wp_is_wave2(wp) && kWpWave2 - wp <= (sizeof(T) == 4 ? 2 : 1)) ? 8
@@ -102,8 +114,15 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     T *slots = reinterpret_cast<T *>(smem + L.slots_off());
     uint8_t *flags = reinterpret_cast<uint8_t *>(smem + L.flags_off());
 
-    k = fresh ? 0 : kenv[e];
-    dvl = fresh ? 0.0 : dvenv[e];
+    // workgroup-uniform: in SGPRs (as VGPRs they stayed live across the sweep loops -- a register
+    // pair the batched DoorKey loop at 80 VGPRs had to spill to scratch)
+    k = __builtin_amdgcn_readfirstlane(fresh ? 0 : kenv[e]);
+    {
+        const long long b = fresh ? 0ll : __double_as_longlong(dvenv[e]);
+        const unsigned int lo = __builtin_amdgcn_readfirstlane((unsigned int)b);
+        const unsigned int hi = __builtin_amdgcn_readfirstlane((unsigned int)(b >> 32));
+        dvl = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+    }
     if (geo.kprio[2] > 0 && k_target < 0) {
         // learned priority: the grids that ran longest last time get the SIMDs' issue slots first, so
         // the launch's critical path (its longest grids) is not stretched by the short ones
@@ -237,25 +256,31 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
         }
         return true;
     }
-    if constexpr (WP == kWpDkRow) {  // its own LDS layout (dkrow_*): slots, flags, row map, cells, tiles
+    if constexpr (wp_is_dkrow(WP)) {  // its own LDS layout (dkrow_*): slots, flags, row map, cells, tiles
         static_assert(MODEL == MGDP_MODEL_DOORKEY && !SLIP && MAP == MGDP_MAP_CELL && !SERVED, "dkrow: batched DoorKey");
         uint8_t *cl2 = smem + dkrow_cells_off();
         copy16(cl2, cells + (long long)e * geo.HWp, geo.HWp);
         __syncthreads();
         T *tiles = reinterpret_cast<T *>(smem + dkrow_tile_off(geo.HWp));
         T *slots2 = reinterpret_cast<T *>(smem);
+        // after the loop the thread index is late_tid's (fused_dk_rows): nothing below reads threadIdx.x
+        int tl = 0;
         auto done2 = [&](int kk, double dv) {
-            if (lone && threadIdx.x == 0)
+            if (lone && tl == 0)
                 publish(host_out, (unsigned long long)kk, (unsigned long long)__double_as_longlong(dv),
                         (unsigned long long)kk, epoch);
         };
-        if (k_target < 0)
+        if constexpr (WP == kWpDkRow16) {  // own-rule launches only (the host picks kWpDkRow for run_to)
+            fused_dk_rows<T, true, 256>(geo, cf, cl2, tiles, slots2, smem + 256, smem + 320, V + vb, V + vb, pi + vb, k,
+                                        k_target, dvl, done2, tl);
+        } else if (k_target < 0) {
             fused_dk_rows<T, true>(geo, cf, cl2, tiles, slots2, smem + 256, smem + 320, V + vb, V + vb, pi + vb, k,
-                                   k_target, dvl, done2);
-        else
+                                   k_target, dvl, done2, tl);
+        } else {
             fused_dk_rows<T, false>(geo, cf, cl2, tiles, slots2, smem + 256, smem + 320, V + vb, V + vb, pi + vb, k,
-                                    k_target, dvl, done2);
-        if (threadIdx.x == 0) {
+                                    k_target, dvl, done2, tl);
+        }
+        if (tl == 0) {
             kenv[e] = k;
             if (geo.kexec) geo.kexec[e] = k;
             dvenv[e] = dvl;
@@ -412,7 +437,7 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Smem L = smem_layout(geo.Ss, geo.HWp, (int)sizeof(T), geo.nbuf);
     constexpr bool kOwnLds = wp_is_wave2(WP) || wp_is_wave2n(WP) || wp_is_band(WP) || wp_is_mix(WP);  // wave2-family layouts, gk
-    T *slots = reinterpret_cast<T *>(smem + (kOwnLds || WP == kWpDkRow ? 0 : L.slots_off()));
+    T *slots = reinterpret_cast<T *>(smem + (kOwnLds || wp_is_dkrow(WP) ? 0 : L.slots_off()));
     // a one-wave grid of a mixed launch: its second wave leaves before touching anything
     if constexpr (wp_is_mix(WP))
         if (threadIdx.x >= 64 && (int)blockIdx.x >= geo.nmix) return;
@@ -428,6 +453,8 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
     }
     int k;
     double dvl;
+    // kWpDkRow: the wave index in an SGPR, for late_tid after the sweep loop (fused_dk_rows)
+    const int wvk = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     const bool lone = in_kernel_reduce && gridDim.x == 1;
     const bool work = fused_grid<T, MODEL, SLIP, MAP, false, WP>(geo, cf, cells, V, pi, kenv, dvenv, host_out, k_target,
                                                                  fresh, lone, epoch,
@@ -437,7 +464,8 @@ vi_fused_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__res
     // a launch-wide-rule launch (wave2 with gk) reduces and publishes through its own counter tree
     const bool gk_pub = kOwnLds && gk != nullptr && k_target < 0 && !k_target_dev;
     if (in_kernel_reduce && !gk_pub)
-        fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16), epoch, work);
+        fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16), epoch, work,
+                     wp_is_dkrow(WP) ? late_tid(wvk) : (int)threadIdx.x);
 }
 
 // Persistent solver for a lone grid: one workgroup stays resident and serves solve requests posted
@@ -698,7 +726,9 @@ vi_fused_opts_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *
             dvenv[e] = dvl;
         }
     }
-    if (in_kernel_reduce) fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16), epoch, work);
+    if (in_kernel_reduce)
+        fused_reduce(red, ticket, host_out, k, dvl, reinterpret_cast<unsigned int *>(slots + 16), epoch, work,
+                     (int)threadIdx.x);
 }
 
 // The sharded protocol's gate (mgdp_vi_run_to_dev_sync): kdv = the all-reduced {K, E}, written by

@@ -263,14 +263,14 @@ __device__ __forceinline__ void store_pi_exit(int8_t *p, uint32_t pk, bool wt) {
 
 __device__ __forceinline__ void fused_reduce(unsigned long long *red, unsigned int *ticket,
                                              unsigned long long *host_out, int k, double dvl,
-                                             unsigned int *lds_flag, unsigned int epoch, bool published) {
+                                             unsigned int *lds_flag, unsigned int epoch, bool published, int tid) {
     if (gridDim.x == 1) {  // a lone grid publishes directly (early, if it swept: see `done`)
-        if (threadIdx.x == 0 && !published)
+        if (tid == 0 && !published)
             publish(host_out, (unsigned long long)k, (unsigned long long)__double_as_longlong(dvl),
                     (unsigned long long)k, epoch);
         return;
     }
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
         unsigned long long *r = red + (blockIdx.x & (kRedShards - 1)) * 4;
         const unsigned long long a = __hip_atomic_fetch_max(r + 0, (unsigned long long)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long b = __hip_atomic_fetch_max(r + 1, (unsigned long long)__double_as_longlong(dvl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -280,8 +280,8 @@ __device__ __forceinline__ void fused_reduce(unsigned long long *red, unsigned i
         *lds_flag = t == gridDim.x - 1;
     }
     __syncthreads();
-    if (*lds_flag && threadIdx.x < 64) {
-        unsigned long long *r = red + threadIdx.x * 4;
+    if (*lds_flag && tid < 64) {
+        unsigned long long *r = red + tid * 4;
         unsigned long long km = __hip_atomic_exchange(r + 0, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         unsigned long long dv = __hip_atomic_exchange(r + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         unsigned long long kn = __hip_atomic_exchange(r + 2, 0x7fffffffull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -291,7 +291,7 @@ __device__ __forceinline__ void fused_reduce(unsigned long long *red, unsigned i
             dv = max(dv, (unsigned long long)__shfl_xor(dv, o));
             kn = min(kn, (unsigned long long)__shfl_xor(kn, o));
         }
-        if (threadIdx.x == 0) {
+        if (tid == 0) {
             __hip_atomic_exchange(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             publish(host_out, km, dv, kn, epoch);
         }
@@ -1859,12 +1859,16 @@ __device__ __forceinline__ T dk_rows_step(uint32_t walk, const uint32_t (&f)[4],
     return vmax(vmax(vmax(a, b), c), vmax(vmax(e, h), df[15]));
 }
 
-template <typename T, bool LOCAL, typename Done>
+// HWS_C: the workgroup size (HWs) when known at compile time (kWpDkRow16), else 0
+template <typename T, bool LOCAL, int HWS_C = 0, typename Done>
 __device__ __forceinline__ void fused_dk_rows(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *tiles,
                                               T *slots, uint8_t *flags, uint8_t *rowmap, const T *Vg, T *Vg_out,
-                                              int8_t *pig, int &k, int k_target, double &dvl, const Done &done) {
+                                              int8_t *pig, int &k, int k_target, double &dvl, const Done &done,
+                                              int &t_late) {
     const int t = (int)threadIdx.x, lane = t & 63;
-    const int HW = geo.HW, HWs = (int)blockDim.x, PL = dkrow_plane(HWs);
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);  // the wave index, an SGPR (late_tid after the loop)
+    const bool lane0 = lane == 0;
+    const int HW = geo.HW, HWs = HWS_C ? HWS_C : (int)blockDim.x, PL = dkrow_plane(HWs);
     k = __builtin_amdgcn_readfirstlane(k);  // uniform: the sweep count in an SGPR (as fused_wave2_xyd)
     const int nrow = HWs >> 4;  // row slots (rows past H are idle; <= 64: HWs <= 1024)
     // 1. Row classes from the identity map (thread t on cell t): bit 1 KD, bit 0 GOAL, bit 2 walkable.
@@ -1957,7 +1961,10 @@ __device__ __forceinline__ void fused_dk_rows(const Geo &geo, const Coef<T> &cf,
             diff = d;
             *reinterpret_cast<V4<T> *>(Tout + o1) = V4<T>{{out[4], out[5], out[6], out[7]}};
             *reinterpret_cast<V4<T> *>(Tout + o3) = V4<T>{{out[12], out[13], out[14], out[15]}};
-            if (LOCAL) flag_write(d >= cf.tol, flags, par);
+            if (LOCAL) {
+                const unsigned long long b = __ballot(d >= cf.tol);
+                if (lane0) flags[par * 16 + wv] = b != 0ull;
+            }
             __syncthreads();
             ++k;
             if (LOCAL) {
@@ -1979,8 +1986,20 @@ __device__ __forceinline__ void fused_dk_rows(const Geo &geo, const Coef<T> &cf,
     if (wcls == 0u) run(No{}, No{});
     else if (wcls == 1u) run(Yes{}, No{});
     else run(Yes{}, Yes{});
-    dvl = (double)block_max(diff, slots, 0);
+    const int t2 = late_tid(wv);
+    t_late = t2;
+    dvl = (double)block_max_tid(diff, slots, 0, t2);
     done(k, dvl);
+    // The pi pass re-derives the thread's cell and topology from LDS (row map and cells are still
+    // there) instead of keeping them live across the sweep loop: at 6 waves per SIMD (80 VGPRs) the
+    // loop leaves no room for them, and the compiler spilled them to scratch -- 76 B per thread
+    // stored to memory once per launch, 0.85 GB of the DoorKey-16 x 65536 launch's HBM writes
+    // (round-5 verdict).  The opaque copy of the thread index keeps the compiler from reusing the
+    // values computed before the loop.
+    const int c2 = rowmap[t2 >> 4] * 16 + (t2 & 15);
+    const bool own2 = c2 < HW;
+    const DkTopo tp2 = dk_topo(cl, geo, own2 ? c2 : 0);
+    const int p1 = (16 + c2) * 4, p3 = (PL + 16 + c2) * 4;
     T vk[16], vp[16];
 #pragma unroll
     for (int l = 0; l < 16; ++l) {
@@ -1994,16 +2013,17 @@ __device__ __forceinline__ void fused_dk_rows(const Geo &geo, const Coef<T> &cf,
         nbs[0].v[hd] = dpp_shl1_zero(vp[hd]);
         nbs[2].v[hd] = dpp_shr1_zero(vp[8 + hd]);
     }
-    nbs[1] = *reinterpret_cast<const V4<T> *>(Tp + o1 + 64);
-    nbs[3] = *reinterpret_cast<const V4<T> *>(Tp + o3 - 64);
-    if (own_cell) {
-        T tmp[16];
-        uint32_t pk[4];
-        dk_step<T, true>(tp, cf, vp, nbs, tmp, pk);
-        *reinterpret_cast<uint4 *>(pig + c * 16) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    nbs[1] = *reinterpret_cast<const V4<T> *>(Tp + p1 + 64);
+    nbs[3] = *reinterpret_cast<const V4<T> *>(Tp + p3 - 64);
+    if (own2) {
+        // V_k leaves first, so its registers are free for the per-action pi pass
 #pragma unroll
         for (int qd = 0; qd < 4; ++qd)
-            *reinterpret_cast<V4<T> *>(Vg_out + c * 16 + 4 * qd) = V4<T>{{vk[4 * qd], vk[4 * qd + 1], vk[4 * qd + 2], vk[4 * qd + 3]}};
+            *reinterpret_cast<V4<T> *>(Vg_out + c2 * 16 + 4 * qd) = V4<T>{{vk[4 * qd], vk[4 * qd + 1], vk[4 * qd + 2], vk[4 * qd + 3]}};
+        T tmp[16];
+        uint32_t pk[4];
+        dk_step<T, true>(tp2, cf, vp, nbs, tmp, pk);
+        *reinterpret_cast<uint4 *>(pig + c2 * 16) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
     }
 }
 

@@ -91,19 +91,33 @@ __device__ __forceinline__ T wave_max(T v) {
     return tmax(tmax(lane_read(v, 0), lane_read(v, 16)), tmax(lane_read(v, 32), lane_read(v, 48)));
 }
 
+// The thread index re-derived after a long loop: the wave index (workgroup-uniform, an SGPR the
+// caller took before the loop) * 64 + the lane from v_mbcnt.  The mbcnt is asm, so the compiler
+// cannot substitute the thread-index VGPR kept from before the loop: a kernel whose loop needs
+// every VGPR then keeps no per-thread index live across it (the batched DoorKey loop at 80 VGPRs
+// spilled it to scratch).
+__device__ __forceinline__ int late_tid(int wave_s) {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return (wave_s << 6) | l;
+}
+
 // Block-wide max with ONE barrier; slots = [2][16] alternating by parity so that consecutive
 // calls never race (a slot set is rewritten only after every thread passed the next barrier).
+// tid: the caller's thread index (late_tid after a long loop).
 template <typename T>
-__device__ __forceinline__ T block_max(T v, T *slots, int parity) {
+__device__ __forceinline__ T block_max_tid(T v, T *slots, int parity, int tid) {
     v = wave_max(v);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) slots[parity * 16 + w] = v;
+    const int w = tid >> 6;
+    if ((tid & 63) == 0) slots[parity * 16 + w] = v;
     __syncthreads();
     const int nw = blockDim.x >> 6;
     T m = slots[parity * 16];
     for (int i = 1; i < nw; ++i) m = tmax(m, slots[parity * 16 + i]);
     return m;
 }
+template <typename T>
+__device__ __forceinline__ T block_max(T v, T *slots, int parity) { return block_max_tid(v, slots, parity, (int)threadIdx.x); }
 
 // Block-wide OR of a predicate with ONE barrier: one byte flag per wave, two parities.
 __device__ __forceinline__ bool block_any(bool p, uint8_t *flags, int parity) {
