@@ -392,23 +392,27 @@ def main():
         if not reducer_box and backend == "nccl" and os.environ.get("MGDP_BENCH_LIB_COMM", "1") != "0":
             from minigrid_dynamicprogramming_amd.distributed import LibComm
 
-            # every rank takes the library's communicator or none does: a rank whose mgdp_comm_create
-            # failed (an error code, not a hang) sends the whole job to the torch.distributed protocol
-            comm, err = None, ""
+            # every rank takes the library's communicator or none does.  The ranks first agree on a
+            # LOCAL check (librccl loads: mgdp_comm_available), with one MIN all-reduce, and only then
+            # start the collective bootstrap (the id broadcast and ncclCommInitRank): a rank that
+            # cannot load librccl sends the whole job to the torch.distributed protocol before any
+            # rank waits in a collective the others never join.  A failure inside ncclCommInitRank
+            # itself (after agreement) leaves its peers waiting there and cannot be recovered from.
+            err = ""
             try:
                 if os.environ.get("MGDP_BENCH_LIB_COMM_FAIL") == str(rank):  # rehearsal of the fallback
                     raise RuntimeError("MGDP_BENCH_LIB_COMM_FAIL")
-                comm = LibComm(device=local)
+                here = LibComm.available()
+                if not here:
+                    err = "librccl could not be loaded"
             except Exception as ex:  # noqa: BLE001 -- reported, then the torch path
-                err = f"{type(ex).__name__}: {ex}"
-            ok = torch.tensor([0 if comm is None else 1], dtype=torch.int32, device=red_dev)
+                here, err = False, f"{type(ex).__name__}: {ex}"
+            ok = torch.tensor([1 if here else 0], dtype=torch.int32, device=red_dev)
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
             if int(ok.item()) == 1:
-                reducer_box.append(comm)
+                reducer_box.append(LibComm(device=local))
             else:
-                if comm is not None:
-                    comm.close()
-                log(f"[rank {rank}] library communicator unavailable ({err or 'failed on another rank'}); "
+                log(f"[rank {rank}] library communicator unavailable ({err or 'unavailable on another rank'}); "
                     "torch.distributed protocol instead")
         if not reducer_box:
             from minigrid_dynamicprogramming_amd.distributed import Reducer
@@ -784,7 +788,8 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded, split_ev
         if type(reducer).__name__ == "LibComm":
             collectives = {"allreduces_per_solve": calls / args.steps, "host_reads_per_solve": reads / args.steps,
                            "path": "libmgdp communicator (mgdp_vi_solve_sharded: RCCL enqueued by the library on "
-                                   "the handle's stream, one C call and one host wait per solve)"}
+                                   "the handle's stream, one C call per solve; host waits counted by the library, "
+                                   "mgdp_comm_host_waits)"}
         else:
             collectives = {"allreduces_per_solve": calls / args.steps,
                            "host_reads_per_solve": reads / args.steps,

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MGDP_ABI_VERSION 11
+#define MGDP_ABI_VERSION 12
 
 enum {
     MGDP_OK = 0,
@@ -207,15 +207,33 @@ int mgdp_vi_set_result(mgdp_vi *vi, int32_t k, double dv);
  * side channel (a torch.distributed store, MPI, a file); every rank then calls mgdp_comm_create with
  * its rank and device.  One communicator per process and device, shared by its handles. */
 typedef struct mgdp_comm mgdp_comm;
+/* 0 when librccl can be loaded in this process (ABI 12).  A local check with no communication: every
+ * rank calls it and the ranks agree (e.g. a MIN all-reduce of the flags over their bootstrap group)
+ * BEFORE any of them calls mgdp_comm_unique_id / mgdp_comm_create, which are collective (a failure
+ * inside ncclCommInitRank itself leaves the other ranks waiting and cannot be recovered from). */
+int mgdp_comm_available(void);
 int mgdp_comm_unique_id(uint8_t *id_out /* 128 bytes */);
 int mgdp_comm_create(const uint8_t *id /* 128 bytes */, int32_t nranks, int32_t rank, int32_t device,
                      mgdp_comm **out);
+/* The host communicator (ABI 12): the same collectives through a shared-memory segment of this host,
+ * /dev/shm<name> (name = "/..." with no other "/"), for ranks that cannot form an RCCL communicator
+ * -- several ranks on ONE GPU, which RCCL refuses -- e.g. tests of mgdp_vi_solve_sharded at world > 1
+ * on a one-GPU box.  Each device all-reduce becomes a stream synchronisation, a host MAX and a copy
+ * back (a test and rehearsal path, not the xGMI one).  Every rank opens the segment (created
+ * zero-filled by the first); the caller picks a name no earlier run used and removes the file once
+ * every rank has opened it (the mappings stay valid).  A collective waits at most 120 s for its
+ * peers, then fails with MGDP_E_INVALID. */
+int mgdp_comm_create_host(const char *name, int32_t nranks, int32_t rank, int32_t device, mgdp_comm **out);
 int mgdp_comm_destroy(mgdp_comm *comm);
 /* Synchronous MAX all-reduce of n int64 host values in place (for ranks that drive the protocol from
  * the host: an empty shard, the sweep method, DP options -- they join the same collectives). */
 int mgdp_comm_allreduce_max(mgdp_comm *comm, int64_t *vals, int32_t n);
 /* All-reduces issued on the communicator so far, its size and this process's rank. */
 int mgdp_comm_stats(const mgdp_comm *comm, int64_t *allreduces, int32_t *nranks, int32_t *rank);
+/* Host waits on the GPU so far (ABI 12): one per sharded solve (its run_to result), one per dV(K) or
+ * fallback-sweep all-reduce and per mgdp_comm_allreduce_max, and with the host kind one more per
+ * device all-reduce; kind: 0 RCCL, 1 host. */
+int mgdp_comm_host_waits(const mgdp_comm *comm, int64_t *waits, int32_t *kind);
 /* One sharded solve of this rank's handle (fused method, no horizon / lava options), every rank of
  * the communicator at once: reset -> run_local_dev -> MAX all-reduce of {K, own-rule dV bits} on the
  * handle's stream -> gate / run_to(K) with one host wait on host-mapped words -> [only if the
@@ -224,7 +242,8 @@ int mgdp_comm_stats(const mgdp_comm *comm, int64_t *allreduces, int32_t *nranks,
  * through mgdp_comm_allreduce_max: {k, dV bits} (2 words), then dV(K) bits (1 word) only if the
  * all-reduced dV bits are non-zero, then one word per fallback sweep while dV >= tol and
  * k < max_sweeps.  Results as mgdp_vi_solve (V and pi of the global rule, bit-identical to one global
- * Jacobi loop over every rank's grids). */
+ * Jacobi loop over every rank's grids).  Sharded solves of several handles on one communicator must
+ * not overlap (one host thread calling them in turn): they share its device protocol words. */
 int mgdp_vi_solve_sharded(mgdp_vi *vi, mgdp_comm *comm, int32_t *sweeps_out, double *dv_out,
                           int32_t *converged_out);
 

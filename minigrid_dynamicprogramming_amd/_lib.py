@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # MGDP_LIB: an alternative build of the same sources (tools/ experiments with compile-time knobs)
 LIB_PATH = os.environ.get("MGDP_LIB") or os.path.join(HERE, "libmgdp.so")
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 MGDP_OK = 0
 MGDP_E_INVALID = -1
 MGDP_E_HIP = -2
@@ -89,11 +89,14 @@ SIGNATURES = {
     "mgdp_vi_run_local_dev": (ctypes.c_int, [_P, _P]),
     "mgdp_vi_run_to_dev": (ctypes.c_int, [_P, _P, _P]),
     "mgdp_vi_set_result": (ctypes.c_int, [_P, _I32, ctypes.c_double]),
+    "mgdp_comm_available": (ctypes.c_int, []),
     "mgdp_comm_unique_id": (ctypes.c_int, [_P]),
     "mgdp_comm_create": (ctypes.c_int, [_P, _I32, _I32, _I32, ctypes.POINTER(_P)]),
+    "mgdp_comm_create_host": (ctypes.c_int, [ctypes.c_char_p, _I32, _I32, _I32, ctypes.POINTER(_P)]),
     "mgdp_comm_destroy": (ctypes.c_int, [_P]),
     "mgdp_comm_allreduce_max": (ctypes.c_int, [_P, _P, _I32]),
     "mgdp_comm_stats": (ctypes.c_int, [_P, _I64P, _I32P, _I32P]),
+    "mgdp_comm_host_waits": (ctypes.c_int, [_P, _I64P, _I32P]),
     "mgdp_vi_solve_sharded": (ctypes.c_int, [_P, _P, _I32P, _DP, _I32P]),
     "mgdp_vi_run_to_dev_sync": (ctypes.c_int, [_P, _P, _I32P, _DP, _DP]),
     "mgdp_vi_local_result": (ctypes.c_int, [_P, _I32P, _DP, _I32P]),

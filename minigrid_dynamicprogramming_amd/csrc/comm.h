@@ -7,9 +7,12 @@
 namespace mgdp {
 // MAX all-reduce of n int64 words of device memory, in place, enqueued on `stream`.
 int comm_allreduce_max_dev(mgdp_comm *c, int64_t *d, size_t n, hipStream_t stream);
-// The communicator's device protocol buffer: int64[8] of device memory ({K, dV bits, kmin, 0},
-// [5] = dV(K) bits), and a pinned host word for the one-word collectives.
+// The communicator's device protocol buffer: int64[16] of device memory ([0..7] the protocol's words:
+// {K, dV bits, kmin, 0}, [5] = dV(K) bits; [8..15] host-driven staging), and a pinned host word for
+// the one-word collectives.
 int64_t *comm_proto(mgdp_comm *c);
 int64_t *comm_host_word(mgdp_comm *c);
 int comm_device(const mgdp_comm *c);
+// One host wait on the GPU made on the communicator's behalf (mgdp_comm_host_waits).
+void comm_note_host_wait(mgdp_comm *c);
 }  // namespace mgdp

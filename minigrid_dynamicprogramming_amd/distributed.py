@@ -166,10 +166,24 @@ class LibComm:
     Python between the launches.  Bootstrapped once per process over a torch.distributed group
     (gloo or nccl): rank 0's 128-byte ncclUniqueId is broadcast to every rank.  Ranks whose shard
     cannot run the device protocol (empty shards, the sweep method, DP options) join the same
-    collectives host-driven (mgdp_comm_allreduce_max); see solve_sharded."""
+    collectives host-driven (mgdp_comm_allreduce_max); see solve_sharded.
 
-    def __init__(self, group=None, device: int | None = None):
+    kind="host": the host communicator (mgdp_comm_create_host, ABI 12) -- the same C calls, their
+    collectives through a shared-memory segment, for ranks that share one GPU (RCCL refuses them):
+    the multi-rank tests of mgdp_vi_solve_sharded.  The constructor is collective; call
+    LibComm.available() on every rank and agree first (bench.py does)."""
+
+    @staticmethod
+    def available() -> bool:
+        """Whether librccl loads in this process (mgdp_comm_available): a local check, no communication."""
+        from . import _lib
+
+        return _lib.load().mgdp_comm_available() == 0
+
+    def __init__(self, group=None, device: int | None = None, kind: str = "rccl"):
         import ctypes
+        import os
+        import uuid
 
         import torch
         import torch.distributed as dist
@@ -180,15 +194,31 @@ class LibComm:
         L = _lib.load()
         self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
         self.device = torch.cuda.current_device() if device is None else int(device)
-        uid = (ctypes.c_uint8 * 128)()
-        if self.rank == 0:
-            _lib.check(L.mgdp_comm_unique_id(uid), "mgdp_comm_unique_id")
-        obj = [bytes(uid) if self.rank == 0 else None]
+        self.kind = kind
         src = 0 if group is None else dist.get_global_rank(group, 0)
-        dist.broadcast_object_list(obj, src=src, group=group)
-        uid = (ctypes.c_uint8 * 128).from_buffer_copy(obj[0])
         h = ctypes.c_void_p()
-        _lib.check(L.mgdp_comm_create(uid, self.world, self.rank, self.device, ctypes.byref(h)), "mgdp_comm_create")
+        if kind == "host":
+            # a fresh segment name from rank 0; every rank opens it, then it is unlinked (the mappings stay)
+            obj = [f"/mgdp_comm_{os.getpid()}_{uuid.uuid4().hex[:12]}" if self.rank == 0 else None]
+            dist.broadcast_object_list(obj, src=src, group=group)
+            _lib.check(L.mgdp_comm_create_host(obj[0].encode(), self.world, self.rank, self.device, ctypes.byref(h)),
+                       "mgdp_comm_create_host")
+            dist.barrier(group=group)
+            if self.rank == 0:
+                try:
+                    os.remove("/dev/shm" + obj[0])
+                except OSError:
+                    pass
+        elif kind == "rccl":
+            uid = (ctypes.c_uint8 * 128)()
+            if self.rank == 0:
+                _lib.check(L.mgdp_comm_unique_id(uid), "mgdp_comm_unique_id")
+            obj = [bytes(uid) if self.rank == 0 else None]
+            dist.broadcast_object_list(obj, src=src, group=group)
+            uid = (ctypes.c_uint8 * 128).from_buffer_copy(obj[0])
+            _lib.check(L.mgdp_comm_create(uid, self.world, self.rank, self.device, ctypes.byref(h)), "mgdp_comm_create")
+        else:
+            raise ValueError(f"kind must be 'rccl' or 'host', not {kind!r}")
         self.handle = h
         self._words = (ctypes.c_int64 * 8)()
         # Reducer-like counters for bench.py's collectives block (no per-collective events: the
@@ -198,14 +228,27 @@ class LibComm:
         self.reset_counters()
 
     def reset_counters(self):
-        self._base = self.allreduces if getattr(self, "handle", None) is not None else 0
-        self.host_reads = 0
+        live = getattr(self, "handle", None) is not None
+        self._base = self.allreduces if live else 0
+        self._wbase = self.host_waits if live else 0
         self.wall_s = 0.0
         self.device_ms = 0.0
 
     @property
     def calls(self) -> int:
         return self.allreduces - self._base
+
+    @property
+    def host_reads(self) -> int:
+        """Host waits on the GPU since reset_counters (mgdp_comm_host_waits): the library counts them."""
+        return self.host_waits - self._wbase
+
+    @property
+    def host_waits(self) -> int:
+        c = self._ct.c_int64(0)
+        self._lib.check(self._lib.load().mgdp_comm_host_waits(self.handle, self._ct.byref(c), None),
+                        "mgdp_comm_host_waits")
+        return int(c.value)
 
     def collect(self) -> float:
         return self.device_ms
@@ -376,20 +419,18 @@ def solve_sharded(vi, group=None, reducer=None, comm=None) -> dict:
     library's own collectives -- one mgdp_vi_solve_sharded call per solve on ranks whose shard can
     run it, the same collectives host-driven on the others."""
     if comm is not None:
-        n0 = comm.allreduces
+        n0, w0 = comm.allreduces, comm.host_waits
         if getattr(vi, "sharded_capable", False):
             k = vi.solve_sharded(comm)
-            if hasattr(comm, "host_reads"):
-                comm.host_reads += 1
             return {"sweeps": k, "dv": vi.dv, "converged": vi.converged, "allreduces": comm.allreduces - n0,
-                    "host_reads": 1, "protocol": "lib"}
+                    "host_reads": comm.host_waits - w0, "protocol": "lib"}
         k, dv = _lib_host_protocol(vi, comm)
         while not (dv < vi.tol) and k < vi.max_sweeps:
             dv = bits_to_double(comm.allreduce_max([double_to_bits(vi.sweep())])[0])
             k += 1
         vi.finish(k, dv)
         return {"sweeps": k, "dv": dv, "converged": dv < vi.tol, "allreduces": comm.allreduces - n0,
-                "host_reads": comm.allreduces - n0, "protocol": "lib-host"}
+                "host_reads": comm.host_waits - w0, "protocol": "lib-host"}
     red = reducer or Reducer(group)
     device = _device_capable(vi, red)
     calls0, reads0 = red.calls, red.host_reads

@@ -29,7 +29,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_version_and_error_string():
     L = _lib.load()
-    assert L.mgdp_abi_version() == _lib.ABI_VERSION == 11
+    assert L.mgdp_abi_version() == _lib.ABI_VERSION == 12
     n = ctypes.c_int32(-1)
     assert L.mgdp_device_count(ctypes.byref(n)) == 0
     assert n.value >= 0

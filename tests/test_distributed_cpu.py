@@ -350,6 +350,7 @@ class GlooLibComm:
 
     def __init__(self):
         self.allreduces = 0
+        self.host_waits = 0  # as mgdp_comm_host_waits: one per host-driven all-reduce (+ the C path's own)
 
     def allreduce_max(self, vals):
         import torch
@@ -358,6 +359,7 @@ class GlooLibComm:
         t = torch.tensor([int(v) for v in vals], dtype=torch.int64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         self.allreduces += 1
+        self.host_waits += 1
         return [int(x) for x in t.tolist()]
 
 
@@ -372,7 +374,9 @@ class LibOracleShard(OracleShard):
         self.reset()
         k_loc = self.run_local()
         K, e_bits = comm.allreduce_max([k_loc, double_to_bits(self._local[1])])
+        comm.host_waits -= 1  # the C path's {K, E} all-reduce stays on the stream ...
         dv = self.run_to(K)
+        comm.host_waits += 1  # ... and its one host wait is run_to's result
         if bits_to_double(e_bits) != 0.0:
             dv = bits_to_double(comm.allreduce_max([double_to_bits(dv)])[0])
         k = K
@@ -396,7 +400,7 @@ def _lib_worker(rank, world, port, cells, slip, out, kinds):
     shard = EmptyShard() if hi == lo else (LibOracleShard if kind == "lib" else OracleShard)(cells[lo:hi], slip=slip)
     res = solve_sharded(shard, comm=comm)
     out[rank] = (res["sweeps"], res["allreduces"], getattr(shard, "V", None), getattr(shard, "pi", None), lo, hi,
-                 res["protocol"])
+                 res["protocol"], res["host_reads"])
     dist.barrier()
     dist.destroy_process_group()
 
@@ -414,10 +418,13 @@ def test_lib_comm_protocol_matches_global_loop(world, kinds, slip):
     out = mgr.dict()
     mp.spawn(_lib_worker, args=(world, port, cells, slip, out, kinds), nprocs=world, join=True)
     res = dict(out)
-    for r, (k, n, V, pi, lo, hi, proto) in res.items():
+    for r, (k, n, V, pi, lo, hi, proto, waits) in res.items():
         assert k == ref["sweeps"]
         # deterministic: one collective per solve; slip: the dV(K) word too
         assert n == (1 if slip is None else 2) or (slip is not None and n >= 2)
+        # host waits: every collective of a host-driven rank; on the C path the {K, E} all-reduce stays on
+        # the stream and run_to's result is the wait instead -- so the count equals the collectives either way
+        assert waits == n
         assert proto == ("lib" if (hi > lo and kinds[r % len(kinds)] == "lib") else "lib-host")
         if hi > lo:
             np.testing.assert_array_equal(V, ref["V"][lo:hi])

@@ -72,10 +72,10 @@ mode = sys.argv[2]
 env_id, B, dtype = sys.argv[3], int(sys.argv[4]), sys.argv[5]
 slip = float(sys.argv[6]) if len(sys.argv) > 6 else None
 cells = gen.generate(env_id, 0, B, enc=False, cells=True, agent=False)["cells"]
-ref = mg.ValueIteration(cells, dtype=dtype, slip_p=slip)
-k_ref = ref.solve()
-V_ref, pi_ref = ref.values(), ref.policy()
-ref.close()
+# the reference is the CPU oracle's literal global Jacobi loop over the whole batch (tests only)
+from oracle import oracle
+o = oracle.value_iteration(1 if "DoorKey" in env_id else 0, cells, slip_p=slip, dtype=dtype, nthreads=8)
+k_ref, V_ref, pi_ref = o["sweeps"], o["V"], o["pi"]
 vi = mg.ValueIteration(cells, dtype=dtype, slip_p=slip)
 if mode == "steps":
     # the C entry points alone, on a torch stream: K and dV stay in device memory between launches
@@ -166,7 +166,8 @@ def test_device_protocol(mode, env_id, B, dtype):
     RCCL group (the all-reduces are real RCCL collectives ordered on the protocol stream); "lib1":
     the library's own RCCL communicator (mgdp_vi_solve_sharded, one C call per solve) plus a
     sweep-method handle joining its collectives host-driven.  Batches
-    on both sides of the in-kernel-reduce limit (512) and a lone grid; equal to a one-device solve."""
+    on both sides of the in-kernel-reduce limit (512) and a lone grid; every mode equal to the CPU
+    oracle's global loop (sweeps, V, pi bit for bit)."""
     import subprocess
     import sys
 
@@ -182,7 +183,7 @@ def test_device_protocol(mode, env_id, B, dtype):
 @pytest.mark.parametrize("B", [300, 2048])
 def test_device_protocol_rccl1_slip(B, mode):
     """Slip grids over a one-rank RCCL group: the own-rule dV is not an exact fixed point, so the
-    protocol all-reduces dV at K too (two collectives) and still equals a one-device solve."""
+    protocol all-reduces dV at K too (two collectives) and still equals the oracle's global loop."""
     import subprocess
     import sys
 
@@ -192,3 +193,85 @@ def test_device_protocol_rccl1_slip(B, mode):
     r = subprocess.run([sys.executable, "-c", _DEVICE_PROTO, root, mode, "MiniGrid-LavaCrossingS11N5-v0", str(B),
                         "f32", "0.9"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "device protocol ok" in r.stdout, r.stdout + r.stderr
+
+
+# -- mgdp_vi_solve_sharded at world > 1 on one GPU: the host communicator -----------------------------
+def _multi_worker(rank, world, port, env_id, B, dtype, slip, kinds, out):
+    """One rank: a gloo group for the bootstrap, the library's host communicator (mgdp_comm_create_host),
+    and this rank's shard on the path its kind names: "lib" = a fused handle, one mgdp_vi_solve_sharded
+    call per solve (the C code's collectives); "host" = a sweep-method handle driving the same
+    collectives from Python (mgdp_comm_allreduce_max); "empty" = no grids (EmptyShard)."""
+    import torch.distributed as dist
+
+    import minigrid_dynamicprogramming_amd as mg
+    from minigrid_dynamicprogramming_amd import gen
+    from minigrid_dynamicprogramming_amd.distributed import EmptyShard, LibComm, shard_range, solve_sharded
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    kind = kinds[rank]
+    holders = [r for r in range(world) if kinds[r] != "empty"]
+    lo = hi = 0
+    if kind != "empty":
+        lo, hi = shard_range(B, holders.index(rank), len(holders))
+    cells = gen.generate(env_id, 0, B, enc=False, cells=True, agent=False)["cells"]
+    comm = LibComm(kind="host", device=0)
+    if kind == "empty":
+        shard = EmptyShard()
+    else:
+        shard = mg.ValueIteration(cells[lo:hi], dtype=dtype, slip_p=slip, method="fused" if kind == "lib" else "sweep")
+    res = []
+    for _ in range(2):  # a second solve on the same communicator and handles
+        r = solve_sharded(shard, comm=comm)
+        res.append((r["sweeps"], r["allreduces"], r["host_reads"], r["protocol"]))
+    V = shard.values() if kind != "empty" else None
+    pi = shard.policy() if kind != "empty" else None
+    out[rank] = (res, V, pi, lo, hi, comm.kind)
+    if kind != "empty":
+        shard.close()
+    comm.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("env_id,B,dtype,slip,kinds", [
+    ("MiniGrid-FourRooms-v0", 96, "f32", None, ("lib", "lib")),
+    ("MiniGrid-FourRooms-v0", 96, "f32", None, ("lib", "host")),
+    ("MiniGrid-LavaCrossingS11N5-v0", 600, "f32", 0.9, ("lib", "lib")),
+    ("MiniGrid-LavaCrossingS11N5-v0", 600, "f32", 0.9, ("host", "lib")),
+    ("MiniGrid-LavaCrossingS11N5-v0", 2048, "f32", None, ("lib", "host", "empty", "lib")),
+    ("MiniGrid-FourRooms-v0", 300, "f64", 0.9, ("lib", "empty", "lib", "host")),
+    ("MiniGrid-DoorKey-16x16-v0", 64, "f32", None, ("lib", "lib", "lib", "lib")),
+])
+def test_solve_sharded_multi_rank_host_comm(env_id, B, dtype, slip, kinds):
+    """The unchanged C entry mgdp_vi_solve_sharded at world 2 and 4 on one GPU (RCCL refuses two ranks
+    on one device, so the ranks share the host communicator): fused ranks on the C path next to
+    host-driven sweep-method ranks and empty shards, deterministic and slip grids.  Every rank ends at
+    the oracle's global stopping sweep with its block's V and pi bit for bit, and every rank issues
+    the same collectives: 1 per deterministic solve, >= 2 for slip (the dV(K) word), equal on all ranks
+    (the C sequence is the Python restatement's)."""
+    from oracle import oracle
+    from minigrid_dynamicprogramming_amd import gen
+
+    cells = gen.generate(env_id, 0, B, enc=False, cells=True, agent=False)["cells"]
+    o = oracle.value_iteration(1 if "DoorKey" in env_id else 0, cells, slip_p=slip, dtype=dtype, nthreads=8)
+    world = len(kinds)
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_multi_worker, args=(world, _port(), env_id, B, dtype, slip, kinds, out), nprocs=world, join=True)
+    got = dict(out)
+    assert sorted(got) == list(range(world))
+    counts = set()
+    for rank, (res, V, pi, lo, hi, ckind) in got.items():
+        assert ckind == "host"  # the host communicator
+        for k, nred, nwait, proto in res:
+            assert k == o["sweeps"], (rank, k, o["sweeps"])
+            assert proto == ("lib" if kinds[rank] == "lib" else "lib-host"), (rank, proto)
+            assert nred == 1 if slip is None else nred >= 2
+            assert nwait >= 1
+            counts.add(nred)
+        if kinds[rank] != "empty":
+            np.testing.assert_array_equal(V, o["V"][lo:hi])
+            np.testing.assert_array_equal(pi, o["pi"][lo:hi])
+    assert len(counts) == 1, counts  # every rank met the same collectives

@@ -18,6 +18,10 @@
 //  13 as 9 with the flag of sweep k written after barrier k (at sweep k+1's start, from the ballot
 //     kept in a register) and read at sweep k+2's start: the write waits for nothing
 //  14 as 13 with the DPP east/west fronts
+//  15 TWO sweeps per barrier (round 6): 4 planes written per pair, the N/S fronts of the pair's second
+//     sweep from the first sweep's lanes +-16 by ds_bpermute (one halo value per boundary lane from
+//     3 extra LDS reads), both sweeps' ballots in one flag byte; clock64 per PAIR / 2 reported
+//  16 as 15 with the +-16 lane shifts by v_permlane16_swap / v_permlane32_swap (VALU, no LDS)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -31,6 +35,23 @@ __device__ __forceinline__ float dpp_row_shr1(float v) {
 }
 __device__ __forceinline__ float dpp_row_shl1(float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x101, 0xf, 0xf, false));
+}
+
+// lane l <- lane l + 16 (rows 0..2 of the wave's four 16-lane rows; row 3 takes `edge`)
+__device__ __forceinline__ float shift_up16_pl(float x, float edge, int row) {
+    const unsigned int u = __float_as_uint(x);
+    auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);   // r[0] = (X0,X0,X2,X2), r[1] = (X1,X1,X3,X3)
+    auto q = __builtin_amdgcn_permlane32_swap(r[0], r[0], false, false);  // q[1] = (X2,X2,X2,X2)
+    const float b = __uint_as_float(r[1]), x2 = __uint_as_float(q[1]);
+    return row == 3 ? edge : (row == 1 ? x2 : b);
+}
+// lane l <- lane l - 16 (rows 1..3; row 0 takes `edge`)
+__device__ __forceinline__ float shift_down16_pl(float x, float edge, int row) {
+    const unsigned int u = __float_as_uint(x);
+    auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);   // r[0] = (Y0,Y0,Y2,Y2), r[1] = (Y1,Y1,Y3,Y3)
+    auto q = __builtin_amdgcn_permlane32_swap(r[1], r[1], false, false);  // q[0] = (Y1,Y1,Y1,Y1)
+    const float a = __uint_as_float(r[0]), y1 = __uint_as_float(q[0]);
+    return row == 0 ? edge : (row == 2 ? y1 : a);
 }
 
 template <int V>
@@ -49,7 +70,59 @@ __global__ __launch_bounds__(256) void chain(float *out, long long *cyc, float g
     bool more = true;
     const long long t0 = clock64(), r0 = wall_clock64();
     for (int it = 0; it < ITERS; ++it) {
-        if constexpr (V == 0) {
+        if constexpr (V == 15 || V == 16) {
+            if (it & 1) continue;  // one pair per two iterations
+            const float *tin = tiles[parity];
+            float *tout = tiles[parity ^ 1];
+            const int lane = c & 63, row = lane >> 4;
+            const unsigned int fl = *reinterpret_cast<const unsigned int *>(flags + (parity ^ 1) * 16);
+            const float fS = tin[nb[1]], fN = tin[nb[3]];
+            const bool bottom = row == 3;
+            const int hc = bottom ? (c + 16) & 255 : (c + 240) & 255;
+            const float h0 = tin[hc], h2 = tin[512 + hc];
+            const float hf = bottom ? tin[256 + ((hc + 16) & 255)] : tin[768 + ((hc + 240) & 255)];
+            const float hs = bottom ? fS : fN;
+            float o[4], dm1 = 0.f;
+            {
+                const float f[4] = {dpp_row_shl1(own[0]), fS, dpp_row_shr1(own[2]), fN};
+                const float a = fmaxf(own[0], own[2]), b = fmaxf(own[1], own[3]);
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const float m = fmaxf(fmaxf((d & 1) ? a : b, own[d]), f[d]);
+                    o[d] = fmaxf(g * m, goal ? 1.0f : 0.0f);
+                    dm1 = fmaxf(dm1, fabsf(o[d] - own[d]));
+                }
+            }
+            const float hv = fmaxf(g * fmaxf(fmaxf(h0, h2), fmaxf(hs, hf)), goal ? 1.0f : 0.0f);
+            float S2, N2;
+            if constexpr (V == 15) {
+                S2 = bottom ? hv : __int_as_float(__builtin_amdgcn_ds_bpermute(((c + 16) & 63) * 4, __float_as_int(o[1])));
+                N2 = row == 0 ? hv : __int_as_float(__builtin_amdgcn_ds_bpermute(((c + 48) & 63) * 4, __float_as_int(o[3])));
+            } else {
+                S2 = shift_up16_pl(o[1], hv, row);
+                N2 = shift_down16_pl(o[3], hv, row);
+            }
+            float o2[4], dm2 = 0.f;
+            {
+                const float f[4] = {dpp_row_shl1(o[0]), S2, dpp_row_shr1(o[2]), N2};
+                const float a = fmaxf(o[0], o[2]), b = fmaxf(o[1], o[3]);
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const float m = fmaxf(fmaxf((d & 1) ? a : b, o[d]), f[d]);
+                    o2[d] = fmaxf(g * m, goal ? 1.0f : 0.0f);
+                    dm2 = fmaxf(dm2, fabsf(o2[d] - o[d]));
+                }
+            }
+            if (it > 0 && fl == 0u) more = false;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) tout[d * 256 + c] = o2[d];
+            const unsigned int bits = (__ballot(dm1 >= tol) != 0ull ? 1u : 0u) | (__ballot(dm2 >= tol) != 0ull ? 2u : 0u);
+            if ((c & 63) == 0) flags[parity * 16 + (c >> 6)] = bits;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) own[d] = o2[d];
+            parity ^= 1;
+            __syncthreads();
+        } else if constexpr (V == 0) {
             __syncthreads();
         } else if constexpr (V == 1) {
             tiles[it & 1][c] = own[0];
@@ -172,6 +245,8 @@ int main() {
     run<12>(d_out, d_cyc);
     run<13>(d_out, d_cyc);
     run<14>(d_out, d_cyc);
+    run<15>(d_out, d_cyc);
+    run<16>(d_out, d_cyc);
     CHECK(hipFree(d_out));
     CHECK(hipFree(d_cyc));
     return 0;
