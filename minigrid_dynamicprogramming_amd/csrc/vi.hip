@@ -112,6 +112,7 @@ struct mgdp_vi {
     int wave_p = 0;               // lone XYD grid on one wave: cells per lane (fused_wave_xyd)
     int cpt = 1;                  // batched XYD fused path: cells per thread (MGDP_CPT; 2 = fused_fast_xyd_soa_x2)
     int serve_ew = 0;             // served lone deterministic XYD grid on fused_serve_xyd (MGDP_SERVE_EW=0: off)
+    int serve_pair = 0;           // ... two sweeps per barrier, fused_serve_pair (MGDP_SERVE_PAIR=0: off)
     int dk1t = 0;                 // batched fp32 DoorKey on one LDS tile (MGDP_DK_1T; fused_fast_dk_1t)
     int dkhalf = 0;               // batched DoorKey, states split by has_key over two threads (MGDP_DK_HALF; fused_dk_half)
     int dkrow = 0;                // batched DoorKey of width 16 on whole-row thread maps (MGDP_DK_ROWS; fused_dk_rows)
@@ -496,7 +497,8 @@ int launch_serve_t(mgdp_vi *vi, unsigned int served) {
     if constexpr (MODEL == MGDP_MODEL_XYD && MAP == MGDP_MAP_CELL) {
         if (vi->cpt == 2) kern = ServeK<T, MODEL, SLIP, MAP, -2>::fn;
         if constexpr (!SLIP) {
-            if (vi->serve_ew) kern = ServeK<T, MODEL, SLIP, MAP, kWpServeEw>::fn;
+            if (vi->serve_ew) kern = vi->serve_pair ? ServeK<T, MODEL, SLIP, MAP, kWpServePair>::fn
+                                                    : ServeK<T, MODEL, SLIP, MAP, kWpServeEw>::fn;
             if (vi->band) kern = pick_band<ServeK, T, MODEL, SLIP, MAP>(vi->band, kern);
         }
     }
@@ -1042,6 +1044,18 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
         vi->serve_ew = serve_ew && d.B == 1 && d.model == MGDP_MODEL_XYD && d.method == MGDP_METHOD_FUSED &&
                        d.slip_p < 0.0 && !vi->pair && !vi->quad && !vi->opts && !vi->wave_p && vi->cpt == 1 &&
                        vi->fused_block <= 256 && vi->HWs >= vi->fused_block && 2 * vi->HWs >= 3 * padw;
+        // ... with two sweeps per workgroup barrier (fused_serve_pair): its two four-plane tiles take the
+        // first V buffers (nbuf raised to hold them; MGDP_SERVE_PAIR=0: off)
+        int serve_pair = 1;
+        if (const char *ev = std::getenv("MGDP_SERVE_PAIR")) serve_pair = std::atoi(ev);
+        if (vi->serve_ew && serve_pair) {
+            const int need = 2 * serve_pair_tile_elems(vi->HWs, d.W);
+            const int nbuf = std::max(2, (need + vi->Ss - 1) / vi->Ss);
+            if (smem_layout(vi->Ss, vi->HWp, vi->tsize, nbuf).total() <= 64 * 1024) {
+                vi->serve_pair = 1;
+                vi->nbuf = nbuf;
+            }
+        }
         // The served lone deterministic XYD grid on ONE wave in column bands (fused_band_xyd: no
         // barrier, no LDS tile; MGDP_SERVE_BAND=1, A/B)
         int serve_band = 0;
@@ -1051,6 +1065,8 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
             !vi->pair && !vi->quad && !vi->opts && hb1 >= 1 && hb1 <= 8) {
             vi->band = hb1;
             vi->serve_ew = 0;
+            if (vi->serve_pair) vi->nbuf = 2;
+            vi->serve_pair = 0;
             vi->wave_p = 0;
             vi->cpt = 1;
             vi->fused_block = 64;
@@ -1607,6 +1623,7 @@ int comm_max_double(mgdp_comm *c, hipStream_t s, double *x) {
     if (int rc = comm_allreduce_max_dev(c, d, 1, s)) return rc;
     MGDP_HIP(hipMemcpyAsync(h, d, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     MGDP_HIP(hipStreamSynchronize(s));
+    comm_note_host_wait(c);
     std::memcpy(x, h, sizeof(double));
     return 0;
 }
@@ -1626,6 +1643,7 @@ int mgdp_vi_solve_sharded(mgdp_vi *vi, mgdp_comm *comm, int32_t *sweeps_out, dou
     int32_t k = 0;
     double dv = 0.0, rule = 0.0;
     if (int rc = mgdp_vi_run_to_dev_sync(vi, p, &k, &dv, &rule)) return rc;  // the solve's one host wait
+    comm_note_host_wait(comm);
     if (rule == 0.0) {
         // every grid of every rank stopped at an exact fixed point: dV at K is 0 everywhere
         MGDP_CHECK(dv == 0.0, MGDP_E_INVALID, "fixed-point invariant violated: dV at sweep %d is %g", k, dv);
@@ -1733,7 +1751,7 @@ const char *mgdp_vi_variant(const mgdp_vi *vi) {
     if (serve_eligible(vi)) {
         if (vi->dkhalf) return "serve_dk_half";
         if (vi->band) return "serve_band";
-        if (vi->serve_ew) return "serve_ew";
+        if (vi->serve_ew) return vi->serve_pair ? "serve_pair" : "serve_ew";
         return vi->wave_p ? "serve_wave" : "serve";
     }
     if (vi->dkrow) return "dk_rows";

@@ -89,6 +89,9 @@ constexpr int kWpDkHalf = -500;
 // vi_serve_kernel variant tag: the served lone deterministic XYD grid on fused_serve_xyd (east / west
 // fronts by DPP; <= 4 waves), fused_fast_xyd_soa for a grid whose wave edges do not allow it
 constexpr int kWpServeEw = -600;
+// ... the same grids with two sweeps per workgroup barrier (fused_serve_pair, round 6)
+constexpr int kWpServePair = -601;
+__host__ __device__ constexpr bool wp_is_serve_ew(int wp) { return wp == kWpServeEw || wp == kWpServePair; }
 // MGDP_DK_PERM=0 (A/B builds): batched DoorKey grids keep thread t on cell t (no dk_class_perm)
 #ifndef MGDP_DK_PERM
 #define MGDP_DK_PERM 1
@@ -293,7 +296,7 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
     constexpr bool SOA_ONLY = WP < 0;  // every negative tag runs the direction-major path alone
     constexpr bool PAIR2 = wp_is_pair(WP);
     constexpr bool DKHALF = wp_is_dkhalf(WP);
-    constexpr bool SERVE_EW = WP == kWpServeEw;
+    constexpr bool SERVE_EW = wp_is_serve_ew(WP);
     constexpr int CPT = PAIR2 ? 2 : (WP < 0 && !DK1T && !DKHALF && !SERVE_EW && WP != kWpSoa ? -WP : 1);
     const bool fast = MAP == MGDP_MAP_CELL && geo.HW <= CPT * (int)blockDim.x;
     const bool soa = SOA_ONLY || (fast && !geo.pair && !geo.quad);
@@ -351,10 +354,22 @@ __device__ __forceinline__ bool fused_grid(const Geo &geo, const Coef<T> &cf, co
             else fused_fast_dk_1t<T, false>(geo, cf, cl, V0, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
         } else if constexpr (SERVE_EW) {
             static_assert(SERVED && MODEL == MGDP_MODEL_XYD && !SLIP && MAP == MGDP_MAP_CELL, "served plain XYD grid");
-            // ew: 0 = this grid falls back, 1 = fused_serve_xyd, 2 = the same, first solve of the grid
-            if (ew) fused_serve_xyd<T>(geo, cf, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, dvl, done, *pre, ew == 2);
-            else fused_fast_xyd_soa<T, false, true>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target,
-                                                     dvl, done, nullptr, nullptr, 0, pre);
+            // ew: 0 = this grid falls back, 1 = fused_serve_xyd (kWpServePair: fused_serve_pair), 2 = the
+            // same, first solve of the grid
+            bool ran = false;
+            if constexpr (WP == kWpServePair) {
+                if (ew) {
+                    fused_serve_pair<T>(geo, cf, V0, V0 + serve_pair_tile_elems(geo.HWs, geo.W), slots, flags,
+                                        V + vb, V + vb, pi + vb, k, dvl, done, *pre, ew == 2);
+                    ran = true;
+                }
+            } else if (ew) {
+                fused_serve_xyd<T>(geo, cf, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, dvl, done, *pre, ew == 2);
+                ran = true;
+            }
+            if (!ran)
+                fused_fast_xyd_soa<T, false, true>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target,
+                                                   dvl, done, nullptr, nullptr, 0, pre);
         } else if constexpr (MODEL == MGDP_MODEL_XYD && CPT > 1) {
             if (k_target < 0) fused_fast_xyd_soa_xn<T, SLIP, true, CPT>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
             else fused_fast_xyd_soa_xn<T, SLIP, false, CPT>(geo, cf, cl, V0, V1, slots, flags, V + vb, V + vb, pi + vb, k, k_target, dvl, done);
@@ -521,8 +536,10 @@ __device__ __forceinline__ void poll_issue(const unsigned long long *src, unsign
         : "memory");
 }
 
+// (kWpServePair: <= 4 waves by the host's serve_ew rule, so its three register sets and halo state may
+// use up to 512 VGPRs per lane: no spill)
 template <typename T, int MODEL, bool SLIP, int MAP, int WP = 0>
-__global__ void __launch_bounds__(WP > 0 ? 64 : 1024)
+__global__ void __launch_bounds__(WP > 0 ? 64 : (WP == kWpServePair ? 256 : 1024))
 vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict__ V,
                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
                 unsigned long long *__restrict__ host_out, const unsigned long long *__restrict__ host_cmd,
@@ -552,12 +569,13 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
     int ew = 0;  // kWpServeEw: 0 = the grid falls back, 1 = fused_serve_xyd, 2 = the same, tiles to clear
     __shared__ int s_ew;
     auto resolve = [&]() {
-        if constexpr (WP == 0 || WP == kWpServeEw) {
+        if constexpr (WP == 0 || wp_is_serve_ew(WP)) {
             const int cc = (int)threadIdx.x < geo.HW ? (int)threadIdx.x : 0;
             if constexpr (MODEL == MGDP_MODEL_XYD) topo = xyd_topo_soa<T>(cl, geo, cc);
             else topo = dk_topo_soa(cl, geo, cc);
         }
-        if constexpr (WP == kWpServeEw) ew = serve_ew_ok(cl, geo, &s_ew) ? 2 : 0;
+        if constexpr (WP == kWpServePair && MODEL == MGDP_MODEL_XYD) topo.halo = serve_pair_halo(cl, geo, (int)threadIdx.x);
+        if constexpr (wp_is_serve_ew(WP)) ew = serve_ew_ok(cl, geo, &s_ew) ? 2 : 0;
     };
     resolve();
     while (true) {
@@ -621,7 +639,7 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
         double dvl;
         if (!fused_grid<T, MODEL, SLIP, MAP, true, WP>(geo, cf, cells, V, pi, kenv, dvenv, host_out, -1, 1, true,
                                                    (unsigned int)cmd, 0, k, dvl,
-                                                   (WP == 0 || WP == kWpServeEw) ? &topo : nullptr, nullptr, ew) &&
+                                                   (WP == 0 || wp_is_serve_ew(WP)) ? &topo : nullptr, nullptr, ew) &&
             threadIdx.x == 0)
             publish_tagged(host_out, k, dvl, (unsigned int)cmd);
         if (ew == 2) ew = 1;  // the tiles' pads stay +0 until the next grid

@@ -581,6 +581,215 @@ __device__ __forceinline__ void fused_serve_xyd(const Geo &geo, const Coef<T> &c
     }
 }
 
+// The served lone deterministic XYD grid, TWO sweeps per workgroup barrier (vi_serve_kernel,
+// WP = kWpServePair; grids on <= 4 waves whose wave edges pass serve_ew_ok).  Round 6.  A lone grid's
+// sweep is latency-bound: its LDS write -> s_barrier -> LDS read round trip and the stop test's
+// ballot / flag byte around it cost more than the arithmetic (tools/probe_sweep_chain.hip,
+// profiles/r06_dist/: 449 cycles per sweep with the round trip, 289 without the stop test).  Here a
+// workgroup barrier closes every second sweep:
+//  * The pair reads V_k from the input tile (all four planes are kept in LDS): its own cell's north /
+//    south fronts as fused_serve_xyd, and the values its NEIGHBOURS' sweep k+1 needs for the two
+//    planes this cell's sweep k+2 reads: plane 1 of cell c + W (planes 0, 1, 2 there and plane 1 of
+//    c + 2W) and plane 3 of cell c - W (planes 0, 2, 3 there and plane 3 of c - 2W).  So each lane
+//    computes sweep k+1 of its own cell (fused_serve_xyd's arithmetic) and those two neighbour values
+//    (the same max of the same four V_k values, the same multiply and goal select as their owners:
+//    bit-identical), and sweep k+2 needs nothing from another lane but its east / west fronts, by
+//    DPP as in fused_serve_xyd: no cross-wave (or cross-lane LDS) exchange inside the pair.
+//  * Sweep k+2 then writes its four planes; each wave's two ballots (|dV| >= tol of sweeps k+1 and
+//    k+2, a bit also 0 at the max_sweeps cap) go into one flag byte, and the barrier closes the pair.
+//  * The next pair tests both bits behind its first sweep's arithmetic (the flag dword travels with
+//    the data reads; that sweep writes only the set that held V_{k-2}; testing before it measured
+//    slower: the test's scalar chain then sits in front of every pair's VALU work): stop after sweep
+//    k-1 (V_{k-1} = the last pair's middle set, pi from V_{k-2}: the last pair's input tile, all four
+//    planes, untouched) or after sweep k (V_k = its output set, pi from the middle set, whose north /
+//    south fronts are the last pair's two neighbour values).  So the rule, the cap (a pair may
+//    compute past it: discarded), the reported dV (the block max of the stopping sweep's |dV|) and
+//    pi (argmax on V_{K-1}, lowest index on ties) are fused_serve_xyd's, bit for bit.
+//  * The solve's first call computes one sweep (its first half is the identity), so the pairs cover
+//    sweeps (k_start + 2, k_start + 3), ...: a stop on a pair's second sweep costs the next pair's
+//    first-sweep arithmetic only, a stop on its first sweep that and the pair's second sweep
+//    (Empty-16's 29 sweeps from 0 end on a second sweep).
+//  * Three register sets rotate (in, middle, out) with the two tiles: the loop is unrolled by six
+//    pairs.  LDS: two tiles of four planes, each [pad][HWs cells][pad], pad = round_up(2W, 16), the
+//    host sizes the V buffers for them (serve_pair_tile_elems).
+// Requires k < max_sweeps on entry (fused_grid only calls with work to do).
+__host__ __device__ inline int serve_pair_pad(int W) { return (2 * W + 15) / 16 * 16; }
+__host__ __device__ inline int serve_pair_plane(int HWs, int W) { return HWs + 2 * serve_pair_pad(W); }
+__host__ __device__ inline int serve_pair_tile_elems(int HWs, int W) { return 4 * serve_pair_plane(HWs, W); }
+
+// The pair loop's neighbour topology of thread t (resolved once per grid by the server): bit 0 the
+// cell t + W is walkable, bit 1 a goal lies south of it (its plane 1 is then max(., 1)); bits 2 / 3
+// the same for t - W and north.  Cells outside the grid: 0 (their value is +0, the geometric front).
+__device__ __forceinline__ uint32_t serve_pair_halo(const uint8_t *cl, const Geo &geo, int t) {
+    const int W = geo.W;
+    uint32_t h = 0;
+    const int s = t + W, n = t - W;  // a walkable cell is interior: its own fronts are in the grid
+    if (t < geo.HW && s < geo.HW && xyd_free(cl[s])) h |= 1u | (cl[s + W] == T_GOAL ? 2u : 0u);
+    if (t < geo.HW && n >= 0 && xyd_free(cl[n])) h |= 4u | (cl[n - W] == T_GOAL ? 8u : 0u);
+    return h;
+}
+
+template <typename T, typename Done>
+__device__ __forceinline__ void fused_serve_pair(const Geo &geo, const Coef<T> &cf, T *T0, T *T1, T *slots,
+                                                 uint8_t *flags, const T *Vg, T *Vg_out, int8_t *pig, int &k,
+                                                 double &dvl, const Done &done, const XydTopo<T> &tp,
+                                                 bool zero_tiles) {
+    const int c = threadIdx.x, lane = c & 63;
+    const int cc = c < geo.HW ? c : 0;
+    const bool own_cell = c < geo.HW;
+    const int W = geo.W, PL = serve_pair_plane(geo.HWs, W);
+    k = __builtin_amdgcn_readfirstlane(k);  // uniform: the sweep count in an SGPR
+    const int o0 = serve_pair_pad(W) + c;  // plane d of this cell at d * PL + o0
+    const T ge = tp.valid ? cf.g : (T)0;
+    T tq[4];  // the goal rewards in registers for the loop (the server's topology may live in memory)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) tq[d] = tp.tq[d];
+    // the neighbours' topology: cell c + W (its plane 1), cell c - W (its plane 3)
+    const T geS = (tp.halo & 1u) ? cf.g : (T)0, tqS = (tp.halo & 2u) ? (T)1 : (T)0;
+    const T geN = (tp.halo & 4u) ? cf.g : (T)0, tqN = (tp.halo & 8u) ? (T)1 : (T)0;
+    T A[4], B[4], C[4];
+    {
+        V4<T> x = V4<T>{{(T)0, (T)0, (T)0, (T)0}};
+        if (k != 0) x = *reinterpret_cast<const V4<T> *>(Vg + cc * 4);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) A[d] = own_cell ? x.v[d] : (T)0;
+    }
+    if (zero_tiles) {
+        const int te = 4 * PL;
+        for (int i = c; i < te; i += blockDim.x) {  // pads (and planes) of both tiles start at +0
+            T0[i] = (T)0;
+            T1[i] = (T)0;
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        B[d] = (T)0;
+        C[d] = (T)0;
+        T0[d * PL + o0] = A[d];
+    }
+    __syncthreads();
+    uint8_t *const fwave = flags + (threadIdx.x >> 6);
+    const bool lane0 = lane == 0;
+    // the last pair's |dV| of its two sweeps and its middle set's north / south fronts
+    T dm1p = (T)0, dm2p = (T)0, vSp = (T)0, vNp = (T)0;
+    int stop = 0;  // 1: K = k - 1, 2: K = k
+    // one sweep of this lane's cell from its own values and its four geometric fronts (fused_serve_xyd's)
+    auto step = [&](const T (&in)[4], const T fE, const T fS, const T fW, const T fN, T (&out)[4]) -> T {
+        const T m02 = vmax(in[0], in[2]), m13 = vmax(in[1], in[3]);
+        const T m[4] = {vmax(vmax(in[0], m13), fE), vmax(vmax(in[1], m02), fS), vmax(vmax(in[2], m13), fW),
+                        vmax(vmax(in[3], m02), fN)};
+        T dm = (T)0;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            out[d] = vmax(ge * m[d], tq[d]);
+            dm = vmax(dm, vabs(out[d] - in[d]));
+        }
+        return dm;
+    };
+    // par: this pair's flag slot (a constant at each unrolled call); test: whether a previous pair exists.
+    // The sets rotate so that `mid` held V_{k-2} (dead: its planes are in Tout) and `out` holds the last
+    // pair's middle set V_{k-1} until the test has passed.  half (the solve's first call): the first
+    // sweep is the identity (mid = in, its neighbours' values read from the tile): ONE sweep.
+    auto pair = [&](const T *Tin, T *Tout, const T (&in)[4], T (&mid)[4], T (&out)[4], const int par,
+                    auto test, auto half) -> bool {
+        constexpr bool HALF = decltype(half)::value;
+        const uint32_t fl = *reinterpret_cast<const uint32_t *>(flags + (par ^ 1) * 16);
+        const T fS = Tin[PL + o0 + W], fN = Tin[3 * PL + o0 - W];
+        T dm1 = (T)0, vS, vN;
+        if (HALF) {
+#pragma unroll
+            for (int d = 0; d < 4; ++d) mid[d] = in[d];
+            vS = fS;
+            vN = fN;
+        } else {
+            const T s0 = Tin[o0 + W], s2 = Tin[2 * PL + o0 + W], sf = Tin[PL + o0 + 2 * W];
+            const T n0 = Tin[o0 - W], n2 = Tin[2 * PL + o0 - W], nf = Tin[3 * PL + o0 - 2 * W];
+            dm1 = step(in, dpp_shl1_zero(in[0]), fS, dpp_shr1_zero(in[2]), fN, mid);
+            // sweep k+1 of plane 1 of c + W and plane 3 of c - W (their owners' arithmetic)
+            vS = vmax(geS * vmax(vmax(s0, s2), vmax(fS, sf)), tqS);
+            vN = vmax(geN * vmax(vmax(n0, n2), vmax(fN, nf)), tqN);
+            asm volatile("" ::"v"(vS), "v"(vN));  // reads and arithmetic ahead of the test (not sunk past it)
+        }
+        // the last pair's sweeps k - 1 and k (a bit is 0 when that sweep's |dV| < tol everywhere in the
+        // wave or it reached max_sweeps)
+        if (decltype(test)::value) {
+            if ((fl & 0x01010101u) == 0u) { stop = 1; return false; }
+            if ((fl & 0x02020202u) == 0u) { stop = 2; return false; }
+        }
+        const T dm2 = step(mid, dpp_shl1_zero(mid[0]), vS, dpp_shr1_zero(mid[2]), vN, out);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) Tout[d * PL + o0] = out[d];
+        constexpr int n = HALF ? 1 : 2;  // sweeps this call computes
+        const uint32_t bits = (HALF || (__ballot(dm1 >= cf.tol) != 0ull && k + 1 < geo.max_sweeps) ? 1u : 0u) |
+                              (__ballot(dm2 >= cf.tol) != 0ull && k + n < geo.max_sweeps ? 2u : 0u);
+        if (lane0) fwave[par * 16] = (uint8_t)bits;
+        dm1p = dm1;
+        dm2p = dm2;
+        vSp = vS;
+        vNp = vN;
+        __syncthreads();
+        k += n;
+        return true;
+    };
+    using Yes = std::integral_constant<bool, true>;
+    using No = std::integral_constant<bool, false>;
+    // p: the loop position of the pair that stopped, before its second sweep.  Its sets (in, out) by
+    // p % 3: (C, B), (B, A), (A, C) -- `in` = V_k, `out` = V_{k-1} (the last pair's middle set) -- and its
+    // output tile (T0 for even p) still holds V_{k-2}, the last pair's input.
+    int p;
+    pair(T0, T1, A, B, C, 0, No{}, Yes{});
+    while (true) {
+        if (!pair(T1, T0, C, A, B, 1, Yes{}, No{})) { p = 0; break; }
+        if (!pair(T0, T1, B, C, A, 0, Yes{}, No{})) { p = 1; break; }
+        if (!pair(T1, T0, A, B, C, 1, Yes{}, No{})) { p = 2; break; }
+        if (!pair(T0, T1, C, A, B, 0, Yes{}, No{})) { p = 3; break; }
+        if (!pair(T1, T0, B, C, A, 1, Yes{}, No{})) { p = 4; break; }
+        if (!pair(T0, T1, A, B, C, 0, Yes{}, No{})) { p = 5; break; }
+    }
+    const T diff = stop == 1 ? dm1p : dm2p;
+    if (stop == 1) k -= 1;
+    dvl = (double)block_max(diff, slots, 0);
+    done(k, dvl);
+    // element selects (a pointer to one of the sets would put them in scratch)
+    const int r = p % 3;
+    T vk_[4], vk1[4];  // V_k, V_{k-1}
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        vk_[d] = r == 0 ? C[d] : (r == 1 ? B[d] : A[d]);
+        vk1[d] = r == 0 ? B[d] : (r == 1 ? A[d] : C[d]);
+    }
+    const T *Tp = (p & 1) ? T1 : T0;  // V_{k-2}, all four planes
+    // V_K and V_{K-1}, and V_{K-1}'s fronts
+    T vk[4], vp[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        vk[d] = stop == 1 ? vk1[d] : vk_[d];
+        vp[d] = stop == 1 ? Tp[d * PL + o0] : vk1[d];
+    }
+    const T pS = stop == 1 ? Tp[PL + o0 + W] : vSp;
+    const T pN = stop == 1 ? Tp[3 * PL + o0 - W] : vNp;
+    const T pE = dpp_shl1_zero(vp[0]), pW = dpp_shr1_zero(vp[2]);
+    if (own_cell) {
+        // forward reads the front state when the agent can enter it, else its own (xyd_step's nbv)
+        const T geo_f[4] = {pE, pS, pW, pN};
+        const int HWs = geo.HWs;
+        T nbv[4];
+        V4<T> op;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            op.v[d] = vp[d];
+            const bool enter = tp.nbi[d] != d * HWs + c;
+            nbv[d] = enter ? geo_f[d] : vp[d];
+        }
+        V4<T> tmp;
+        uint32_t pk;
+        xyd_step<T, false, true>(tp, cf, op, nbv, tmp, pk);
+        *reinterpret_cast<uint32_t *>(pig + c * 4) = pk;
+        *reinterpret_cast<V4<T> *>(Vg_out + c * 4) = V4<T>{{vk[0], vk[1], vk[2], vk[3]}};
+    }
+}
+
 // Batched XYD grids with N cells per thread (cells t + j*blockDim, j < N; HWs = N * blockDim): the
 // same sweep as fused_fast_xyd_soa on 1/N of the waves, so the per-sweep fixed work of a wave (flag
 // read, address set-up, ballot, barrier) is paid once per N cells.  Plain deterministic / slip

@@ -154,6 +154,7 @@ struct XydTopo {
     int nbi[4];      // V index read by forward from dir d (own state when blocked / terminal / invalid)
     T tq[4];         // terminal forward value: 1 (goal, R = 1) or 0 (lava)
     uint32_t lavaF;  // NoDeath: bit d = forward from dir d enters (walkable, non-terminal) lava
+    uint32_t halo;   // served pair loop (serve_pair_halo): bit 0 the halo cell is walkable, bit 1 a goal ahead of it
 };
 
 template <typename T, bool ND = false>
@@ -163,6 +164,7 @@ __device__ __forceinline__ XydTopo<T> xyd_topo(const uint8_t *cl, const Geo &geo
     tp.valid = xyd_free(cl[c]) || (ND && cl[c] == T_LAVA);
     tp.term = 0;
     tp.lavaF = 0;
+    tp.halo = 0;
     // Branch-free (selects only, every LDS byte read unconditional): it runs once per grid-sweep
     // in the HBM sweep kernels.
 #pragma unroll

@@ -180,6 +180,7 @@ class ValueIteration:
         self.method, self.lava = method, lava
         self.desc = d
         self._solve_args = None
+        self._live = None  # the last solve()'s ctypes outputs while they are the current result
         self._sharded_args = None
         self._load_dev_fn = None
         h = ctypes.c_void_p()
@@ -269,9 +270,30 @@ class ValueIteration:
         rc = (self._solve_last_fn if last else self._solve_fn)(*self._solve_args)
         if rc:
             _lib.check(rc, "mgdp_vi_solve")
-        k, dv, conv = self._out
-        self.sweeps, self.dv, self.converged = k.value, dv.value, bool(conv.value)
-        return self.sweeps
+        # the result stays in the ctypes outputs (sweeps / dv / converged read them): a served solve
+        # takes a few microseconds, and converting and storing three attributes per call was a
+        # measurable part of the host's turnaround between requests
+        self._live = self._out
+        return self._out[0].value
+
+    # sweeps / dv / converged of the last result: read from solve()'s outputs while they are current
+    def _result_attr(self, i, name):
+        live = self.__dict__.get("_live")
+        if live is not None:
+            return (live[0].value, live[1].value, bool(live[2].value))[i]
+        return self.__dict__[name]
+
+    def _set_result_attr(self, name, v):
+        live = self.__dict__.get("_live")
+        if live is not None:  # leaving the live outputs: the other two keep their values
+            self.__dict__.update(_sweeps=live[0].value, _dv=live[1].value, _converged=bool(live[2].value))
+            self.__dict__["_live"] = None
+        self.__dict__[name] = v
+
+    sweeps = property(lambda self: self._result_attr(0, "_sweeps"), lambda self, v: self._set_result_attr("_sweeps", v))
+    dv = property(lambda self: self._result_attr(1, "_dv"), lambda self, v: self._set_result_attr("_dv", v))
+    converged = property(lambda self: self._result_attr(2, "_converged"),
+                         lambda self, v: self._set_result_attr("_converged", v))
 
     def solve_sharded(self, comm) -> int:
         """One sharded solve with the library's own collectives (mgdp_vi_solve_sharded on a

@@ -3,7 +3,9 @@ planes, three rotating register sets; csrc/vi_loops.h) against the CPU oracle, b
 V, pi and the last sweep's dV.  Covers grids whose wave edges allow the DPP path and grids whose
 first / last lane of a wave has a valid neighbour in the next wave (the in-kernel fallback to
 fused_fast_xyd_soa), both in one resident server through new-grid requests, and the host switch
-MGDP_SERVE_EW=0."""
+MGDP_SERVE_EW=0.  Round 6: every case also on the two-sweeps-per-barrier loop (fused_serve_pair, the
+default; MGDP_SERVE_PAIR=0 keeps fused_serve_xyd), including odd and even max_sweeps caps (a pair may
+compute past the cap) and wide grids (W up to 50: neighbours two rows away read from the pads)."""
 import numpy as np
 import pytest
 
@@ -52,14 +54,26 @@ def check(g, res, dtype):
     np.testing.assert_array_equal(pi, o["pi"])
 
 
+PAIR = pytest.mark.parametrize("pair", ["0", "1"])
+
+
+def expected_variant(W, pair):
+    return "serve_pair" if pair == "1" else "serve_ew"
+
+
+@PAIR
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
-def test_served_ew_random_grids(dtype, monkeypatch):
+def test_served_ew_random_grids(dtype, pair, monkeypatch):
     monkeypatch.setenv("MGDP_PERSISTENT", "1")
+    monkeypatch.setenv("MGDP_SERVE_PAIR", pair)
     rng = np.random.default_rng(7)
     seen_open = seen_closed = 0
-    for _ in range(24):
+    for i in range(32):
         while True:
-            W, H = int(rng.integers(5, 17)), int(rng.integers(5, 17))
+            if i % 4 == 3:  # wide grids: widths 17..50
+                W, H = int(rng.integers(17, 51)), int(rng.integers(3, 8))
+            else:
+                W, H = int(rng.integers(5, 17)), int(rng.integers(5, 17))
             if 64 < W * H <= 256:
                 break
         g = random_grid(rng, W, H)
@@ -69,16 +83,19 @@ def test_served_ew_random_grids(dtype, monkeypatch):
             seen_closed += 1
         vi = mg.ValueIteration(g[None], dtype=dtype)
         assert vi.persistent
+        assert vi.variant == expected_variant(W, pair), (W, vi.variant)
         check(g, solve_served(vi), dtype)
         check(g, solve_served(vi), dtype)  # a second request on the resident server
         vi.close()
     assert seen_open and seen_closed
 
 
-def test_served_ew_grid_changes_between_requests(monkeypatch):
+@PAIR
+def test_served_ew_grid_changes_between_requests(pair, monkeypatch):
     """One resident server, new grids handed over between requests, alternating between grids the
     DPP path takes and grids that fall back (serve_ew_ok is re-evaluated per grid)."""
     monkeypatch.setenv("MGDP_PERSISTENT", "1")
+    monkeypatch.setenv("MGDP_SERVE_PAIR", pair)
     rng = np.random.default_rng(11)
     W, H = 10, 10
     grids = []
@@ -93,14 +110,16 @@ def test_served_ew_grid_changes_between_requests(monkeypatch):
     vi.close()
 
 
-@pytest.mark.parametrize("ew", ["0", "1"])
-def test_served_empty16(ew, monkeypatch):
-    """The headline grid on either host setting: 29 sweeps, bit-exact."""
+@pytest.mark.parametrize("ew,pair", [("0", "1"), ("1", "0"), ("1", "1")])
+def test_served_empty16(ew, pair, monkeypatch):
+    """The headline grid on every host setting: 29 sweeps, bit-exact."""
     monkeypatch.setenv("MGDP_PERSISTENT", "1")
     monkeypatch.setenv("MGDP_SERVE_EW", ew)
+    monkeypatch.setenv("MGDP_SERVE_PAIR", pair)
     enc, _ = mg.make("MiniGrid-Empty-16x16-v0").generate(seed=0)
     g = np.ascontiguousarray(enc[:, :, 0].T)
     vi = mg.ValueIteration(g[None], dtype="f32")
+    assert vi.variant == ("serve_pair" if ew == "1" and pair == "1" else ("serve_ew" if ew == "1" else vi.variant))
     for _ in range(3):
         res = solve_served(vi)
         assert res[0] == 29
@@ -108,16 +127,20 @@ def test_served_empty16(ew, monkeypatch):
     vi.close()
 
 
-def test_served_ew_max_sweeps_cap(monkeypatch):
-    """Stopped by max_sweeps instead of the rule: V_k and the pi of sweep k as the oracle's."""
+@PAIR
+def test_served_ew_max_sweeps_cap(pair, monkeypatch):
+    """Stopped by max_sweeps instead of the rule: V_k and the pi of sweep k as the oracle's (every
+    cap 1..13: both halves of a pair, both loop positions' parities; and caps past the rule's K)."""
     monkeypatch.setenv("MGDP_PERSISTENT", "1")
+    monkeypatch.setenv("MGDP_SERVE_PAIR", pair)
     enc, _ = mg.make("MiniGrid-Empty-16x16-v0").generate(seed=0)
     g = np.ascontiguousarray(enc[:, :, 0].T)
-    for cap in (1, 2, 3, 5, 6, 7, 13):
+    for cap in list(range(1, 14)) + [28, 29, 30]:
         vi = mg.ValueIteration(g[None], dtype="f32", max_sweeps=cap)
         k, dv, V, pi = solve_served(vi)
         o = oracle.value_iteration(0, g[None], dtype="f32", max_sweeps=cap)
-        assert k == o["sweeps"] == cap
+        assert k == o["sweeps"] == min(cap, 29)
+        assert dv == o["dv"]
         np.testing.assert_array_equal(V, o["V"])
         np.testing.assert_array_equal(pi, o["pi"])
         vi.close()
