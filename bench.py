@@ -103,7 +103,8 @@ def shard_of(world: int) -> int:
     return n if world == 1 and n > 1 else world
 
 
-def make_cells(spec, rank, world):
+def make_cells(spec, rank, world, seed_offset=0):
+    """This rank's grids of a workload; seed_offset shifts every seed (fresh grid sets)."""
     from minigrid_dynamicprogramming_amd import make
     from minigrid_dynamicprogramming_amd.distributed import shard_range
 
@@ -122,7 +123,7 @@ def make_cells(spec, rank, world):
     # to the reference's grid digests by tests/test_gpu_gen.py); not part of the timed region
     from minigrid_dynamicprogramming_amd import gen
 
-    cells = gen.generate(env, lo, hi - lo, enc=False, cells=True, agent=False)["cells"]
+    cells = gen.generate(env, lo + seed_offset, hi - lo, enc=False, cells=True, agent=False)["cells"]
     return cells, (lo, hi)
 
 
@@ -427,8 +428,13 @@ def main():
         log(f"[rank {rank}] {name}: grids [{lo},{hi}) generated in {time.perf_counter() - t_gen:.1f}s")
         sharded = spec["sharded"] and (world > 1 or force_dist)
         wargs = argparse.Namespace(**{**vars(args), "workload": name})
+        fresh = None
+        if split_events and not spec.get("replicate") and not spec.get("distinct") and FRESH_SETS > 0:
+            # fresh grid sets for the first-solve timing: seeds shifted past the workload's own
+            n_all = spec["global_grids"] if spec["sharded"] else spec["per_gpu"] * world
+            fresh = [make_cells(spec, rank, world, seed_offset=(i + 1) * n_all)[0] for i in range(FRESH_SETS)]
         m = measure(wargs, dtype or args.dtype, cells, local, dist, red_dev, get_reducer() if sharded else None, sharded,
-                    split_events=split_events)
+                    split_events=split_events, fresh=fresh)
         return spec, cells, (lo, hi), sharded, m
 
     # the BASELINE configs 3-5 beside the default line (every rank takes part), run BEFORE the
@@ -463,6 +469,8 @@ def main():
                     blk["executed_updates_per_s"] = blk["value"] * bm["executed"]["frac_of_global_rule"]
                 if bm.get("collectives"):
                     blk["collectives"] = bm["collectives"]
+                if bm.get("fresh"):
+                    blk["fresh"] = bm["fresh"]
                 if world == 1 and not args.no_cpu:
                     model = bm["info"]["model"]
                     blk["cpu_baseline"] = cpu_baseline(bcells, model, args.gamma, args.tol, args.dtype, BLOCK_CPU_S)
@@ -591,6 +599,8 @@ def compact_line(out: dict) -> dict:
             e = b.get("executed_rank0") or {}
             v = (b.get("roofline") or {}).get("valu") or {}
             d = {"v": _g(b["value"]), "x": _g(b.get("executed_updates_per_s")), "ms": _g(b["ms_per_solve"]),
+                 "msf": _g((b.get("fresh") or {}).get("ms_per_solve")), "msa": _g((b.get("fresh") or {}).get("ms_per_solve_again")),
+                 "kf": _g((b.get("fresh") or {}).get("kernel_ratio"), 3),
                  "k": b["sweeps"], "xf": _g(e.get("frac_of_global_rule"), 3), "valu": _g(v.get("frac"), 2)}
             for key, src in (("c1", "cpu_baseline"), ("c16", "cpu_baseline_all_cores"), ("f1", "cpu_baseline_fp"),
                              ("f16", "cpu_baseline_fp_all_cores")):
@@ -600,7 +610,10 @@ def compact_line(out: dict) -> dict:
     if cfgs:
         c["configs"] = cfgs
         c["configs_keys"] = ("v updates/s as the metric counts (B*S*A*K); x executed updates/s (grid-sweeps run); "
-                             "ms per solve; k sweeps; xf executed/K; valu VALU-issue frac; c1/c16 CPU oracle, "
+                             "ms per solve; msf / msa ms of the first / second solve of fresh grids, one solve per region, kf their "
+                             "kernel-time ratio; k sweeps; "
+                             "xf executed/K; "
+                             "valu VALU-issue frac; c1/c16 CPU oracle, "
                              "literal global loop, 1/16 threads; f1/f16 same with the per-grid fixed-point stop")
     return c
 
@@ -635,7 +648,7 @@ def compulsory_bytes_per_solve(info, tsize, method, sweeps):
     return B * (compulsory_bytes_per_sweep(S, HW, tsize) * sweeps + S * tsize + HW + S)
 
 
-def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded, split_events=False):
+def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded, split_events=False, fresh=None):
     """W warmup solves, then K timed solves (barrier + synchronize on both sides, max over ranks).
     split_events (the BASELINE-config blocks beside the headline): the timed region runs without the
     library's per-launch HIP events -- on a batched solve they cost 6-9 us of host time per launch
@@ -785,6 +798,45 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded, split_ev
     clock = vi.serve_clock() if vi.persistent else None
     gsw = vi.grid_sweeps() if vi.B > 1 else None  # sweeps each grid executed in the last solve
     vi.enable_timing(False)
+    fresh_out = None
+    if fresh:
+        # First solves of FRESH grids (round 6): a new grid set is loaded -- uploaded,
+        # its dispatch order computed from the cells -- outside the timing, then ONE solve is timed like
+        # a region of one step (the solve and the closing synchronize), on every rank at once; the max
+        # over ranks of each, then the median over the sets.  The repeated region above solves the same
+        # grids K times; this says what a user solving new grids every time gets.
+        def one_timed():
+            barrier()
+            torch.cuda.synchronize()
+            vi.enable_timing(True)
+            t = time.perf_counter()
+            k_f = one_solve()
+            vi.synchronize()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t
+            kms, _ = vi.kernel_time()
+            vi.enable_timing(False)
+            if dist is not None:
+                tt = torch.tensor([dt, kms], dtype=torch.float64, device=red_dev)
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                dt, kms = float(tt[0].item()), float(tt[1].item())
+            return dt, kms, k_f
+
+        first, again = [], []
+        for fc in fresh:
+            vi.load(fc)
+            first.append(one_timed())  # the first solve of these grids
+            again.append(one_timed())  # the same grids once more, timed the same way (one solve + its edge)
+        med = lambda xs, i: round(float(np.median([x[i] for x in xs])) * (1e3 if i == 0 else 1.0), 5)
+        fresh_out = {"ms_per_solve": med(first, 0), "ms_per_solve_again": med(again, 0),
+                     "kernel_ms": med(first, 1), "kernel_ms_again": med(again, 1),
+                     "ratio": round(med(first, 0) / med(again, 0), 4),
+                     "kernel_ratio": round(med(first, 1) / med(again, 1), 4), "sets": len(first),
+                     "ms_each": [round(x[0] * 1e3, 5) for x in first], "sweeps": [x[2] for x in first],
+                     "rule": "per set: load (upload + dispatch order from the cells, untimed), then ONE timed solve "
+                             "+ the closing synchronize (a region of one step, so its edge is not amortized as in "
+                             "the K-step region; per-launch events on), then the same grids once more, timed the "
+                             "same way; max over ranks, median over sets.  kernel_ms: the launches' event time"}
     info = {"A": 7 if vi.model == "xyd" else 5, "W": vi.W, "H": vi.H, "S": vi.S, "B": vi.B, "model": vi.model,
             "updates_per_sweep": vi.updates_per_sweep, "kernel": vi.kernel_name, "persistent": vi.persistent}
     vi.close()
@@ -851,7 +903,7 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded, split_ev
             "events_in_region": not split,
             "executed": executed,
             "launches": launches, "primed": primed, "timed_primed": PRIME_RELAUNCH if info["persistent"] else 0,
-            "info": info, "collectives": collectives, "latency": lat}
+            "info": info, "collectives": collectives, "latency": lat, "fresh": fresh_out}
 
 
 def host_cores() -> int:
@@ -1123,6 +1175,8 @@ def gen_cpu_baseline(env, budget_s):
 
 
 BLOCK_CPU_S = 2.0  # seconds of oracle sampling per BASELINE-config block (1 thread, then all cores)
+FRESH_SETS = 3  # fresh grid sets per BASELINE-config block: first-solve timing (MGDP_BENCH_FRESH overrides)
+FRESH_SETS = int(os.environ.get("MGDP_BENCH_FRESH", FRESH_SETS))
 # steady-state priming of a resident lone-grid server (measure(): the stated criterion)
 PRIME_MIN_S, PRIME_WIN, PRIME_TOL, PRIME_MAX_S, PRIME_RELAUNCH = 0.2, 512, 0.02, 1.0, 16
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9  # MI355X_MICROARCH.md: 4 SIMD-32 per CU, one wave64 VALU op per 2 cycles

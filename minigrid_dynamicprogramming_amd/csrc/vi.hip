@@ -74,6 +74,7 @@ struct mgdp_vi {
     // measured (profiles/r05_ab2/): the order alone +3-6 % (LavaS11N5 x 8192 / x 65536, FourRooms x
     // 4096, DoorKey-16 x 65536); the priority on top of it nothing or worse -- off by default
     bool learn_order = true, learn_prio = false;
+    int order_src = 1;  // dispatch order key: 1 the cells' depth proxy (at load), 2 the last solve's sweeps, 0 none (MGDP_ORDER)
     double *d_dvenv = nullptr;
     unsigned long long *d_shards = nullptr;
     unsigned long long *d_red = nullptr;    // fused reduction shards [64][4]
@@ -1165,6 +1166,7 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     if (const char *ev = std::getenv("MGDP_CHAIN")) vi->chain = std::atoi(ev) != 0;
     if (const char *ev = std::getenv("MGDP_LEARN_ORDER")) vi->learn_order = std::atoi(ev) != 0;
     if (const char *ev = std::getenv("MGDP_LEARN_PRIO")) vi->learn_prio = std::atoi(ev) != 0;
+    if (const char *ev = std::getenv("MGDP_ORDER")) vi->order_src = std::strcmp(ev, "learned") == 0 ? 2 : (std::strcmp(ev, "off") == 0 ? 0 : 1);
     if (const char *ev = std::getenv("MGDP_REDUCE_MULTI")) vi->reduce_multi = std::atoi(ev) != 0;
     if (const char *ev = std::getenv("MGDP_INKERNEL_MAX")) vi->inkernel_max = std::max(0, std::atoi(ev));
     // DoorKey (64-128 B of V per thread) measured slower on the register pipeline (5.38 -> 3.3 TB/s
@@ -1239,6 +1241,10 @@ int mgdp_vi_set_stream(mgdp_vi *vi, void *s) {
     return 0;
 }
 
+namespace {
+int cells_dispatch(mgdp_vi *vi);  // the dispatch order from the cells just loaded (below)
+}  // namespace
+
 int mgdp_vi_load_cells(mgdp_vi *vi, const uint8_t *cells) {
     MGDP_CHECK(vi && cells, MGDP_E_INVALID, "null argument");
     if (int rc = validate_cells(vi->d, cells)) return rc;
@@ -1262,7 +1268,7 @@ int mgdp_vi_load_cells(mgdp_vi *vi, const uint8_t *cells) {
     vi->k_done_valid = false;
     vi->order_valid = false;
     vi->solves_since_load = 0;
-    return 0;
+    return cells_dispatch(vi);
 }
 
 int mgdp_vi_load_cells_device(mgdp_vi *vi, const uint8_t *d_cells) {
@@ -1283,21 +1289,21 @@ int mgdp_vi_load_cells_device(mgdp_vi *vi, const uint8_t *d_cells) {
     vi->k_done_valid = false;
     vi->order_valid = false;
     vi->solves_since_load = 0;
-    return 0;
+    return cells_dispatch(vi);
 }
 
 namespace {
-// Learned dispatch order (Geo::order / kprio): once the handle's cells have been solved, the sweeps
-// each grid executed (d_kexec) rank the grids -- longest first in dispatch order (an LPT schedule:
-// the launch's tail holds short grids, and at full residency every CU gets a stratified mix), and
-// the top 1 / 10 / 50 % raise their waves' issue priority.  Once per cells load (a D2H copy of B
-// words and a sort); V, pi and the sweep counts do not depend on it.
+// Dispatch order (Geo::order / kprio): the grids ranked longest first in dispatch order (an LPT
+// schedule: the launch's tail holds short grids, and at full residency every CU gets a stratified
+// mix), and optionally (learn_prio) the top 1 / 10 / 50 % raise their waves' issue priority.  The
+// key per grid is (order_src) 1 = its cells' depth proxy (vi_depth_kernel, computed at each cells
+// load: the order holds from the first solve of fresh grids), 2 = the sweeps it executed in the
+// previous solve (d_kexec; round 5's learned order, from the second solve on).  V, pi and the sweep
+// counts never depend on it.
 constexpr int kLearnMinB = 1024;
-int learn_dispatch(mgdp_vi *vi) {
+int set_order(mgdp_vi *vi, const std::vector<int32_t> &kx) {
     const int B = vi->d.B;
-    std::vector<int32_t> kx(B), idx(B);
-    MGDP_HIP(hipMemcpyAsync(kx.data(), vi->d_kexec, sizeof(int32_t) * (size_t)B, hipMemcpyDeviceToHost, vi->stream));
-    MGDP_HIP(hipStreamSynchronize(vi->stream));
+    std::vector<int32_t> idx(B);
     for (int i = 0; i < B; ++i) idx[i] = i;
     std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return kx[a] > kx[b]; });
     if (!vi->d_order) MGDP_HIP(hipMalloc((void **)&vi->d_order, sizeof(int32_t) * (size_t)B));
@@ -1311,7 +1317,7 @@ int learn_dispatch(mgdp_vi *vi) {
     } else {
         vi->kprio[0] = vi->kprio[1] = vi->kprio[2] = 0;  // no spread to exploit
     }
-    // mixed wave counts: the grids that ran >= mix_frac x the longest sweep on two waves (they are the
+    // mixed wave counts: the grids with keys >= mix_frac x the largest on two waves (they are the
     // first workgroups of the order just set)
     vi->nmix = 0;
     if (vi->mix && kx[idx[0]] > 0) {
@@ -1321,13 +1327,38 @@ int learn_dispatch(mgdp_vi *vi) {
     vi->order_valid = true;
     return 0;
 }
+bool order_eligible(const mgdp_vi *vi) {
+    return vi->order_src != 0 && (vi->learn_order || vi->learn_prio) && vi->d.B >= kLearnMinB &&
+           vi->d.method == MGDP_METHOD_FUSED && !vi->opts && !serve_eligible(vi);
+}
+// order_src 2: from the executed sweeps of the previous solve
+int learn_dispatch(mgdp_vi *vi) {
+    std::vector<int32_t> kx(vi->d.B);
+    MGDP_HIP(hipMemcpyAsync(kx.data(), vi->d_kexec, sizeof(int32_t) * (size_t)vi->d.B, hipMemcpyDeviceToHost, vi->stream));
+    MGDP_HIP(hipStreamSynchronize(vi->stream));
+    return set_order(vi, kx);
+}
+// order_src 1: from the cells just loaded (one small launch, a D2H copy of B words and a sort)
+int cells_dispatch(mgdp_vi *vi) {
+    if (!order_eligible(vi) || vi->order_src != 1 || vi->HW > kDepthMaxHW) return 0;
+    int32_t *d_depth = nullptr;
+    MGDP_HIP(hipMallocAsync((void **)&d_depth, sizeof(int32_t) * (size_t)vi->d.B, vi->stream));
+    hipLaunchKernelGGL(vi_depth_kernel, dim3(vi->d.B), dim3(64), 0, vi->stream, make_geo(vi),
+                       (const uint8_t *)vi->d_cells, (int)vi->d.model, d_depth);
+    hipError_t e = hipGetLastError();
+    std::vector<int32_t> kx(vi->d.B);
+    if (e == hipSuccess) e = hipMemcpyAsync(kx.data(), d_depth, sizeof(int32_t) * (size_t)vi->d.B, hipMemcpyDeviceToHost, vi->stream);
+    if (e == hipSuccess) e = hipFreeAsync(d_depth, vi->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(vi->stream);
+    if (e != hipSuccess) return hip_fail(e, "dispatch order from the cells", __FILE__, __LINE__);
+    return set_order(vi, kx);
+}
 }  // namespace
 
 int mgdp_vi_reset(mgdp_vi *vi) {
     MGDP_CHECK(vi, MGDP_E_INVALID, "null handle");
     DeviceGuard guard(vi->d.device);
-    if (!vi->order_valid && vi->solves_since_load > 0 && (vi->learn_order || vi->learn_prio) && vi->d.B >= kLearnMinB &&
-        vi->d.method == MGDP_METHOD_FUSED && !vi->opts && !serve_eligible(vi)) {
+    if (!vi->order_valid && vi->order_src == 2 && vi->solves_since_load > 0 && order_eligible(vi)) {
         if (int rc = server_stop(vi)) return rc;
         if (int rc = learn_dispatch(vi)) return rc;
     }

@@ -749,6 +749,60 @@ vi_fused_opts_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *
                      (int)threadIdx.x);
 }
 
+// Dispatch order from the cells (round 6): a proxy for the sweep at which each grid's own rule stops,
+// computed once per cells load, so the longest grids start first from a handle's FIRST solve on.
+// For a deterministic grid that stop is the longest shortest path to the goal (plus one sweep), so the
+// proxy is a breadth-first depth over cells (moves only, no turns): XYD, the farthest walkable cell
+// from a goal; DoorKey, the larger of that (doors and keys passable) and the farthest cell of the
+// key's side (door shut) from the key plus the key's distance to the goal (fetch the key, then the
+// goal).  Spearman rank correlation with the own-rule stopping sweep over reference-generated grids
+// (orc_vi_fp): FourRooms 0.985, LavaS11N5 0.873, DoorKey-16 0.994.  Results never
+// depend on it.  One 64-lane workgroup per grid, level-synchronous BFS in LDS (a lane's LDS accesses
+// are ordered and a cell at level L+1 is only set next to one at level L, so no barrier is needed).
+constexpr int kDepthMaxHW = 1024;
+__device__ __forceinline__ int depth_bfs(const uint8_t *cl, uint16_t *dist, int HW, int W, int src_type,
+                                         bool dk_open) {
+    const int lane = threadIdx.x;
+    constexpr uint16_t kUnseen = 0xffff;
+    auto passable = [&](int t) { return dk_open ? (xyd_free(t) || t == T_DOOR || t == T_KEY) : xyd_free(t); };
+    for (int c = lane; c < HW; c += 64) dist[c] = cl[c] == src_type ? 0 : kUnseen;
+    int level = 0, maxd = 0;
+    while (true) {
+        bool grew = false;
+        for (int c = lane; c < HW; c += 64) {
+            if (dist[c] != kUnseen || !passable(cl[c])) continue;
+            const bool nb = (c >= W && dist[c - W] == level) || (c + W < HW && dist[c + W] == level) ||
+                            (c % W != 0 && dist[c - 1] == level) || (c % W != W - 1 && dist[c + 1] == level);
+            if (nb) {
+                dist[c] = (uint16_t)(level + 1);
+                grew = true;
+            }
+        }
+        if (__ballot(grew) == 0ull) break;
+        maxd = ++level;
+    }
+    return maxd;
+}
+__global__ void __launch_bounds__(64) vi_depth_kernel(Geo geo, const uint8_t *__restrict__ cells, int model,
+                                                      int32_t *__restrict__ depth) {
+    __shared__ uint8_t cl[kDepthMaxHW];
+    __shared__ uint16_t d1[kDepthMaxHW], d2[kDepthMaxHW];
+    const int b = blockIdx.x, HW = geo.HW, W = geo.W;
+    for (int c = threadIdx.x; c < HW; c += 64) cl[c] = cells[(long long)b * geo.HWp + c];
+    int proxy = depth_bfs(cl, d1, HW, W, T_GOAL, model == MGDP_MODEL_DOORKEY);
+    if (model == MGDP_MODEL_DOORKEY) {
+        // the key's distance to the goal (doors and keys passable: d1), then the key side's depth
+        int kd = 0x7fffffff;
+        for (int c = threadIdx.x; c < HW; c += 64)
+            if (cl[c] == T_KEY && d1[c] != 0xffff) kd = min(kd, (int)d1[c]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) kd = min(kd, __shfl_xor(kd, o));
+        const int side = depth_bfs(cl, d2, HW, W, T_KEY, false);
+        if (kd != 0x7fffffff) proxy = max(proxy, side + kd);
+    }
+    if (threadIdx.x == 0) depth[b] = proxy;
+}
+
 // The sharded protocol's gate (mgdp_vi_run_to_dev_sync): kdv = the all-reduced {K, E}, written by
 // the collective ordered before this launch.  E == 0: every grid everywhere is at an exact fixed
 // point, so the result is {K, dV 0, K}; else kmin = kGateMore asks the host for run_to(K).

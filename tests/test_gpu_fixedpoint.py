@@ -197,12 +197,15 @@ def test_capacity_batches_next_to_a_resident_server(delta):
 
 @pytest.mark.parametrize("env_id,B", [("MiniGrid-LavaCrossingS11N5-v0", 4096), ("MiniGrid-FourRooms-v0", 2048),
                                       ("MiniGrid-DoorKey-16x16-v0", 1024)])
-@pytest.mark.parametrize("learn", [{}, {"MGDP_LEARN_PRIO": "1"}, {"MGDP_LEARN_ORDER": "0", "MGDP_LEARN_PRIO": "1"}])
+@pytest.mark.parametrize("learn", [{}, {"MGDP_LEARN_PRIO": "1"}, {"MGDP_ORDER": "learned"},
+                                   {"MGDP_ORDER": "learned", "MGDP_LEARN_PRIO": "1"}, {"MGDP_ORDER": "off"},
+                                   {"MGDP_LEARN_ORDER": "0", "MGDP_LEARN_PRIO": "1"}])
 def test_learned_dispatch_order_is_exact(env_id, B, learn):
-    """From the second solve of the same cells on, workgroups take the grids longest-first (the
-    previous solve's executed sweeps), optionally the longest raise their issue priority
-    (MGDP_LEARN_PRIO=1): every solve, and a
-    solve after new cells (order dropped), equals the oracle's global loop; executed sweeps too."""
+    """Workgroups take the grids longest-first: by default from the first solve on, ranked by the
+    cells' breadth-first depth proxy computed at each load (vi_depth_kernel); with MGDP_ORDER=learned
+    from the second solve on, ranked by the previous solve's executed sweeps; optionally the longest
+    raise their issue priority (MGDP_LEARN_PRIO=1).  Every solve, and the solves after new cells
+    (a new order), equal the oracle's global loop; executed sweeps too."""
     cells = gen.generate(env_id, 0, B, enc=False, cells=True, agent=False)["cells"]
     model = 1 if "DoorKey" in env_id else 0
     o = oracle.value_iteration(model, cells, dtype="f32", nthreads=16, fixed_point=True)
@@ -214,11 +217,12 @@ def test_learned_dispatch_order_is_exact(env_id, B, learn):
             np.testing.assert_array_equal(vi.policy(), o["pi"])
             np.testing.assert_array_equal(vi.grid_sweeps(), o["grid_sweeps"])
         other = cells[::-1].copy()
-        o2 = oracle.value_iteration(model, other, dtype="f32", nthreads=16)
+        o2 = oracle.value_iteration(model, other, dtype="f32", nthreads=16, fixed_point=True)
         vi.load(other)
         for _ in range(2):
             assert vi.solve() == o2["sweeps"]
             np.testing.assert_array_equal(vi.values(), o2["V"])
             np.testing.assert_array_equal(vi.policy(), o2["pi"])
+            np.testing.assert_array_equal(vi.grid_sweeps(), o2["grid_sweeps"])
     finally:
         vi.close()
