@@ -609,12 +609,10 @@ def compact_line(out: dict) -> dict:
             cfgs[name] = {k: x for k, x in d.items() if x is not None}
     if cfgs:
         c["configs"] = cfgs
-        c["configs_keys"] = ("v updates/s as the metric counts (B*S*A*K); x executed updates/s (grid-sweeps run); "
-                             "ms per solve; msf / msa ms of the first / second solve of fresh grids, one solve per region, kf their "
-                             "kernel-time ratio; k sweeps; "
-                             "xf executed/K; "
-                             "valu VALU-issue frac; c1/c16 CPU oracle, "
-                             "literal global loop, 1/16 threads; f1/f16 same with the per-grid fixed-point stop")
+        c["configs_keys"] = ("v upd/s as the metric counts (B*S*A*K); x executed upd/s; ms per solve; msf/msa ms of "
+                             "the 1st/2nd solve of fresh grids (1-solve regions), kf their kernel ratio; k sweeps; "
+                             "xf executed/K; valu VALU frac; c1/c16 CPU oracle 1/16 threads; f1/f16 same, per-grid "
+                             "fixed-point stop")
     return c
 
 
