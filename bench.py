@@ -743,6 +743,11 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded, split_ev
             one_solve()
             primed += 1
             pstamps.append(time.perf_counter())
+    if split and not sharded:
+        # a resident batch server (vi_bserve_kernel, round 6) left at the timing switch and the device
+        # synchronize above: one more untimed solve relaunches it right before the region (as the lone
+        # server's relaunch priming does), so the region times served solves, not a relaunch per K
+        one_solve()
     stamps = [] if os.environ.get("MGDP_BENCH_STAMPS") else None  # diagnostics: where the region's time goes
     # the plain case calls the bound solve() directly (no wrapper, no per-step argument): a served
     # lone grid answers in a few microseconds and the loop's own Python is part of each step's host turnaround

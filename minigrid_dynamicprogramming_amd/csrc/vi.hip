@@ -163,6 +163,14 @@ struct mgdp_vi {
     bool gk = false;
     int gk_capacity = 0;          // resident workgroups of the wave2 kernel on this device (MGDP_GK=2)
     unsigned long long *d_gk = nullptr;
+    // the resident batch server (vi_bserve_kernel): one-wave batches within its resident capacity,
+    // solves with launch timing off (MGDP_BSERVE=0: off)
+    bool bserve = true;
+    int bserve_cap = 0;                  // resident workgroups of vi_bserve_kernel on this device
+    int bserve_copies = kBreqCopies;     // request lines the workgroups poll (MGDP_BSERVE_COPIES)
+    int bserve_nap = 1;                  // s_sleep(10)s between polls (MGDP_BSERVE_NAP)
+    int bserve_wait_pub = 1;             // the forwarder polls the host only after the publication (MGDP_BSERVE_WAIT_PUB)
+    unsigned long long *d_breq = nullptr;  // its device words (kBreqWords): forwarded request, exit counter
 };
 
 namespace {
@@ -489,8 +497,54 @@ int launch_fused_t(mgdp_vi *vi, int k_target, unsigned long long *pub = nullptr,
 
 void account_server_clock(mgdp_vi *vi);
 
+// The batch server's instantiation for P cells per lane (the wave2 kernel's P); nullptr if out of range.
+template <typename T>
+const void *pick_bserve(int P) {
+    switch (P) {
+    case 1: return (const void *)vi_bserve_kernel<T, 1>;
+    case 2: return (const void *)vi_bserve_kernel<T, 2>;
+    case 3: return (const void *)vi_bserve_kernel<T, 3>;
+    case 4: return (const void *)vi_bserve_kernel<T, 4>;
+    case 5: return (const void *)vi_bserve_kernel<T, 5>;
+    case 6: return (const void *)vi_bserve_kernel<T, 6>;
+    case 7: return (const void *)vi_bserve_kernel<T, 7>;
+    case 8: return (const void *)vi_bserve_kernel<T, 8>;
+    default: return nullptr;
+    }
+}
+template <typename T, int P>
+int launch_bserve_p(mgdp_vi *vi, unsigned int served, TimedPair tp) {
+    const int smem = wave2_smem_bytes(vi->HWp, vi->d.W, P, (int)sizeof(T));
+    hipExtLaunchKernelGGL(vi_bserve_kernel<T, P>, dim3(vi->d.B), dim3(64), smem, vi->stream, tp.a, tp.b, 0, make_geo(vi),
+                          make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv, vi->d_dvenv, vi->d_hout,
+                          vi->d_hout + kHoutReq, vi->d_breq, vi->d_gk, (unsigned long long)served, vi->serve_idle_ticks,
+                          vi->serve_life_ticks, vi->serve_tag, vi->bserve_copies, vi->bserve_nap, vi->bserve_wait_pub);
+    MGDP_HIP(hipGetLastError());
+    return 0;
+}
+
 template <typename T, int MODEL, bool SLIP, int MAP>
 int launch_serve_t(mgdp_vi *vi, unsigned int served) {
+    if (vi->d.B > 1) {  // the resident batch server (bserve_eligible: deterministic XYD, one wave per grid)
+        if constexpr (MODEL == MGDP_MODEL_XYD && !SLIP && MAP == MGDP_MAP_CELL) {
+            TimedPair tp;
+            if (int rc = timed_begin(vi, -1, &tp)) return rc;
+            account_server_clock(vi);
+            ++vi->serve_tag;
+            switch (vi->wave2) {
+            case 1: return launch_bserve_p<T, 1>(vi, served, tp);
+            case 2: return launch_bserve_p<T, 2>(vi, served, tp);
+            case 3: return launch_bserve_p<T, 3>(vi, served, tp);
+            case 4: return launch_bserve_p<T, 4>(vi, served, tp);
+            case 5: return launch_bserve_p<T, 5>(vi, served, tp);
+            case 6: return launch_bserve_p<T, 6>(vi, served, tp);
+            case 7: return launch_bserve_p<T, 7>(vi, served, tp);
+            case 8: return launch_bserve_p<T, 8>(vi, served, tp);
+            default: break;
+            }
+        }
+        MGDP_CHECK(false, MGDP_E_INVALID, "batch server: not a one-wave deterministic XYD batch");
+    }
     const Geo g = make_geo(vi);
     const Smem L = smem_layout(vi->Ss, vi->HWp, sizeof(T), vi->nbuf);
     auto kern = pick_wave<ServeK, T, MODEL, SLIP, MAP>(vi);
@@ -538,11 +592,15 @@ int launch_sweep_pipe(mgdp_vi *vi, const T *Vin, T *Vout, int k, int check_prev,
     const int smem = sweep_pipe_smem_bytes(vi->S, vi->HW, vi->HWs, vi->HWp, sizeof(T));
     auto kern = vi_sweep_pipe_kernel<T, MODEL, SLIP, DEPTH>;
     if (smem > 64 * 1024) MGDP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
-    if (vi->pipe_grid == 0) {  // every workgroup resident at once: grid = resident blocks per CU x CUs
+    if (vi->pipe_grid == 0) {  // resident workgroups, at most 4 per CU
+        // Empty-16 x 65536 (profiles/r06_sweep2/): 8 per CU (every resident slot, 2048 workgroups)
+        // 98.5 us per sweep, 6 per CU 100.1, 5 94.4, 4 90.3-90.8 (6.10-6.13 TB/s compulsory), 3 92.5,
+        // 2 109.3: four 256-thread workgroups, each with two grids' loads in flight, keep enough bytes
+        // moving, and fewer co-resident workgroups contend less for the channels.
         int per_cu = 0, cus = 0;
         MGDP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)kern, vi->HWs, smem));
         MGDP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, vi->d.device));
-        vi->pipe_grid = std::max(1, per_cu) * std::max(1, cus);
+        vi->pipe_grid = std::min(4, std::max(1, per_cu)) * std::max(1, cus);
         if (const char *ev = std::getenv("MGDP_SWEEP_GRID")) vi->pipe_grid = std::max(1, std::atoi(ev));
     }
     const int grid = std::min(vi->d.B, vi->pipe_grid);
@@ -614,7 +672,8 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
     // that left before it saw the request.
     const volatile unsigned long long *h = vi->h_out;
     const unsigned long long ep = (unsigned long long)vi->epoch;
-    const bool tagged = vi->serving;
+    const bool served = vi->serving;                 // a resident server answers (a relaunch may be needed)
+    const bool tagged = served && vi->d.B == 1;      // ... in the lone server's words [5..7]
     auto ready = [&]() -> bool {
         if (!tagged) return (h[0] >> 32) == ep && (h[1] >> 32) == ep && (h[2] >> 32) == ep && (h[3] >> 32) == ep;
         return (h[5] >> 32) == ep && (h[6] >> 32) == ep && (h[7] >> 32) == ep;
@@ -637,7 +696,7 @@ int reduce_env(mgdp_vi *vi, int32_t *kmax, double *dvmax) {
             const hipError_t q = hipStreamQuery(vi->stream);
             if (q == hipSuccess) {
                 if (ready()) break;
-                if (tagged && relaunches < 4) {
+                if (served && relaunches < 4) {
                     ++relaunches;
                     DeviceGuard guard(vi->d.device);  // the served fast path of mgdp_vi_solve holds none
                     if (int rc = dispatch<ServeF>(vi, vi->epoch - 1u)) return rc;
@@ -690,6 +749,15 @@ bool serve_eligible(const mgdp_vi *vi) {
     return vi->persistent && !vi->opts && vi->d.method == MGDP_METHOD_FUSED && vi->d.B == 1 && vi->d.mapping == MGDP_MAP_CELL &&
            (vi->HW <= vi->cpt * vi->fused_block || vi->wave_p || vi->band) && !vi->pair && !vi->quad;
 }
+// The resident batch server (vi_bserve_kernel): a deterministic XYD batch on one wave per grid
+// (the wave2 kernel with its in-launch reduction) that fits the server's resident capacity, solved
+// with launch timing off (a timed solve is a launch, so kernel_time() keeps timing one solve per
+// launch), from V_0 = 0 under the own rule with at least one sweep.
+bool bserve_eligible(const mgdp_vi *vi) {
+    return vi->persistent && vi->bserve && vi->d_breq && !vi->timing && vi->d.B > 1 && vi->d.B <= vi->bserve_cap &&
+           !vi->opts && vi->d.method == MGDP_METHOD_FUSED && vi->d.horizon == 0 && vi->d.max_sweeps >= 1;
+}
+bool served_eligible(const mgdp_vi *vi) { return serve_eligible(vi) || bserve_eligible(vi); }
 // Ask a resident server to leave and drain the stream.  Every entry point that enqueues other
 // work on the stream, or reads results, calls this first.  A grid handed over for the next request
 // but not yet served goes to d_cells here, so every other launch sees it.
@@ -748,7 +816,7 @@ int server_stop(mgdp_vi *vi, bool drain = true) {
 // Post the next request word: epoch, plus kServeNewCells and the tagged source word when a new
 // grid is pending (source first, then the request, both release stores: x86 keeps them in order).
 void post_request(mgdp_vi *vi) {
-    ++vi->epoch;
+    if (++vi->epoch == 0u) ++vi->epoch;  // never 0: a batch server publishes tagged with it (publish())
     unsigned long long w = (unsigned long long)vi->epoch;
     if (vi->last_req) w |= kServeLast;
     if (vi->pending_src) {
@@ -1036,6 +1104,17 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k2, vi->fused_block, smem2) == hipSuccess)
                 vi->gk_capacity = per_cu * cus;
             vi->gk = gk_on == 1 || (gk_on == 2 && d.B <= vi->gk_capacity);
+            // the resident batch server runs the same loop (wave2 layout, in-launch reduction)
+            if (const char *ev = std::getenv("MGDP_BSERVE")) vi->bserve = std::atoi(ev) != 0;
+            if (const char *ev = std::getenv("MGDP_BSERVE_COPIES")) vi->bserve_copies = std::min(kBreqCopies, std::max(1, std::atoi(ev)));
+            if (const char *ev = std::getenv("MGDP_BSERVE_NAP")) vi->bserve_nap = std::min(64, std::max(0, std::atoi(ev)));
+            if (const char *ev = std::getenv("MGDP_BSERVE_WAIT_PUB")) vi->bserve_wait_pub = std::atoi(ev) != 0;
+            if (vi->bserve && vi->gk && !vi->band && !vi->mix && !vi->wave2n && d.slip_p < 0.0 && d.B > 1) {
+                const void *kb = f32 ? pick_bserve<float>(vi->wave2) : pick_bserve<double>(vi->wave2);
+                int per_cu = 0;
+                if (kb && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kb, 64, smem2) == hipSuccess)
+                    vi->bserve_cap = per_cu * cus;
+            }
         }
         // The served lone deterministic XYD grid: east / west fronts by DPP, <= 4 waves (one dword
         // of stop flags); the two-plane padded tiles must fit the usual V buffers.
@@ -1132,6 +1211,10 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
         al((void **)&vi->d_gk, sizeof(unsigned long long) * gk_words(d.B));
         if (e == hipSuccess) e = hipMemset(vi->d_gk, 0, sizeof(unsigned long long) * gk_words(d.B));
     }
+    if (vi->bserve && vi->bserve_cap > 0 && d.B <= vi->bserve_cap) {
+        al((void **)&vi->d_breq, sizeof(unsigned long long) * kBreqWords);
+        if (e == hipSuccess) e = hipMemset(vi->d_breq, 0, sizeof(unsigned long long) * kBreqWords);
+    }
     if (d.horizon > 0) {
         al(&vi->d_rgoal, (size_t)d.horizon * vi->tsize);
         if (d.flags & MGDP_KEEP_POLICY_T) al((void **)&vi->d_pi_t, (size_t)d.horizon * BS);
@@ -1217,6 +1300,7 @@ int mgdp_vi_destroy(mgdp_vi *vi) {
     (void)hipFree(vi->d_red);
     (void)hipFree(vi->d_pub1);
     (void)hipFree(vi->d_gk);
+    (void)hipFree(vi->d_breq);
     (void)hipFree(vi->d_rgoal);
     (void)hipFree(vi->d_pi_t);
     if (vi->h_out) (void)hipHostFree(vi->h_out);
@@ -1382,7 +1466,7 @@ int mgdp_vi_run_local(mgdp_vi *vi, int32_t *k_local_max) {
     MGDP_CHECK(vi->cells_loaded, MGDP_E_INVALID, "no cells loaded");
     DeviceGuard guard(vi->d.device);
     if (vi->d.method == MGDP_METHOD_FUSED) {
-        const bool serve = serve_eligible(vi) && vi->fresh;
+        const bool serve = served_eligible(vi) && vi->fresh;
         if (serve) {
             if (int rc = serve_request(vi)) return rc;
         } else {
@@ -1563,7 +1647,9 @@ int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *con
     // Resident lone-grid server: a solve is a request word and a wait on host memory, so the
     // steady state makes no HIP call at all (no device guard either); anything else -- a server
     // that may be leaving, a rounding-level fallback sweep -- takes the general path below.
-    if (vi->serving && serve_eligible(vi) && vi->d.horizon == 0) {
+    // (a batch whose learned dispatch order is due takes the general path: mgdp_vi_reset learns it)
+    const bool learn_due = vi->d.B > 1 && !vi->order_valid && vi->order_src == 2 && vi->solves_since_load > 0;
+    if (vi->serving && served_eligible(vi) && vi->d.horizon == 0 && !learn_due) {
         const double idle_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - vi->serve_last).count();
         if (idle_us * 100.0 <= 0.5 * (double)vi->serve_idle_ticks) {
             vi->cur = 0;
@@ -1575,7 +1661,10 @@ int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *con
             if (int rc = reduce_env(vi, &k, nullptr)) return rc;
             vi->serve_last = std::chrono::steady_clock::now();
             const double dv = vi->dv_red;
-            if (dv < vi->d.tol || k >= vi->d.max_sweeps) {
+            // a batch is complete at K when every grid ended there or at an exact fixed point (mgdp_vi_run_to)
+            const bool at_k = vi->d.B == 1 || vi->k_min == k || (vi->dv_red == 0.0 && vi->k_min > 0);
+            if (vi->d.B > 1) ++vi->solves_since_load;
+            if (at_k && (dv < vi->d.tol || k >= vi->d.max_sweeps)) {
                 vi->k_done = k;
                 vi->sweeps = k;
                 vi->converged = dv < vi->d.tol;

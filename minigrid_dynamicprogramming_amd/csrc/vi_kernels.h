@@ -674,6 +674,181 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
     }
 }
 
+// Persistent server for a resident batch (round 6): the resident one-wave batch (fused_wave2_xyd,
+// B <= the kernel's resident capacity, deterministic XYD grids) stays on the device between
+// solves, so a solve costs a request word instead of a launch, a dispatch of B workgroups, their
+// cells copy and the end-of-kernel release.  Every request is a full solve from
+// V_0 = 0 with the in-launch reduction (GkCtx) publishing {kmax, dV, kmin} tagged with the request
+// exactly as a launch does; nothing is carried from one request to the next but the grids' cells
+// in LDS.  Lane 0 of workgroup 0 (the forwarder) polls the host's request word (LDS-DMA mailbox,
+// as vi_serve_kernel) and forwards it to `copies` device words, one per 128-B line (tag of this launch in bits
+// 32..47, the request's epoch in the low 32 bits, kServeLast kept, kBreqQuit to leave); every
+// other wave polls that word at agent scope with s_sleep between polls and at priority 0 (the
+// waves still sweeping get the issue slots).  Only the forwarder decides to leave (quit word,
+// idle or life limit); the others leave on its quit word, or after the life limit plus a grace
+// period, so every wave reaches the exit.  The last wave out (the exit counter) writes the exit
+// word, as a lone server does.
+constexpr unsigned long long kBreqQuit = 1ull << 63;
+constexpr int kBreqCopies = 64;                                       // request lines (workgroup w polls w % copies)
+constexpr int kBreqExit = kBreqCopies * 16;                           // the exit counter's word (its own line)
+constexpr int kBreqWords = kBreqExit + 16;
+constexpr unsigned long long kBserveGraceTicks = 100000000ull;        // 1 s at 100 MHz
+__device__ __forceinline__ unsigned long long rfl64(unsigned long long x) {
+    const unsigned int lo = __builtin_amdgcn_readfirstlane((unsigned int)x);
+    const unsigned int hi = __builtin_amdgcn_readfirstlane((unsigned int)(x >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
+// Waves per SIMD the server is compiled for: those of the fused kernel's wave2 instantiation of the
+// same P (its resident capacity; fp32 P = 3: 5 instead of 7, which spilled).  Inside the request loop
+// the compiler spent 25-60 % more VGPRs on the same sweep loop (fp32 P = 6: 173 vs 115 -- half the
+// grids resident); with the lane index opaque per request (fused_wave2_xyd OPQ) and this bound,
+// every instantiation fits without scratch.
+template <typename T>
+__host__ __device__ constexpr int bserve_min_waves(int P) {
+    return sizeof(T) == 4 ? (P <= 2 ? 8 : P <= 4 ? 5 : P <= 6 ? 4 : 3)
+                          : (P == 1 ? 8 : P == 2 ? 5 : P == 3 ? 4 : P == 4 ? 3 : P <= 7 ? 2 : 1);
+}
+#ifndef MGDP_BSERVE_MINW  // A/B builds: 0 = the compiler's choice (wave2_min_waves)
+#define MGDP_BSERVE_MINW 1
+#endif
+#ifndef MGDP_BSERVE_PRIO  // A/B builds: 0 = no s_setprio (polling waves at the solving waves' priority)
+#define MGDP_BSERVE_PRIO 1
+#endif
+#ifndef MGDP_BSERVE_OPQ  // A/B builds: 0 = the lane index as threadIdx.x in the request loop's solve
+#define MGDP_BSERVE_OPQ 1
+#endif
+template <typename T, int P>
+__global__ void __launch_bounds__(64, MGDP_BSERVE_MINW ? bserve_min_waves<T>(P) : wave2_min_waves<T>(kWpWave2 - P))
+vi_bserve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
+                 int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
+                 unsigned long long *__restrict__ host_out, const unsigned long long *__restrict__ host_cmd,
+                 unsigned long long *__restrict__ breq, unsigned long long *__restrict__ gk, unsigned long long served,
+                 unsigned long long idle_ticks, unsigned long long life_ticks, unsigned long long exit_tag, int copies,
+                 int nap, int wait_pub) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ __attribute__((aligned(16))) unsigned long long s_box[2];  // the forwarder's poll mailbox
+    const int lane = (int)threadIdx.x;
+    const int e = geo.order ? (int)geo.order[blockIdx.x] : (int)blockIdx.x;
+    uint8_t *cl = smem + 256;
+    copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
+    T *tile = reinterpret_cast<T *>(smem + wave2_tile_off(geo.HWp));
+    const bool fwd = blockIdx.x == 0;
+    const unsigned long long tg = (exit_tag & 0xffffull) << 32;
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long c_start = __builtin_amdgcn_s_memtime();
+    unsigned long long t_last = t_start, busy = 0, solves = 0;
+    if (fwd && lane == 0) {
+        s_box[0] = served;
+        s_box[1] = 0;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its LDS accesses are in order
+    const long long vb = (long long)e * geo.S;
+    while (true) {
+        unsigned long long cmd;
+        if (MGDP_BSERVE_PRIO) __builtin_amdgcn_s_setprio(0);
+        if (fwd) {
+            unsigned long long c = served;
+            // Host polls are PCIe reads the forwarder keeps in flight (up to 24, LDS DMA); while other grids
+            // of the request still sweep they would hold its CU's memory path (trace build: the grids
+            // that finished 15-18 us after the rest).  So first wait, at agent scope, for the request's
+            // publication (gk_exit's device copy of the epoch); the host posts the next one only after it.
+            if (wait_pub && solves > 0) {
+                while (__hip_atomic_load(gk + kGkTop2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+                       (served & 0xffffffffull)) {
+                    if (__builtin_amdgcn_s_memrealtime() - t_start > life_ticks) break;
+                    __builtin_amdgcn_s_sleep(4);
+                }
+                t_last = __builtin_amdgcn_s_memrealtime();  // the idle limit counts from the publication
+            }
+            if (lane == 0) {
+                while (true) {
+                    poll_issue(host_cmd, s_box);
+                    __builtin_amdgcn_s_sleep(1);
+                    c = __hip_atomic_load(&s_box[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (c != served) break;
+                    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+                    if (now - t_last > idle_ticks || now - t_start > life_ticks) {
+                        c = kServeQuit;
+                        break;
+                    }
+                }
+            }
+            cmd = rfl64(c);
+            const unsigned long long dw =
+                cmd == kServeQuit ? (tg | kBreqQuit) : (tg | (cmd & 0xffffffffull) | (cmd & kServeLast));
+            if (lane < copies) {
+#ifdef MGDP_BSERVE_TRACE  // trace build: the forwarder's request-seen stamp beside each copy
+                __hip_atomic_store(breq + lane * 16 + 1, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+#endif
+                __hip_atomic_store(breq + lane * 16, dw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else {
+            unsigned long long dw;
+            const unsigned long long *word = breq + (blockIdx.x % (unsigned)copies) * 16u;
+            while (true) {  // the whole wave loads the word (one request): no divergent loop
+                dw = rfl64(__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if ((dw & (0xffffull << 32)) == tg &&
+                    ((dw & kBreqQuit) || (dw & 0xffffffffull) != (served & 0xffffffffull)))
+                    break;
+                if (__builtin_amdgcn_s_memrealtime() - t_start > life_ticks + kBserveGraceTicks) {
+                    dw = tg | kBreqQuit;
+                    break;
+                }
+                for (int i = 0; i < nap; ++i) __builtin_amdgcn_s_sleep(10);
+            }
+            cmd = (dw & kBreqQuit) ? kServeQuit : ((dw & 0xffffffffull) | (dw & kServeLast));
+        }
+        if (cmd == kServeQuit) break;
+        if (MGDP_BSERVE_PRIO) __builtin_amdgcn_s_setprio(1);
+        const unsigned long long t_seen = __builtin_amdgcn_s_memrealtime();
+        int k = 0;
+        double dvl = 0.0;
+        auto done = [](int, double) {};
+        fused_wave2_xyd<T, true, P, true, (bool)MGDP_BSERVE_OPQ>(geo, cf, cl, tile, V + vb, V + vb, pi + vb, k, -1, dvl, done,
+                                                GkCtx{gk, (unsigned int)cmd, e, geo.B, host_out});
+        if (lane == 0) {
+            kenv[e] = k;
+            if (geo.kexec) geo.kexec[e] = k;
+            dvenv[e] = dvl;
+#ifdef MGDP_BSERVE_TRACE  // trace build: this grid's start / end after the forwarder saw the request,
+                          // 10 ns ticks in the low / high 16 bits of its executed-sweeps word
+            const unsigned long long t0 = __hip_atomic_load(breq + (blockIdx.x % (unsigned)copies) * 16u + 1,
+                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+            const unsigned long long a = t_seen - t0 < 0xffffull ? t_seen - t0 : 0xffffull;
+            const unsigned long long b = t1 - t0 < 0xffffull ? t1 - t0 : 0xffffull;
+            if (geo.kexec) geo.kexec[e] = (int)(a | (b << 16));
+#endif
+        }
+        served = cmd;
+        t_last = __builtin_amdgcn_s_memrealtime();
+        busy += t_last - t_seen;
+        ++solves;
+        if (cmd & kServeLast) break;
+    }
+    // Leaving: this wave's stores complete; the forwarder's clock words (mgdp_vi_serve_clock); the
+    // last wave out resets the counter and writes the launch's exit word (system-scope release).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+        if (fwd) {
+            __hip_atomic_store(host_out + kHoutClk, __builtin_amdgcn_s_memtime() - c_start, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_out + kHoutClk + 1, __builtin_amdgcn_s_memrealtime() - t_start, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_out + kHoutClk + 2, busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_out + kHoutClk + 3, solves, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __threadfence_system();
+        const unsigned long long n = __hip_atomic_fetch_add(breq + kBreqExit, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n == (unsigned long long)gridDim.x - 1ull) {
+            __hip_atomic_store(breq + kBreqExit, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __threadfence_system();
+            __hip_atomic_store(host_out + 11, exit_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 // The fused solve with the SURVEY 8(f) item-3 options (ND = NoDeath lava, HMODE = finite horizon
 // 1 / with pi_t 2): one workgroup per grid on the direction-major one-thread-per-cell path only
 // (the host enforces MGDP_MAP_CELL and no pair / quad steps when options are set).

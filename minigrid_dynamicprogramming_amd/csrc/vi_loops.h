@@ -1100,8 +1100,8 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
 // The whole wave, once it has its final answer: the launch's {kmax, dV, kmin} reduced over the
 // counter tree, the last exit publishing it -- the reduce kernel a batch launch otherwise needs,
 // folded into the launch.
-__device__ __forceinline__ void gk_exit(const GkCtx &g, int k_rep, double dv) {
-    const int lane = (int)threadIdx.x & 63;
+__device__ __forceinline__ void gk_exit(const GkCtx &g, int k_rep, double dv, int lane_in = -1) {
+    const int lane = lane_in >= 0 ? lane_in : (int)threadIdx.x & 63;
     int *kr = reinterpret_cast<int *>(g.buf + gk_kr_off(g.B));
     unsigned long long *dvr = g.buf + gk_dv_off(g.B);
     int *smin = reinterpret_cast<int *>(g.buf + kGkSxMin);
@@ -1156,6 +1156,9 @@ __device__ __forceinline__ void gk_exit(const GkCtx &g, int k_rep, double dv) {
     if (lane == 0) {
         __hip_atomic_exchange(g.buf + kGkTop2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         publish(g.pub, (unsigned long long)mx, dm, (unsigned long long)mn, g.epoch);
+        // the same epoch in device memory (the top counter's line): the resident batch server's forwarder
+        // waits on it before polling the host for the next request
+        __hip_atomic_store(g.buf + kGkTop2 + 1, (unsigned long long)g.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1189,12 +1192,15 @@ __device__ __forceinline__ T tree_max3(const T *x) {
 template <int B> struct WaveBuf { static constexpr int value = B; };
 // WT: write the exit stores through the L2 (store_v4_exit; the caller instantiates it for the launches
 // with the in-launch reduction, i.e. resident batches)
-template <typename T, bool LOCAL, int P, bool WT = false, typename Done>
+// OPQ (the resident batch server, which calls this once per request in its request loop): the lane
+// index is re-derived per call by an asm the compiler cannot hoist, so nothing computed from it
+// (tile and V addresses, cell indices) is moved out of the request loop and held live across it.
+template <typename T, bool LOCAL, int P, bool WT = false, bool OPQ = false, typename Done>
 __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &cf, const uint8_t *cl, T *tile,
                                                 const T *Vg, T *Vg_out, int8_t *pig, int &k, int k_target,
                                                 double &dvl, const Done &done, const GkCtx gk = GkCtx{}) {
     static_assert(P >= 1 && P <= 8, "goal bits: 4 per cell, 32 per lane");
-    const int lane = (int)threadIdx.x;
+    const int lane = OPQ ? late_tid(0) : (int)threadIdx.x;
     const int W = geo.W, padw = wave2_padw(W);
     // k came from a per-grid word in memory (a VGPR); it is wave-uniform, so count sweeps in an SGPR
     // (the loop's k < max_sweeps test and increment are then scalar instructions, not VALU)
@@ -1309,7 +1315,7 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
     // Exit work (reduction, publication, pi pass, V store) on cur = V_k, prv = V_{k-1}.
     auto finish = [&](const T (&cur)[P][4], const T (&prv)[P][4]) {
         dvl = (double)wave_max(diff);
-        if (LOCAL && gk.buf != nullptr) gk_exit(gk, k, dvl);  // this launch's reduction and its publication
+        if (LOCAL && gk.buf != nullptr) gk_exit(gk, k, dvl, OPQ ? late_tid(0) : lane);  // this launch's reduction and its publication
         done(k, dvl);
         // pi of the last sweep = argmax on V_{k-1} (`prv`), per action with the usual topology
 #pragma unroll

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--method", default="fused")
     args = ap.parse_args()
     import torch
 
@@ -28,7 +29,7 @@ def main():
 
     _lib.pin_host_thread(0)
     cells = gen.generate(args.env, 0, args.B, enc=False, cells=True, agent=False)["cells"]
-    vi = mg.ValueIteration(cells, dtype=args.dtype)
+    vi = mg.ValueIteration(cells, dtype=args.dtype, method=args.method)
     wall, kern = [], []
     for _ in range(args.reps):
         vi.enable_timing(False)
@@ -42,12 +43,14 @@ def main():
         for _ in range(args.solves):
             vi.solve()
         ms, n = vi.kernel_time()
-        kern.append(ms * 1e3 / max(n, 1))
+        kern.append(ms * 1e3 / max(n, 1))  # per launch (the sweep method: one launch per sweep)
+        launches = n
     gs = vi.grid_sweeps()
     upd = vi.updates_per_sweep * k
     print(json.dumps({"tag": args.tag, "env": args.env, "B": args.B, "dtype": args.dtype, "kernel": vi.kernel_name,
                       "sweeps": k, "us_per_solve": round(float(np.median(wall)), 2),
-                      "kernel_us": round(float(np.median(kern)), 2),
+                      "kernel_us": round(float(np.median(kern)), 2), "method": args.method,
+                      "launches": launches,
                       "updates_per_s": upd / (float(np.median(wall)) * 1e-6),
                       "executed_frac": round(float(gs.mean()) / k, 4),
                       "wall_all": [round(x, 1) for x in wall]}), flush=True)
