@@ -686,12 +686,13 @@ vi_serve_kernel(Geo geo, Coef<T> cf, uint8_t *__restrict__ cells, T *__restrict_
 // other wave polls that word at agent scope with s_sleep between polls and at priority 0 (the
 // waves still sweeping get the issue slots).  Only the forwarder decides to leave (quit word,
 // idle or life limit); the others leave on its quit word, or after the life limit plus a grace
-// period, so every wave reaches the exit.  The last wave out (the exit counter) writes the exit
+// period, so every wave reaches the exit.  The last wave out (a two-level exit counter) writes the exit
 // word, as a lone server does.
 constexpr unsigned long long kBreqQuit = 1ull << 63;
 constexpr int kBreqCopies = 64;                                       // request lines (workgroup w polls w % copies)
-constexpr int kBreqExit = kBreqCopies * 16;                           // the exit counter's word (its own line)
-constexpr int kBreqWords = kBreqExit + 16;
+constexpr int kBreqExit = kBreqCopies * 16;                           // exit counters: 64 shard lines, then the top line
+constexpr int kBreqExitShards = 64;
+constexpr int kBreqWords = kBreqExit + (kBreqExitShards + 1) * 16;
 constexpr unsigned long long kBserveGraceTicks = 100000000ull;        // 1 s at 100 MHz
 __device__ __forceinline__ unsigned long long rfl64(unsigned long long x) {
     const unsigned int lo = __builtin_amdgcn_readfirstlane((unsigned int)x);
@@ -827,24 +828,35 @@ vi_bserve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__re
         ++solves;
         if (cmd & kServeLast) break;
     }
-    // Leaving: this wave's stores complete; the forwarder's clock words (mgdp_vi_serve_clock); the
-    // last wave out resets the counter and writes the launch's exit word (system-scope release).
+    // Leaving: this wave's stores complete (the exit V / pi stores are write-through, the clock words
+    // system-scope: drained means written), then the exit counters; the last wave out resets them and
+    // writes the launch's exit word.  Waves leaving after a kServeLast request do it while that
+    // request's long grids still sweep, so (tools/probe_bserve.py, the last request's wall): no wave
+    // but the last fences (a system-scope release writes back the L2: +35-60 us), and the count is a
+    // two-level tree like the solve's (64 shard lines, then a top line) -- 8192 atomics on one word
+    // serialised at ~10 ns each ahead of the request's own publication: +82 us.
+    if (lane == 0 && fwd) {
+        __hip_atomic_store(host_out + kHoutClk, __builtin_amdgcn_s_memtime() - c_start, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host_out + kHoutClk + 1, __builtin_amdgcn_s_memrealtime() - t_start, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host_out + kHoutClk + 2, busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host_out + kHoutClk + 3, solves, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) {
-        if (fwd) {
-            __hip_atomic_store(host_out + kHoutClk, __builtin_amdgcn_s_memtime() - c_start, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(host_out + kHoutClk + 1, __builtin_amdgcn_s_memrealtime() - t_start, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(host_out + kHoutClk + 2, busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(host_out + kHoutClk + 3, solves, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        __threadfence_system();
-        const unsigned long long n = __hip_atomic_fetch_add(breq + kBreqExit, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (n == (unsigned long long)gridDim.x - 1ull) {
-            __hip_atomic_store(breq + kBreqExit, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __threadfence_system();
-            __hip_atomic_store(host_out + 11, exit_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned int G = gridDim.x;
+        const unsigned int nsh = G < (unsigned)kBreqExitShards ? G : (unsigned)kBreqExitShards;
+        const unsigned int sh = blockIdx.x % nsh;
+        const unsigned long long size = G / nsh + (sh < G % nsh ? 1u : 0u);
+        unsigned long long *cnt = breq + kBreqExit + sh * 16u, *top = breq + kBreqExit + kBreqExitShards * 16;
+        if (__hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == size - 1ull) {
+            __hip_atomic_store(cnt, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (__hip_atomic_fetch_add(top, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsh - 1ull) {
+                __hip_atomic_store(top, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(host_out + 11, exit_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
     }
 }

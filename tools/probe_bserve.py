@@ -49,6 +49,15 @@ def main():
         st, en = (w & 0xffff) * 0.01, (w >> 16) * 0.01
         trace = {"start_us_pcts": [round(float(np.percentile(st, q)), 2) for q in (0, 50, 90, 99, 100)],
                  "end_us_pcts": [round(float(np.percentile(en, q)), 2) for q in (0, 50, 90, 99, 100)]}
+    # the server's last request (mgdp_vi_solve_last): its wall, and the launches the clock counted
+    vi.enable_timing(False)
+    for _ in range(5):
+        vi.solve()
+    t = time.perf_counter()
+    vi.solve(True)
+    last_us = (time.perf_counter() - t) * 1e6
+    vi.synchronize()
+    clk_last = vi.serve_clock()
     vi.enable_timing(True)
     for _ in range(args.solves):
         vi.solve()
@@ -56,7 +65,9 @@ def main():
     torch.cuda.synchronize()
     print(json.dumps({"tag": args.tag, "env": args.env, "B": args.B, "sweeps": k,
                       "served_us": round(float(np.median(wall)), 2), "served_gpu_us": round(float(np.median(gpu)), 2),
-                      "solves_served": clk["solves"], "launch_kernel_us": round(ms * 1e3 / max(n, 1), 2), "trace": trace}), flush=True)
+                      "solves_served": clk["solves"], "launch_kernel_us": round(ms * 1e3 / max(n, 1), 2), "trace": trace,
+                      "last_us": round(last_us, 2), "last_launches": clk_last["launches"], "last_solves": clk_last["solves"]}),
+          flush=True)
     vi.close()
 
 
