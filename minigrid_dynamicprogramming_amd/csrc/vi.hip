@@ -170,6 +170,7 @@ struct mgdp_vi {
     int bserve_copies = kBreqCopies;     // request lines the workgroups poll (MGDP_BSERVE_COPIES)
     int bserve_nap = 1;                  // s_sleep(10)s between polls (MGDP_BSERVE_NAP)
     int bserve_wait_pub = 1;             // the forwarder polls the host only after the publication (MGDP_BSERVE_WAIT_PUB)
+    double bserve_prio_frac = 0.0;       // this fraction of the dispatch order's longest grids sweeps at a higher issue priority (MGDP_BSERVE_PRIO_FRAC)
     unsigned long long *d_breq = nullptr;  // its device words (kBreqWords): forwarded request, exit counter
 };
 
@@ -518,7 +519,8 @@ int launch_bserve_p(mgdp_vi *vi, unsigned int served, TimedPair tp) {
     hipExtLaunchKernelGGL(vi_bserve_kernel<T, P>, dim3(vi->d.B), dim3(64), smem, vi->stream, tp.a, tp.b, 0, make_geo(vi),
                           make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv, vi->d_dvenv, vi->d_hout,
                           vi->d_hout + kHoutReq, vi->d_breq, vi->d_gk, (unsigned long long)served, vi->serve_idle_ticks,
-                          vi->serve_life_ticks, vi->serve_tag, vi->bserve_copies, vi->bserve_nap, vi->bserve_wait_pub);
+                          vi->serve_life_ticks, vi->serve_tag, vi->bserve_copies, vi->bserve_nap, vi->bserve_wait_pub,
+                          vi->order_valid && vi->learn_order ? (int)(vi->bserve_prio_frac * vi->d.B) : 0);
     MGDP_HIP(hipGetLastError());
     return 0;
 }
@@ -1109,6 +1111,7 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
             if (const char *ev = std::getenv("MGDP_BSERVE_COPIES")) vi->bserve_copies = std::min(kBreqCopies, std::max(1, std::atoi(ev)));
             if (const char *ev = std::getenv("MGDP_BSERVE_NAP")) vi->bserve_nap = std::min(64, std::max(0, std::atoi(ev)));
             if (const char *ev = std::getenv("MGDP_BSERVE_WAIT_PUB")) vi->bserve_wait_pub = std::atoi(ev) != 0;
+            if (const char *ev = std::getenv("MGDP_BSERVE_PRIO_FRAC")) vi->bserve_prio_frac = std::min(1.0, std::max(0.0, std::atof(ev)));
             if (vi->bserve && vi->gk && !vi->band && !vi->mix && !vi->wave2n && d.slip_p < 0.0 && d.B > 1) {
                 const void *kb = f32 ? pick_bserve<float>(vi->wave2) : pick_bserve<double>(vi->wave2);
                 int per_cu = 0;

@@ -725,7 +725,7 @@ vi_bserve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__re
                  unsigned long long *__restrict__ host_out, const unsigned long long *__restrict__ host_cmd,
                  unsigned long long *__restrict__ breq, unsigned long long *__restrict__ gk, unsigned long long served,
                  unsigned long long idle_ticks, unsigned long long life_ticks, unsigned long long exit_tag, int copies,
-                 int nap, int wait_pub) {
+                 int nap, int wait_pub, int prio_n) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ __attribute__((aligned(16))) unsigned long long s_box[2];  // the forwarder's poll mailbox
     const int lane = (int)threadIdx.x;
@@ -801,7 +801,11 @@ vi_bserve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__re
             cmd = (dw & kBreqQuit) ? kServeQuit : ((dw & 0xffffffffull) | (dw & kServeLast));
         }
         if (cmd == kServeQuit) break;
-        if (MGDP_BSERVE_PRIO) __builtin_amdgcn_s_setprio(1);
+        if (MGDP_BSERVE_PRIO) {
+            // the first prio_n workgroups hold the dispatch order's longest grids (MGDP_BSERVE_PRIO_FRAC)
+            if ((int)blockIdx.x < prio_n) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(1);
+        }
         const unsigned long long t_seen = __builtin_amdgcn_s_memrealtime();
         int k = 0;
         double dvl = 0.0;
