@@ -170,6 +170,7 @@ struct mgdp_vi {
     int bserve_copies = kBreqCopies;     // request lines the workgroups poll (MGDP_BSERVE_COPIES)
     int bserve_nap = 1;                  // s_sleep(10)s between polls (MGDP_BSERVE_NAP)
     int bserve_wait_pub = 1;             // the forwarder polls the host only after the publication (MGDP_BSERVE_WAIT_PUB)
+    bool solving = false;                // inside mgdp_vi_solve: its run_local may use the batch server
     double bserve_prio_frac = 0.0;       // this fraction of the dispatch order's longest grids sweeps at a higher issue priority (MGDP_BSERVE_PRIO_FRAC)
     unsigned long long *d_breq = nullptr;  // its device words (kBreqWords): forwarded request, exit counter
 };
@@ -1469,7 +1470,10 @@ int mgdp_vi_run_local(mgdp_vi *vi, int32_t *k_local_max) {
     MGDP_CHECK(vi->cells_loaded, MGDP_E_INVALID, "no cells loaded");
     DeviceGuard guard(vi->d.device);
     if (vi->d.method == MGDP_METHOD_FUSED) {
-        const bool serve = served_eligible(vi) && vi->fresh;
+        // the batch server only for mgdp_vi_solve's own run_local: a caller driving run_local / run_to
+        // itself (a collective protocol) may enqueue device work between them that needs the CU slots a
+        // resident batch server holds
+        const bool serve = (serve_eligible(vi) || (vi->solving && bserve_eligible(vi))) && vi->fresh;
         if (serve) {
             if (int rc = serve_request(vi)) return rc;
         } else {
@@ -1714,8 +1718,11 @@ int mgdp_vi_solve(mgdp_vi *vi, int32_t *sweeps_out, double *dv_out, int32_t *con
                    "chained solve: grids ended at sweeps %d..%d, not at one common K", vi->k_min, vi->k_max);
         vi->k_done = k;
     } else {
-        if (int rc = mgdp_vi_run_local(vi, &k)) return rc;
-        if (int rc = mgdp_vi_run_to(vi, k, &dv)) return rc;
+        vi->solving = true;
+        const int rc = mgdp_vi_run_local(vi, &k);
+        vi->solving = false;
+        if (rc) return rc;
+        if (int rc2 = mgdp_vi_run_to(vi, k, &dv)) return rc2;
     }
     while (vi->d.horizon == 0 && !(dv < vi->d.tol) && k < vi->d.max_sweeps) {  // contraction broken by rounding: global rule
         if (int rc = mgdp_vi_sweep(vi, &dv)) return rc;

@@ -149,3 +149,37 @@ def test_solve_last_and_synchronize():
         _check(vi, o, vi.sweeps)
     finally:
         vi.close()
+
+
+def test_protocol_run_local_does_not_start_a_batch_server():
+    """A caller driving run_local / run_to itself (the sharded protocols) gets launches: a resident
+    batch server would hold the CU slots a collective between them needs."""
+    cells = random_grids(256, 11, 11, seed=5, goals=1)
+    o = oracle.value_iteration(0, cells, dtype="f32", nthreads=16, fixed_point=True)
+    vi = _handle(cells, "f32")
+    try:
+        vi.reset()
+        K = vi.run_local()
+        dv = vi.run_to(K)
+        vi.finish(K, dv)
+        assert K == o["sweeps"]
+        assert vi.serve_clock()["solves"] == 0
+        np.testing.assert_array_equal(vi.values(), o["V"])
+        np.testing.assert_array_equal(vi.policy(), o["pi"])
+        assert vi.solve() == o["sweeps"] and vi.solve() == o["sweeps"]  # solve() itself is served
+        assert vi.serve_clock()["solves"] >= 1
+    finally:
+        vi.close()
+
+
+@pytest.mark.parametrize("B", [2, 3, 64])
+def test_small_served_batches(B):
+    cells = random_grids(B, 13, 13, seed=B, goals=1)
+    o = oracle.value_iteration(0, cells, dtype="f64", nthreads=4, fixed_point=True)
+    vi = _handle(cells, "f64")
+    try:
+        for _ in range(3):
+            assert vi.solve() == o["sweeps"]
+        _check(vi, o, o["sweeps"])
+    finally:
+        vi.close()
