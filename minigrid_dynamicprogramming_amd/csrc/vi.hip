@@ -166,6 +166,7 @@ struct mgdp_vi {
     // the resident batch server (vi_bserve_kernel): one-wave batches within its resident capacity,
     // solves with launch timing off (MGDP_BSERVE=0: off)
     bool bserve = true;
+    bool bserve_any = false;             // also batches past its resident capacity, several grids per workgroup (MGDP_BSERVE=2)
     int bserve_cap = 0;                  // resident workgroups of vi_bserve_kernel on this device
     int bserve_copies = kBreqCopies;     // request lines the workgroups poll (MGDP_BSERVE_COPIES)
     int bserve_nap = 1;                  // s_sleep(10)s between polls (MGDP_BSERVE_NAP)
@@ -501,7 +502,7 @@ void account_server_clock(mgdp_vi *vi);
 
 // The batch server's instantiation for P cells per lane (the wave2 kernel's P); nullptr if out of range.
 template <typename T>
-const void *pick_bserve(int P) {
+const void *pick_bserve(int P) {  // the resident instantiation (the capacity of both is the same by bserve_min_waves)
     switch (P) {
     case 1: return (const void *)vi_bserve_kernel<T, 1>;
     case 2: return (const void *)vi_bserve_kernel<T, 2>;
@@ -517,7 +518,9 @@ const void *pick_bserve(int P) {
 template <typename T, int P>
 int launch_bserve_p(mgdp_vi *vi, unsigned int served, TimedPair tp) {
     const int smem = wave2_smem_bytes(vi->HWp, vi->d.W, P, (int)sizeof(T));
-    hipExtLaunchKernelGGL(vi_bserve_kernel<T, P>, dim3(vi->d.B), dim3(64), smem, vi->stream, tp.a, tp.b, 0, make_geo(vi),
+    static const bool force_multi = std::getenv("MGDP_BSERVE_FORCE_MULTI") != nullptr;  // diagnostics
+    auto kern = (vi->d.B > vi->bserve_cap || force_multi) ? vi_bserve_kernel<T, P, true> : vi_bserve_kernel<T, P, false>;
+    hipExtLaunchKernelGGL(kern, dim3(std::min(vi->d.B, vi->bserve_cap)), dim3(64), smem, vi->stream, tp.a, tp.b, 0, make_geo(vi),
                           make_coef<T>(vi), vi->d_cells, (T *)vi->d_V[0], vi->d_pi, vi->d_kenv, vi->d_dvenv, vi->d_hout,
                           vi->d_hout + kHoutReq, vi->d_breq, vi->d_gk, (unsigned long long)served, vi->serve_idle_ticks,
                           vi->serve_life_ticks, vi->serve_tag, vi->bserve_copies, vi->bserve_nap, vi->bserve_wait_pub,
@@ -757,7 +760,8 @@ bool serve_eligible(const mgdp_vi *vi) {
 // with launch timing off (a timed solve is a launch, so kernel_time() keeps timing one solve per
 // launch), from V_0 = 0 under the own rule with at least one sweep.
 bool bserve_eligible(const mgdp_vi *vi) {
-    return vi->persistent && vi->bserve && vi->d_breq && !vi->timing && vi->d.B > 1 && vi->d.B <= vi->bserve_cap &&
+    return vi->persistent && vi->bserve && vi->d_breq && vi->d_gk && !vi->timing && vi->d.B > 1 &&
+           (vi->d.B <= vi->bserve_cap || vi->bserve_any) &&
            !vi->opts && vi->d.method == MGDP_METHOD_FUSED && vi->d.horizon == 0 && vi->d.max_sweeps >= 1;
 }
 bool served_eligible(const mgdp_vi *vi) { return serve_eligible(vi) || bserve_eligible(vi); }
@@ -1108,12 +1112,15 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
                 vi->gk_capacity = per_cu * cus;
             vi->gk = gk_on == 1 || (gk_on == 2 && d.B <= vi->gk_capacity);
             // the resident batch server runs the same loop (wave2 layout, in-launch reduction)
-            if (const char *ev = std::getenv("MGDP_BSERVE")) vi->bserve = std::atoi(ev) != 0;
+            if (const char *ev = std::getenv("MGDP_BSERVE")) {
+                vi->bserve = std::atoi(ev) != 0;
+                vi->bserve_any = std::atoi(ev) == 2;
+            }
             if (const char *ev = std::getenv("MGDP_BSERVE_COPIES")) vi->bserve_copies = std::min(kBreqCopies, std::max(1, std::atoi(ev)));
             if (const char *ev = std::getenv("MGDP_BSERVE_NAP")) vi->bserve_nap = std::min(64, std::max(0, std::atoi(ev)));
             if (const char *ev = std::getenv("MGDP_BSERVE_WAIT_PUB")) vi->bserve_wait_pub = std::atoi(ev) != 0;
             if (const char *ev = std::getenv("MGDP_BSERVE_PRIO_FRAC")) vi->bserve_prio_frac = std::min(1.0, std::max(0.0, std::atof(ev)));
-            if (vi->bserve && vi->gk && !vi->band && !vi->mix && !vi->wave2n && d.slip_p < 0.0 && d.B > 1) {
+            if (vi->bserve && (vi->gk || vi->bserve_any) && !vi->band && !vi->mix && !vi->wave2n && d.slip_p < 0.0 && d.B > 1) {
                 const void *kb = f32 ? pick_bserve<float>(vi->wave2) : pick_bserve<double>(vi->wave2);
                 int per_cu = 0;
                 if (kb && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kb, 64, smem2) == hipSuccess)
@@ -1211,11 +1218,11 @@ int mgdp_vi_create(const mgdp_vi_desc *desc, mgdp_vi **out) {
     al((void **)&vi->d_shards, sizeof(unsigned long long) * 8 * (size_t)(d.max_sweeps + 1));
     al((void **)&vi->d_red, sizeof(unsigned long long) * (kRedShards * 4 + 2));
     al((void **)&vi->d_pub1, sizeof(unsigned long long) * 4);
-    if (vi->gk) {
+    if (vi->gk || (vi->bserve && vi->bserve_cap > 0 && vi->bserve_any)) {
         al((void **)&vi->d_gk, sizeof(unsigned long long) * gk_words(d.B));
         if (e == hipSuccess) e = hipMemset(vi->d_gk, 0, sizeof(unsigned long long) * gk_words(d.B));
     }
-    if (vi->bserve && vi->bserve_cap > 0 && d.B <= vi->bserve_cap) {
+    if (vi->bserve && vi->bserve_cap > 0 && (d.B <= vi->bserve_cap || vi->bserve_any)) {
         al((void **)&vi->d_breq, sizeof(unsigned long long) * kBreqWords);
         if (e == hipSuccess) e = hipMemset(vi->d_breq, 0, sizeof(unsigned long long) * kBreqWords);
     }

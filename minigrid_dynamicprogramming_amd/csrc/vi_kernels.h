@@ -718,7 +718,9 @@ __host__ __device__ constexpr int bserve_min_waves(int P) {
 #ifndef MGDP_BSERVE_OPQ  // A/B builds: 0 = the lane index as threadIdx.x in the request loop's solve
 #define MGDP_BSERVE_OPQ 1
 #endif
-template <typename T, int P>
+// MULTI: the launch has fewer workgroups than grids (a batch past the resident capacity, MGDP_BSERVE=2):
+// its own instantiation, so the resident loop keeps its registers.
+template <typename T, int P, bool MULTI = false>
 __global__ void __launch_bounds__(64, MGDP_BSERVE_MINW ? bserve_min_waves<T>(P) : wave2_min_waves<T>(kWpWave2 - P))
 vi_bserve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__restrict__ V,
                  int8_t *__restrict__ pi, int32_t *__restrict__ kenv, double *__restrict__ dvenv,
@@ -729,9 +731,10 @@ vi_bserve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__re
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ __attribute__((aligned(16))) unsigned long long s_box[2];  // the forwarder's poll mailbox
     const int lane = (int)threadIdx.x;
-    const int e = geo.order ? (int)geo.order[blockIdx.x] : (int)blockIdx.x;
+    constexpr bool multi = MULTI;  // past the resident capacity: several grids per workgroup
+    const int e = multi ? 0 : (geo.order ? (int)geo.order[blockIdx.x] : (int)blockIdx.x);
     uint8_t *cl = smem + 256;
-    copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
+    if (!multi) copy16(cl, cells + (long long)e * geo.HWp, geo.HWp);
     T *tile = reinterpret_cast<T *>(smem + wave2_tile_off(geo.HWp));
     const bool fwd = blockIdx.x == 0;
     const unsigned long long tg = (exit_tag & 0xffffull) << 32;
@@ -810,9 +813,44 @@ vi_bserve_kernel(Geo geo, Coef<T> cf, const uint8_t *__restrict__ cells, T *__re
         int k = 0;
         double dvl = 0.0;
         auto done = [](int, double) {};
-        fused_wave2_xyd<T, true, P, true, (bool)MGDP_BSERVE_OPQ>(geo, cf, cl, tile, V + vb, V + vb, pi + vb, k, -1, dvl, done,
-                                                GkCtx{gk, (unsigned int)cmd, e, geo.B, host_out});
-        if (lane == 0) {
+        if constexpr (MULTI) {
+            // More grids than workgroups: this workgroup solves the dispatch order's positions
+            // blockIdx.x, + G, + 2G, ... (round-robin over the longest-first order), each from V_0 = 0
+            // with its cells staged in turn, and arrives ONCE at the counter tree with its grids'
+            // {min, max} sweeps and max dV (a per-grid arrival would hold the wave on its ticket's round
+            // trip before every next grid).
+            int kmn = 0x7fffffff, kmx = 0;
+            double dvm = 0.0;
+            for (int i = (int)blockIdx.x; i < geo.B; i += (int)gridDim.x) {
+                const int eg = geo.order ? (int)geo.order[i] : i;
+                const long long vg = (long long)eg * geo.S;
+                copy16(cl, cells + (long long)eg * geo.HWp, geo.HWp);
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // one wave: the cells are in place
+                int kg = 0;
+                double dg = 0.0;
+                fused_wave2_xyd<T, true, P, true, (bool)MGDP_BSERVE_OPQ>(geo, cf, cl, tile, V + vg, V + vg, pi + vg, kg, -1,
+                                                                        dg, done, GkCtx{});
+                if (lane == 0) {
+                    kenv[eg] = kg;
+                    if (geo.kexec) geo.kexec[eg] = kg;
+                    dvenv[eg] = dg;
+#ifdef MGDP_BSERVE_DEBUG_WG  // diagnostics build: which workgroup and iteration solved each grid
+                    if (geo.kexec) geo.kexec[eg] = (int)blockIdx.x | (((i - (int)blockIdx.x) / (int)gridDim.x) << 20);
+#endif
+                }
+                kmn = min(kmn, kg);
+                kmx = max(kmx, kg);
+                dvm = dg > dvm ? dg : dvm;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            gk_exit<true>(GkCtx{gk, (unsigned int)cmd, (int)blockIdx.x, (int)gridDim.x, host_out}, kmx, dvm,
+                          MGDP_BSERVE_OPQ ? late_tid(0) : lane, kmn);
+            k = kmx;
+        } else {
+            fused_wave2_xyd<T, true, P, true, (bool)MGDP_BSERVE_OPQ>(geo, cf, cl, tile, V + vb, V + vb, pi + vb, k, -1, dvl,
+                                                                    done, GkCtx{gk, (unsigned int)cmd, e, geo.B, host_out});
+        }
+        if (lane == 0 && !multi) {
             kenv[e] = k;
             if (geo.kexec) geo.kexec[e] = k;
             dvenv[e] = dvl;

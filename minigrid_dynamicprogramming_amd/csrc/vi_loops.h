@@ -240,10 +240,14 @@ __device__ __forceinline__ void store_v4_exit(T *p, const V4<T> &v, bool wt) {
         if constexpr (sizeof(T) == 4) {
             // one 16-B store, as the plain form (two 8-B atomic stores re-paired the loop's registers:
             // +5 VALU per two sweeps at P = 2); its vmcnt is not tracked by the compiler, which only
-            // makes a later wait of its own more conservative (vector memory returns in order)
+            // makes a later wait of its own more conservative (vector memory returns in order).
+            // The s_nop 1 INSIDE the string is the store-data hazard's wait states: the compiler does not
+            // pad an asm store, and its next VALU may overwrite the data registers before a store of more
+            // than 8 bytes has read them (cdna_hip_programming.md §5.7; found in round 6, where the batch
+            // server's multi-grid loop reused them at once: the first dword of 4-lane groups stored stale)
             typedef float f4v __attribute__((ext_vector_type(4)));
             const f4v x = {v.v[0], v.v[1], v.v[2], v.v[3]};
-            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
+            asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(x) : "memory");
         } else {
 #pragma unroll
             for (int d = 0; d < 4; ++d)
@@ -1076,7 +1080,8 @@ constexpr int kGkSxMax = kGkSxMin + kGkShards / 2;             // int32 [256] sh
 constexpr int kGkSxDv = kGkSxMax + kGkShards / 2;              // u64 [256] shard max dV bits
 __host__ __device__ inline int gk_kr_off(int B) { (void)B; return kGkSxDv + kGkShards; }  // int32 [B] sweeps,
 __host__ __device__ inline int gk_dv_off(int B) { return gk_kr_off(B) + (B + 1) / 2; }     // u64 [B] dV bits
-__host__ __device__ inline int gk_words(int B) { return gk_dv_off(B) + B; }
+__host__ __device__ inline int gk_kn_off(int B) { return gk_dv_off(B) + B; }               // int32 [B] min sweeps (KMIN)
+__host__ __device__ inline int gk_words(int B) { return gk_kn_off(B) + (B + 1) / 2; }
 
 __device__ __forceinline__ int wave_max_i(int v) {
 #pragma unroll
@@ -1100,9 +1105,13 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
 // The whole wave, once it has its final answer: the launch's {kmax, dV, kmin} reduced over the
 // counter tree, the last exit publishing it -- the reduce kernel a batch launch otherwise needs,
 // folded into the launch.
-__device__ __forceinline__ void gk_exit(const GkCtx &g, int k_rep, double dv, int lane_in = -1) {
+// KMIN (the batch server's workgroups past the resident capacity, one arrival per workgroup for all
+// its grids): the entry reports a {min, max} sweep pair, k_min_rep its min.
+template <bool KMIN = false>
+__device__ __forceinline__ void gk_exit(const GkCtx &g, int k_rep, double dv, int lane_in = -1, int k_min_rep = 0) {
     const int lane = lane_in >= 0 ? lane_in : (int)threadIdx.x & 63;
     int *kr = reinterpret_cast<int *>(g.buf + gk_kr_off(g.B));
+    int *kn = KMIN ? reinterpret_cast<int *>(g.buf + gk_kn_off(g.B)) : kr;
     unsigned long long *dvr = g.buf + gk_dv_off(g.B);
     int *smin = reinterpret_cast<int *>(g.buf + kGkSxMin);
     int *smax = reinterpret_cast<int *>(g.buf + kGkSxMax);
@@ -1113,6 +1122,7 @@ __device__ __forceinline__ void gk_exit(const GkCtx &g, int k_rep, double dv, in
     unsigned long long t = 0;
     if (lane == 0) {
         __hip_atomic_store(kr + g.e, k_rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (KMIN) __hip_atomic_store(kn + g.e, k_min_rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(dvr + g.e, (unsigned long long)__double_as_longlong(dv), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1124,7 +1134,7 @@ __device__ __forceinline__ void gk_exit(const GkCtx &g, int k_rep, double dv, in
     for (int i = lane; i < size; i += 64) {
         const int x = __hip_atomic_load(kr + s + i * nsh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long y = __hip_atomic_load(dvr + s + i * nsh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        mn = min(mn, x);
+        mn = min(mn, KMIN ? __hip_atomic_load(kn + s + i * nsh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : x);
         mx = max(mx, x);
         dm = y > dm ? y : dm;
     }

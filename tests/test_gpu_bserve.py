@@ -183,3 +183,25 @@ def test_small_served_batches(B):
         _check(vi, o, o["sweeps"])
     finally:
         vi.close()
+
+
+@pytest.mark.parametrize("extra", [1, 777])
+def test_multi_grid_server_past_capacity(extra):
+    """MGDP_BSERVE=2: a batch past the server's resident capacity, several grids per workgroup (the
+    multi-grid loop).  Also the regression test of the write-through exit store's data hazard (an asm
+    global_store_dwordx4 without its s_nop: the loop's next VALU overwrote the store's first data
+    register before it was read, and some 4-lane groups stored a stale first dword -- ~0.3 % of the
+    grids wrong here before the fix)."""
+    import torch
+
+    cap = 32 * torch.cuda.get_device_properties(0).multi_processor_count  # 9x7 grids: 8 waves per SIMD
+    cells = random_grids(cap + extra, 9, 7, seed=extra, goals=2)
+    o = oracle.value_iteration(0, cells, dtype="f32", nthreads=16, fixed_point=True)
+    vi = _handle(cells, "f32", {"MGDP_BSERVE": "2"})
+    try:
+        for _ in range(3):
+            assert vi.solve() == o["sweeps"]
+        assert vi.serve_clock()["solves"] >= 2
+        _check(vi, o, o["sweeps"])
+    finally:
+        vi.close()
