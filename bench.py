@@ -690,6 +690,12 @@ def measure(args, dtype, cells, local, dist, red_dev, reducer, sharded, split_ev
     for i in range(args.warmup):
         one_solve(last=i == args.warmup - 1)
         wstamps.append(time.perf_counter())
+    if split and not sharded:
+        # the BASELINE-config blocks: the W warmup solves of a batch last well under a millisecond, so the
+        # device's clock has not ramped when the region starts; keep solving for PRIME_BLOCK_S first (the
+        # headline's priming rule, shorter: a batched solve does far more work per call)
+        while time.perf_counter() - wstamps[0] < PRIME_BLOCK_S:
+            one_solve()
     vi.synchronize()
     torch.cuda.synchronize()
     warm_us = [(b - a) * 1e6 for a, b in zip(wstamps[:-1], wstamps[1:])]
@@ -1182,6 +1188,7 @@ FRESH_SETS = 3  # fresh grid sets per BASELINE-config block: first-solve timing 
 FRESH_SETS = int(os.environ.get("MGDP_BENCH_FRESH", FRESH_SETS))
 # steady-state priming of a resident lone-grid server (measure(): the stated criterion)
 PRIME_MIN_S, PRIME_WIN, PRIME_TOL, PRIME_MAX_S, PRIME_RELAUNCH = 0.2, 512, 0.02, 1.0, 16
+PRIME_BLOCK_S = 0.1  # warmup time of each BASELINE-config block (round 6)
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9  # MI355X_MICROARCH.md: 4 SIMD-32 per CU, one wave64 VALU op per 2 cycles
 
 
