@@ -1175,6 +1175,9 @@ __device__ __forceinline__ void gk_exit(const GkCtx &g, int k_rep, double dv, in
 #ifndef MGDP_WAVE2_PREFETCH  // A/B builds: 1 = fused_wave2_xyd reads the next sweep's fronts early
 #define MGDP_WAVE2_PREFETCH 0   // measured neutral (profiles/r05_pf/) and +9 VGPRs at P = 4
 #endif
+#ifndef MGDP_WAVE2_PK  // A/B builds: 1 = fused_wave2_xyd's multiplies and |dV| differences as packed fp32 pairs
+#define MGDP_WAVE2_PK 0
+#endif
 #ifndef MGDP_WAVE2_DVTREE  // A/B builds: 1 = fused_wave2_xyd folds |dV| as a v_max3 tree
 #define MGDP_WAVE2_DVTREE 0   // measured neutral (profiles/r05_tree/) and +9 VGPRs at P = 2, 4 (81 -> 90: 6 -> 5 waves)
 #endif
@@ -1280,8 +1283,18 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
             const T m02 = vmax(in[j][0], in[j][2]), m13 = vmax(in[j][1], in[j][3]);
             const T m[4] = {vmax(vmax(in[j][0], m13), FE), vmax(vmax(in[j][1], m02), FS[j]),
                             vmax(vmax(in[j][2], m13), FW), vmax(vmax(in[j][3], m02), FN[j])};
+            if constexpr (MGDP_WAVE2_PK && sizeof(T) == 4) {  // two packed multiplies (v_pk_mul_f32)
+                typedef float f2 __attribute__((ext_vector_type(2)));
+                const f2 g2 = {ge[j], ge[j]};
+                const f2 a = f2{m[0], m[1]} * g2, b = f2{m[2], m[3]} * g2;
+                o[j][0] = a.x;
+                o[j][1] = a.y;
+                o[j][2] = b.x;
+                o[j][3] = b.y;
+            } else {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) o[j][q] = ge[j] * m[q];
+                for (int q = 0; q < 4; ++q) o[j][q] = ge[j] * m[q];
+            }
         }
 #pragma unroll
         for (int j = 0; j < P; ++j) {
@@ -1306,6 +1319,15 @@ __device__ __forceinline__ void fused_wave2_xyd(const Geo &geo, const Coef<T> &c
 #pragma unroll
                     for (int q = 0; q < 4; ++q) ad[4 * j + q] = vabs(o[j][q] - in[j][q]);
                 dm = tree_max3<4 * P, T>(ad);
+            } else if constexpr (MGDP_WAVE2_PK && sizeof(T) == 4) {  // packed differences (v_pk_add_f32)
+                typedef float f2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+                for (int j = 0; j < P; ++j) {
+                    const f2 a = f2{o[j][0], o[j][1]} - f2{in[j][0], in[j][1]};
+                    const f2 b = f2{o[j][2], o[j][3]} - f2{in[j][2], in[j][3]};
+                    dm = vmax(vmax(dm, vabs(a.x)), vabs(a.y));
+                    dm = vmax(vmax(dm, vabs(b.x)), vabs(b.y));
+                }
             } else {
 #pragma unroll
                 for (int j = 0; j < P; ++j)
