@@ -1188,7 +1188,7 @@ FRESH_SETS = 3  # fresh grid sets per BASELINE-config block: first-solve timing 
 FRESH_SETS = int(os.environ.get("MGDP_BENCH_FRESH", FRESH_SETS))
 # steady-state priming of a resident lone-grid server (measure(): the stated criterion)
 PRIME_MIN_S, PRIME_WIN, PRIME_TOL, PRIME_MAX_S, PRIME_RELAUNCH = 0.2, 512, 0.02, 1.0, 16
-PRIME_BLOCK_S = 0.1  # warmup time of each BASELINE-config block (round 6)
+PRIME_BLOCK_S = 0.03  # warmup time of each BASELINE-config block (round 6)
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9  # MI355X_MICROARCH.md: 4 SIMD-32 per CU, one wave64 VALU op per 2 cycles
 
 
